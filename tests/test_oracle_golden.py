@@ -1,0 +1,102 @@
+"""Pin the oracle (oracle/ref_cpu.py, oracle/vtrace.py) against fixtures produced by the
+reference's own code (tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu, vtrace as ovt
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def test_param_layout_matches_reference_state_dict():
+    d = _load("model_forward.npz")
+    keys = [str(k) for k in d["keys"]]
+    assert keys == [k for k, _ in ref_cpu.PARAM_SPECS]
+    m = ref_cpu.RefModel()
+    assert [k for k in m.state_dict().keys()] == keys
+    assert sum(int(np.prod(s)) for _, s in ref_cpu.PARAM_SPECS) == 344496 == d["params"].size
+
+
+def test_forward_matches_reference():
+    d = _load("model_forward.npz")
+    m = ref_cpu.RefModel()
+    ref_cpu.load_flat(m, d["params"])
+    lg, v = ref_cpu.forward_numpy(m, d["obs"])
+    np.testing.assert_allclose(lg, d["logits"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(v, d["values"], rtol=1e-6, atol=1e-6)
+
+
+def test_seed0_init_matches_reference():
+    d = _load("model_forward.npz")
+    m = ref_cpu.make_model(0)
+    np.testing.assert_array_equal(ref_cpu.flat_params(m), d["params"])
+
+
+def test_train_steps_match_reference():
+    d = _load("train_step.npz")
+    m = ref_cpu.RefModel()
+    ref_cpu.load_flat(m, d["params0"])
+    opt = ref_cpu.make_optimizer(m)
+    names = ("loss", "entropy", "td", "pg", "kl", "ratio", "grad_norm")
+    for i in range(3):
+        batch = ref_cpu.to_trajectories(d[f"obs{i}"], d[f"act{i}"], d[f"rew{i}"],
+                                        d[f"disc{i}"], d[f"mu{i}"])
+        met = ref_cpu.train_step(m, opt, batch)
+        got = np.array([float(met["train/" + k]) for k in names])
+        exp = np.array([d[k][i] for k in names])
+        np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-6)
+        if i == 0:
+            np.testing.assert_allclose(ref_cpu.flat_grads(m), d["grads1"], rtol=1e-5, atol=1e-8)
+            np.testing.assert_allclose(ref_cpu.flat_params(m), d["params1"], rtol=0, atol=1e-7)
+    np.testing.assert_allclose(ref_cpu.flat_params(m), d["params3"], rtol=0, atol=1e-7)
+
+
+def test_head_loss_matches_reference():
+    d = _load("head_loss.npz")
+    out = ref_cpu.loss_from_outputs(d["logits"], d["values"], d["act"], d["rew"], d["disc"],
+                                    d["mu"])
+    for k in ("adv", "err", "q", "rho", "dlogits", "dvalues"):
+        np.testing.assert_allclose(out[k], d[k], rtol=1e-5, atol=1e-7, err_msg=k)
+    got = [out[k] for k in ("loss", "entropy", "td", "pg", "kl", "ratio")]
+    np.testing.assert_allclose(got, d["scalars"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("tag,lam", [("l100", 1.0), ("l095", 0.95)])
+def test_vtrace_golden(tag, lam):
+    d = _load("vtrace_random.npz")
+    adv, err, q = ovt.vtrace_numpy(d["v_tm1"].astype(np.float64), d["v_t"], d["r"], d["g"],
+                                   d["rho"], lambda_=lam)
+    np.testing.assert_allclose(adv, d[f"adv_{tag}"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(err, d[f"err_{tag}"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(q, d[f"q_{tag}"], rtol=1e-5, atol=1e-6)
+
+
+def test_vtrace_known_answers():
+    rng = np.random.default_rng(3)
+    B, L = 5, 12
+    v_tm1 = rng.standard_normal((B, L))
+    v_t = rng.standard_normal((B, L))
+    r = rng.standard_normal((B, L))
+    g = np.full((B, L), 0.9)
+    # rho == 1, lambda == 1  =>  err_t = n-step return to the end minus v_tm1
+    # (telescoping needs v_t[k] == v_tm1[k+1], as in the learner: values[:, 1:])
+    v_t2 = np.concatenate([v_tm1[:, 1:], rng.standard_normal((B, 1))], axis=1)
+    adv, err, q = ovt.vtrace_numpy(v_tm1, v_t2, r, g, np.ones((B, L)))
+    for t in range(L):
+        ret = sum((0.9 ** (k - t)) * r[:, k] for k in range(t, L)) + 0.9 ** (L - t) * v_t2[:, L - 1]
+        np.testing.assert_allclose(err[:, t], ret - v_tm1[:, t], rtol=1e-10, atol=1e-10)
+    # discount == 0  =>  err = r - v_tm1 (rho<=1), adv == err
+    rho = rng.uniform(0.2, 1.0, (B, L))
+    adv, err, q = ovt.vtrace_numpy(v_tm1, v_t, r, np.zeros((B, L)), rho)
+    np.testing.assert_allclose(err, rho * (r - v_tm1), atol=1e-12)
+    np.testing.assert_allclose(adv, rho * (r - v_tm1), atol=1e-12)
+    # rho == 0  =>  err == 0 and adv == 0
+    adv, err, q = ovt.vtrace_numpy(v_tm1, v_t, r, g, np.zeros((B, L)))
+    assert np.all(err == 0) and np.all(adv == 0)
