@@ -1,0 +1,118 @@
+"""ctypes binding of ``libimpala_hip.so`` (C-ABI declared in ``include/impala_hip.h``).
+
+The shared library is built in-tree (``python -m impala_amd.build`` or
+``__graft_entry__.build()``) and loaded from ``impala_amd/libimpala_hip.so``.  There is no
+fallback: if the library is missing every compute entry point raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("IMPALA_HIP_LIB", os.path.join(_HERE, "libimpala_hip.so"))
+
+IMPALA_DTYPE_F32 = 0
+IMPALA_DTYPE_BF16 = 1
+NUM_METRICS = 8
+METRIC_NAMES = ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl",
+                "train/ratio", "train/grad_norm")
+
+# every symbol declared in include/impala_hip.h
+EXPORTS = (
+    "impala_abi_version", "impala_last_error", "impala_config_default", "impala_param_count",
+    "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
+    "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
+    "impala_apply_update", "impala_vtrace", "impala_loss_head",
+)
+
+
+class ImpalaConfig(C.Structure):
+    _fields_ = [
+        ("batch_size", C.c_int), ("rollout_length", C.c_int), ("num_actions", C.c_int),
+        ("dtype", C.c_int), ("lr", C.c_float), ("adam_beta1", C.c_float),
+        ("adam_beta2", C.c_float), ("adam_eps", C.c_float), ("max_grad_norm", C.c_float),
+        ("entropy_coeff", C.c_float), ("vtrace_lambda", C.c_float),
+        ("clip_rho_threshold", C.c_float), ("clip_pg_rho_threshold", C.c_float),
+        ("world_size", C.c_int),
+    ]
+
+
+class ImpalaBatch(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("actions", C.c_void_p), ("rewards", C.c_void_p),
+                ("discounts", C.c_void_p), ("behaviour_logits", C.c_void_p)]
+
+
+_lib = None
+_lock = threading.Lock()
+_P = C.c_void_p
+
+
+def _declare(lib):
+    lib.impala_abi_version.restype = C.c_int
+    lib.impala_last_error.restype = C.c_char_p
+    lib.impala_config_default.argtypes = [C.POINTER(ImpalaConfig)]
+    lib.impala_param_count.argtypes = [C.c_int]
+    lib.impala_param_count.restype = C.c_size_t
+    lib.impala_create.argtypes = [C.POINTER(ImpalaConfig), C.c_int, C.POINTER(_P)]
+    lib.impala_destroy.argtypes = [_P]
+    lib.impala_bind_state.argtypes = [_P, _P, _P, _P, _P, _P, _P]
+    lib.impala_refresh_weights.argtypes = [_P, _P]
+    lib.impala_set_step.argtypes = [_P, C.c_int64, _P]
+    lib.impala_forward.argtypes = [_P, _P, C.c_int, _P, _P, _P]
+    lib.impala_train_step.argtypes = [_P, C.POINTER(ImpalaBatch), _P]
+    lib.impala_compute_grads.argtypes = [_P, C.POINTER(ImpalaBatch), _P]
+    lib.impala_apply_update.argtypes = [_P, _P]
+    lib.impala_vtrace.argtypes = [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_float, C.c_float,
+                                  C.c_float, _P, _P, _P, _P]
+    lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
+                                     C.c_float, C.c_float, C.c_float, C.c_float, _P, _P, _P,
+                                     _P, _P, _P, _P, _P]
+    for name in EXPORTS:
+        if name not in ("impala_last_error", "impala_param_count"):
+            getattr(lib, name).restype = C.c_int
+
+
+def lib():
+    """Load (once) and return the HIP library; raise if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"HIP extension not built: {LIB_PATH} is missing "
+                    "(run `python -m impala_amd.build`); there is no CPU fallback")
+            handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+            _declare(handle)
+            _lib = handle
+        return _lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib().impala_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what or 'impala'} failed (status {status}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device/host pointer of a torch tensor (0 for None)."""
+    return 0 if t is None else int(t.data_ptr())
+
+
+def stream_ptr(stream) -> int:
+    """hipStream_t of a torch.cuda.Stream (torch's current stream when None)."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
+
+
+def param_count(num_actions: int = 15) -> int:
+    return int(lib().impala_param_count(num_actions))
+
+
+def default_config() -> ImpalaConfig:
+    cfg = ImpalaConfig()
+    check(lib().impala_config_default(C.byref(cfg)), "impala_config_default")
+    return cfg

@@ -1,0 +1,48 @@
+"""Build the HIP extension in-tree: ``python -m impala_amd.build``.
+
+Compiles ``impala_amd/csrc/impala.hip`` for gfx950 into ``impala_amd/libimpala_hip.so`` with
+hipcc (cross-compiles without a GPU).  The .so is git-ignored and travels with the tree.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC_DIR = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libimpala_hip.so")
+ARCH = os.environ.get("IMPALA_OFFLOAD_ARCH", "gfx950")
+
+
+def sources():
+    return sorted(os.path.join(SRC_DIR, f) for f in os.listdir(SRC_DIR)
+                  if f.endswith((".hip", ".h")))
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = sources() + [os.path.join(os.path.dirname(HERE), "include", "impala_hip.h")]
+    return any(os.path.getmtime(s) > t for s in deps if os.path.exists(s))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return OUT
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    tmp = OUT + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-o", tmp, os.path.join(SRC_DIR, "impala.hip")]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print("built", OUT)

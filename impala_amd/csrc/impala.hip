@@ -1,0 +1,538 @@
+// libimpala_hip.so — C-ABI of the MI355X-native IMPALA learner (see include/impala_hip.h).
+//
+// One handle = one learner replica on one device.  The handle owns the activation, gradient
+// slab and kernel-layout weight workspaces (hipMalloc'd once at create, sized for B*T
+// frames); the caller owns the canonical parameters, gradients, Adam moments and the metrics
+// buffer (bound with impala_bind_state), so the Python host exposes them as ordinary torch
+// tensors (state_dict, checkpoint, RCCL all-reduce) without copies.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/impala_hip.h"
+#include "kernels.h"
+#include "ops.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail((int)e_, std::string(#x) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+#define CK_LAUNCH(name)                                                                \
+  do {                                                                                 \
+    hipError_t e_ = hipGetLastError();                                                 \
+    if (e_ != hipSuccess)                                                              \
+      return fail((int)e_, std::string("launch ") + name + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+inline int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+// recover the decimal constant a float config value was written as (0.9f -> 0.9)
+inline double dec(float x) {
+  if (x == 0.f) return 0.0;
+  const double e = std::floor(std::log10(std::fabs((double)x)));
+  const double s = std::pow(10.0, 7.0 - e);
+  return std::round((double)x * s) / s;
+}
+
+struct Split {
+  int S = 1, mps = 32;  // splits, m per split
+};
+Split plan_split(long M, int tiles, int target_wgs) {
+  Split s;
+  const long chunks = (M + 31) / 32;
+  long S = (target_wgs + tiles - 1) / tiles;
+  if (S < 1) S = 1;
+  if (S > chunks) S = chunks;
+  long mps = ((M + S - 1) / S + 31) / 32 * 32;
+  s.mps = (int)mps;
+  s.S = (int)((M + mps - 1) / mps);
+  return s;
+}
+
+}  // namespace
+
+struct impala_learner {
+  impala_config cfg;
+  int device = 0;
+  int N = 0;  // frames per step = B * T
+  int A = 15;
+  bool bf16 = false;
+  net::Canon cn;
+  net::Shadow sh;
+  // caller-owned (bound)
+  float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr,
+        *metrics = nullptr;
+  // library-owned
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* shadow = nullptr;
+  float* vecs = nullptr;
+  void *act1, *act2, *act3, *y, *h, *dH, *dz, *dact3, *dact2, *dact1;
+  float *lnstat, *z, *heads, *dy;
+  float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
+  float *loss_part, *sumsq_part;
+  int64_t* step;
+  Split sp1, sp2, sp3, spfc, sph;
+  int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0;
+};
+
+namespace {
+
+template <typename T>
+int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st) {
+  using namespace net;
+  const T* sw = reinterpret_cast<const T*>(h->shadow);
+  const Shadow& sh = h->sh;
+  const float* vv = h->vecs;
+  {
+    Conv1Fwd<T> op{n * P1, sw + sh.w1, vv + Vecs::b1, obs, (T*)h->act1};
+    gemm_rc<T, 2, 2><<<dim3(cdiv((long)n * P1, 128), 1), 256, 0, st>>>(op);
+    CK_LAUNCH("conv1_fwd");
+  }
+  {
+    Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
+    gemm_rc<T, 4, 1><<<dim3(cdiv((long)n * P2, 64), 1), 256, 0, st>>>(op);
+    CK_LAUNCH("conv2_fwd");
+  }
+  {
+    Conv3Fwd<T> op{n * P3, sw + sh.w3, vv + Vecs::b3, (const T*)h->act2, (T*)h->act3};
+    gemm_rc<T, 4, 1><<<dim3(cdiv((long)n * P3, 64), 1), 256, 0, st>>>(op);
+    CK_LAUNCH("conv3_fwd");
+  }
+  ln_fwd_kernel<T><<<cdiv(n, 4), 256, 0, st>>>((const T*)h->act3, vv + Vecs::lng, vv + Vecs::lnb,
+                                               (T*)h->y, h->lnstat, n);
+  CK_LAUNCH("ln_fwd");
+  {
+    FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
+    gemm_rc<T, 4, 1><<<dim3(cdiv(n, 64), HID / 64), 256, 0, st>>>(op);
+    CK_LAUNCH("fc_fwd");
+  }
+  {
+    HeadsFwd<T> op{n, sw + sh.wh, vv + Vecs::bh, (const T*)h->h, h->heads};
+    gemm_rc<T, 1, 1><<<dim3(cdiv(n, 64), 1), 256, 0, st>>>(op);
+    CK_LAUNCH("heads_fwd");
+  }
+  return 0;
+}
+
+template <typename T>
+int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
+  using namespace net;
+  const int N = h->N, B = h->cfg.batch_size, Tl = h->cfg.rollout_length;
+  const T* sw = reinterpret_cast<const T*>(h->shadow);
+  const Shadow& sh = h->sh;
+  // ---- loss head: log-softmax, ratio, V-trace, losses, d/dlogits, d/dvalue ----
+  {
+    LossArgs la{};
+    la.logits = h->heads; la.lg_ld = HEADS;
+    la.values = h->heads + VCOL; la.v_ld = HEADS;
+    la.act = b->actions; la.rew = b->rewards; la.disc = b->discounts;
+    la.mu = b->behaviour_logits;
+    la.B = B; la.T = Tl; la.A = h->A; la.S = h->S_seg;
+    la.lam = h->cfg.vtrace_lambda; la.crho = h->cfg.clip_rho_threshold;
+    la.cpg = h->cfg.clip_pg_rho_threshold; la.ent_coef = h->cfg.entropy_coeff;
+    la.partials = h->loss_part;
+    T* dH = (T*)h->dH;
+    loss_head_kernel<T><<<h->n_loss_wg, 256, 0, st>>>(la, dH, HPAD, dH + VCOL, HPAD, VCOL);
+    CK_LAUNCH("loss_head");
+  }
+  {
+    HeadsDgrad<T> op{N, sw + sh.wht, (const T*)h->dH, h->z, (T*)h->dz};
+    gemm_rc<T, 4, 1><<<dim3(cdiv(N, 64), HID / 64), 256, 0, st>>>(op);
+    CK_LAUNCH("heads_dgrad");
+  }
+  {
+    FcDgrad<T> op{N, sw + sh.wfct, (const T*)h->dz, h->dy};
+    gemm_rc<T, 4, 1><<<dim3(cdiv(N, 64), FLAT / 64), 256, 0, st>>>(op);
+    CK_LAUNCH("fc_dgrad");
+  }
+  ln_bwd_kernel<T><<<h->n_ln_wg, 256, 0, st>>>(h->dy, (const T*)h->act3, h->lnstat,
+                                                h->vecs + Vecs::lng, (T*)h->dact3, h->s_ln, N,
+                                                h->ln_fpw);
+  CK_LAUNCH("ln_bwd");
+  {
+    Conv3Dgrad<T> op{N * P2, sw + sh.w3t, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
+    gemm_rc<T, 4, 1><<<dim3(cdiv((long)N * P2, 64), 1), 256, 0, st>>>(op);
+    CK_LAUNCH("conv3_dgrad");
+  }
+  {
+    Conv2Dgrad<T> op{4 * N * 64, N * 64, sw + sh.w2t, (const T*)h->dact2, (const T*)h->act1,
+                     (T*)h->dact1};
+    gemm_rc<T, 2, 1><<<dim3(4 * N, 1), 256, 0, st>>>(op);
+    CK_LAUNCH("conv2_dgrad");
+  }
+  // ---- weight gradients (split-M partial slabs) ----
+  {
+    HeadsWgrad<T> op{};
+    op.M = N; op.dH = (const T*)h->dH; op.h = (const T*)h->h;
+    gemm_wg<T, 16, 64, 1, 4><<<dim3(HID / 64, 1, h->sph.S), 256, 0, st>>>(op, h->s_h, h->s_bh,
+                                                                          h->sph.mps);
+    CK_LAUNCH("heads_wgrad");
+  }
+  {
+    FcWgrad<T> op{};
+    op.M = N; op.dz = (const T*)h->dz; op.y = (const T*)h->y;
+    gemm_wg<T, 64, 64, 2, 2><<<dim3(FLAT / 64, HID / 64, h->spfc.S), 256, 0, st>>>(
+        op, h->s_fc, h->s_bfc, h->spfc.mps);
+    CK_LAUNCH("fc_wgrad");
+  }
+  {
+    Conv3Wgrad<T> op{};
+    op.M = N * P3; op.dy = (const T*)h->dact3; op.x = (const T*)h->act2;
+    gemm_wg<T, 64, 64, 2, 2><<<dim3(K3 / 64, 1, h->sp3.S), 256, 0, st>>>(op, h->s_w3, h->s_b3,
+                                                                         h->sp3.mps);
+    CK_LAUNCH("conv3_wgrad");
+  }
+  {
+    Conv2Wgrad<T> op{};
+    op.M = N * P2; op.dy = (const T*)h->dact2; op.x = (const T*)h->act1;
+    gemm_wg<T, 64, 64, 2, 2><<<dim3(K2 / 64, 1, h->sp2.S), 256, 0, st>>>(op, h->s_w2, h->s_b2,
+                                                                         h->sp2.mps);
+    CK_LAUNCH("conv2_wgrad");
+  }
+  {
+    Conv1Wgrad<T> op{};
+    op.M = N * P1; op.dy = (const T*)h->dact1; op.x = b->obs;
+    gemm_wg<T, 32, 64, 2, 2><<<dim3(K1 / 64, 1, h->sp1.S), 256, 0, st>>>(op, h->s_w1, h->s_b1,
+                                                                         h->sp1.mps);
+    CK_LAUNCH("conv1_wgrad");
+  }
+  // ---- slab reduction -> canonical grads, sum of squares, loss metrics, step += 1 ----
+  {
+    RedArgs ra{};
+    ra.grads = h->grads; ra.cn = h->cn;
+    ra.s_w1 = h->s_w1; ra.s_b1 = h->s_b1; ra.s_w2 = h->s_w2; ra.s_b2 = h->s_b2;
+    ra.s_w3 = h->s_w3; ra.s_b3 = h->s_b3; ra.s_ln = h->s_ln; ra.s_fc = h->s_fc;
+    ra.s_bfc = h->s_bfc; ra.s_h = h->s_h; ra.s_bh = h->s_bh;
+    ra.S1 = h->sp1.S; ra.S2 = h->sp2.S; ra.S3 = h->sp3.S; ra.Sln = h->n_ln_wg;
+    ra.Sfc = h->spfc.S; ra.Sh = h->sph.S;
+    ra.sumsq_part = h->sumsq_part; ra.loss_part = h->loss_part; ra.n_loss_part = h->n_loss_wg;
+    ra.B = B; ra.T = Tl; ra.ent_coef = h->cfg.entropy_coeff; ra.metrics = h->metrics;
+    ra.step = h->step;
+    reduce_grads_kernel<<<h->n_red_wg, 256, 0, st>>>(ra);
+    CK_LAUNCH("reduce_grads");
+  }
+  return 0;
+}
+
+template <typename T>
+int launch_adam(impala_learner* h, hipStream_t st) {
+  AdamArgs aa{};
+  aa.params = h->params; aa.grads = h->grads; aa.m = h->exp_avg; aa.v = h->exp_avg_sq;
+  aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_red_wg;
+  aa.step = h->step;
+  aa.lr = dec(h->cfg.lr); aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
+  aa.eps = h->cfg.adam_eps; aa.max_norm = h->cfg.max_grad_norm;
+  aa.inv_world = 1.f / (float)h->cfg.world_size;
+  aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
+  aa.cn = h->cn; aa.sh = h->sh;
+  adam_kernel<T><<<h->n_red_wg, 256, 0, st>>>(aa);
+  CK_LAUNCH("adam");
+  return 0;
+}
+
+template <typename T>
+int launch_pack(impala_learner* h, hipStream_t st) {
+  pack_params_kernel<T><<<h->n_red_wg, 256, 0, st>>>(h->params, ShadowPtrs{h->shadow, h->vecs, h->A},
+                                                     h->cn, h->sh);
+  CK_LAUNCH("pack_params");
+  return 0;
+}
+
+int check_bound(impala_learner* h, bool train = true) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (!h->params) return fail(IMPALA_E_STATE, "impala_bind_state() not called");
+  if (train && (!h->grads || !h->exp_avg || !h->exp_avg_sq || !h->metrics))
+    return fail(IMPALA_E_STATE, "training needs grads, exp_avg, exp_avg_sq and metrics bound");
+  return 0;
+}
+
+int check_batch(const impala_batch* b) {
+  if (!b || !b->obs || !b->actions || !b->rewards || !b->discounts || !b->behaviour_logits)
+    return fail(IMPALA_E_INVALID, "null batch pointer");
+  if (((uintptr_t)b->obs & 15) != 0) return fail(IMPALA_E_INVALID, "obs must be 16-byte aligned");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int impala_abi_version(void) { return IMPALA_ABI_VERSION; }
+const char* impala_last_error(void) { return g_err.c_str(); }
+
+int impala_config_default(impala_config* c) {
+  if (!c) return fail(IMPALA_E_INVALID, "null cfg");
+  c->batch_size = 8;
+  c->rollout_length = 20;
+  c->num_actions = 15;
+  c->dtype = IMPALA_DTYPE_F32;
+  c->lr = 1e-4f;
+  c->adam_beta1 = 0.9f;
+  c->adam_beta2 = 0.999f;
+  c->adam_eps = 1e-5f;
+  c->max_grad_norm = 0.5f;
+  c->entropy_coeff = 0.01f;
+  c->vtrace_lambda = 1.f;
+  c->clip_rho_threshold = 1.f;
+  c->clip_pg_rho_threshold = 1.f;
+  c->world_size = 1;
+  return 0;
+}
+
+size_t impala_param_count(int num_actions) { return net::canon(num_actions).total; }
+
+int impala_create(const impala_config* cfg, int device, impala_learner** out) {
+  using namespace net;
+  if (!cfg || !out) return fail(IMPALA_E_INVALID, "null argument");
+  *out = nullptr;
+  if (cfg->batch_size < 1) return fail(IMPALA_E_INVALID, "batch_size must be >= 1");
+  if (cfg->rollout_length < 2 || cfg->rollout_length > 64)
+    return fail(IMPALA_E_UNSUPPORTED, "rollout_length must be in [2, 64]");
+  if (cfg->num_actions < 1 || cfg->num_actions > MAX_A)
+    return fail(IMPALA_E_UNSUPPORTED, "num_actions must be in [1, 15]");
+  if (cfg->dtype != IMPALA_DTYPE_F32 && cfg->dtype != IMPALA_DTYPE_BF16)
+    return fail(IMPALA_E_INVALID, "unknown dtype");
+  if (cfg->world_size < 1) return fail(IMPALA_E_INVALID, "world_size must be >= 1");
+  CK(hipSetDevice(device));
+  impala_learner* h = new (std::nothrow) impala_learner();
+  if (!h) return fail(IMPALA_E_INVALID, "out of host memory");
+  h->cfg = *cfg;
+  h->device = device;
+  h->A = cfg->num_actions;
+  h->bf16 = cfg->dtype == IMPALA_DTYPE_BF16;
+  h->N = cfg->batch_size * cfg->rollout_length;
+  h->cn = canon(h->A);
+  h->sh = shadow();
+  const int N = h->N;
+  const size_t es = h->bf16 ? 2 : 4;
+  h->S_seg = next_pow2(cfg->rollout_length);
+  h->n_loss_wg = cdiv(cfg->batch_size, 4 * (64 / h->S_seg));
+  h->n_ln_wg = cdiv(N, 4 * h->ln_fpw);
+  h->n_red_wg = cdiv((long)h->cn.total, 256);
+  h->sph = plan_split(N, HID / 64, 128);
+  h->spfc = plan_split(N, (FLAT / 64) * (HID / 64), 256);
+  h->sp3 = plan_split((long)N * P3, K3 / 64, 512);
+  h->sp2 = plan_split((long)N * P2, K2 / 64, 512);
+  h->sp1 = plan_split((long)N * P1, K1 / 64, 768);
+
+  // ---- one workspace allocation, 256-byte aligned carve ----
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_shadow = take(h->sh.total * es);
+  const size_t o_vecs = take(Vecs::total * 4);
+  const size_t o_act1 = take((size_t)N * P1 * OC1 * es);
+  const size_t o_act2 = take((size_t)N * P2 * OC2 * es);
+  const size_t o_act3 = take((size_t)N * FLAT * es);
+  const size_t o_y = take((size_t)N * FLAT * es);
+  const size_t o_h = take((size_t)N * HID * es);
+  const size_t o_dH = take((size_t)N * HPAD * es);
+  const size_t o_dz = take((size_t)N * HID * es);
+  const size_t o_dact3 = take((size_t)N * FLAT * es);
+  const size_t o_dact2 = take((size_t)N * P2 * OC2 * es);
+  const size_t o_dact1 = take((size_t)N * P1 * OC1 * es);
+  const size_t o_lnstat = take((size_t)N * 2 * 4);
+  const size_t o_z = take((size_t)N * HID * 4);
+  const size_t o_heads = take((size_t)N * HEADS * 4);
+  const size_t o_dy = take((size_t)N * FLAT * 4);
+  const size_t o_sw1 = take((size_t)h->sp1.S * OC1 * K1 * 4);
+  const size_t o_sb1 = take((size_t)h->sp1.S * OC1 * 4);
+  const size_t o_sw2 = take((size_t)h->sp2.S * OC2 * K2 * 4);
+  const size_t o_sb2 = take((size_t)h->sp2.S * OC2 * 4);
+  const size_t o_sw3 = take((size_t)h->sp3.S * OC3 * K3 * 4);
+  const size_t o_sb3 = take((size_t)h->sp3.S * OC3 * 4);
+  const size_t o_sln = take((size_t)h->n_ln_wg * 2 * FLAT * 4);
+  const size_t o_sfc = take((size_t)h->spfc.S * HID * FLAT * 4);
+  const size_t o_sbfc = take((size_t)h->spfc.S * HID * 4);
+  const size_t o_sh = take((size_t)h->sph.S * HEADS * HID * 4);
+  const size_t o_sbh = take((size_t)h->sph.S * HEADS * 4);
+  const size_t o_lpart = take((size_t)h->n_loss_wg * 8 * 4);
+  const size_t o_spart = take((size_t)h->n_red_wg * 4);
+  const size_t o_step = take(8);
+  h->ws_bytes = off;
+  hipError_t e = hipMalloc(&h->ws, off);
+  if (e != hipSuccess) {
+    delete h;
+    return fail((int)e, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
+  }
+  e = hipMemset(h->ws, 0, off);
+  if (e != hipSuccess) {
+    (void)hipFree(h->ws);
+    delete h;
+    return fail((int)e, std::string("hipMemset workspace: ") + hipGetErrorString(e));
+  }
+  char* w = h->ws;
+  h->shadow = w + o_shadow;
+  h->vecs = (float*)(w + o_vecs);
+  h->act1 = w + o_act1; h->act2 = w + o_act2; h->act3 = w + o_act3; h->y = w + o_y;
+  h->h = w + o_h; h->dH = w + o_dH; h->dz = w + o_dz; h->dact3 = w + o_dact3;
+  h->dact2 = w + o_dact2; h->dact1 = w + o_dact1;
+  h->lnstat = (float*)(w + o_lnstat); h->z = (float*)(w + o_z); h->heads = (float*)(w + o_heads);
+  h->dy = (float*)(w + o_dy);
+  h->s_w1 = (float*)(w + o_sw1); h->s_b1 = (float*)(w + o_sb1);
+  h->s_w2 = (float*)(w + o_sw2); h->s_b2 = (float*)(w + o_sb2);
+  h->s_w3 = (float*)(w + o_sw3); h->s_b3 = (float*)(w + o_sb3);
+  h->s_ln = (float*)(w + o_sln); h->s_fc = (float*)(w + o_sfc); h->s_bfc = (float*)(w + o_sbfc);
+  h->s_h = (float*)(w + o_sh); h->s_bh = (float*)(w + o_sbh);
+  h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
+  h->step = (int64_t*)(w + o_step);
+  *out = h;
+  return 0;
+}
+
+int impala_destroy(impala_learner* h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  if (h->ws) (void)hipFree(h->ws);
+  delete h;
+  return 0;
+}
+
+int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp_avg,
+                      float* exp_avg_sq, float* metrics, void* stream) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (!params) return fail(IMPALA_E_INVALID, "null params pointer");
+  h->params = params; h->grads = grads; h->exp_avg = exp_avg; h->exp_avg_sq = exp_avg_sq;
+  h->metrics = metrics;
+  return impala_refresh_weights(h, stream);
+}
+
+int impala_refresh_weights(impala_learner* h, void* stream) {
+  if (int r = check_bound(h, false)) return r;
+  CK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  return h->bf16 ? launch_pack<__bf16>(h, st) : launch_pack<float>(h, st);
+}
+
+int impala_set_step(impala_learner* h, int64_t step, void* stream) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (step < 0) return fail(IMPALA_E_INVALID, "negative step");
+  CK(hipSetDevice(h->device));
+  static thread_local int64_t host_step;
+  host_step = step;
+  CK(hipMemcpyAsync(h->step, &host_step, 8, hipMemcpyHostToDevice, (hipStream_t)stream));
+  CK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, float* values,
+                   void* stream) {
+  if (int r = check_bound(h, false)) return r;
+  if (!obs || !logits || !values) return fail(IMPALA_E_INVALID, "null pointer");
+  if (n < 1 || n > h->N) return fail(IMPALA_E_INVALID, "n must be in [1, B*T]");
+  if (((uintptr_t)obs & 15) != 0) return fail(IMPALA_E_INVALID, "obs must be 16-byte aligned");
+  CK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  int r = h->bf16 ? launch_forward<__bf16>(h, obs, n, st) : launch_forward<float>(h, obs, n, st);
+  if (r) return r;
+  split_heads_kernel<<<cdiv((long)n * net::HEADS, 256), 256, 0, st>>>(h->heads, n, h->A, logits,
+                                                                       values);
+  CK_LAUNCH("split_heads");
+  return 0;
+}
+
+int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream) {
+  if (int r = check_bound(h)) return r;
+  if (int r = check_batch(b)) return r;
+  CK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st)
+                  : launch_forward<float>(h, b->obs, h->N, st);
+  if (r) return r;
+  return h->bf16 ? launch_backward<__bf16>(h, b, st) : launch_backward<float>(h, b, st);
+}
+
+int impala_apply_update(impala_learner* h, void* stream) {
+  if (int r = check_bound(h)) return r;
+  CK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (h->cfg.world_size > 1) {
+    sumsq_kernel<<<h->n_red_wg, 256, 0, st>>>(h->grads, h->cn.total, h->sumsq_part);
+    CK_LAUNCH("sumsq");
+  }
+  return h->bf16 ? launch_adam<__bf16>(h, st) : launch_adam<float>(h, st);
+}
+
+int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (h->cfg.world_size != 1)
+    return fail(IMPALA_E_STATE, "world_size > 1: use compute_grads + all-reduce + apply_update");
+  if (int r = impala_compute_grads(h, b, stream)) return r;
+  return impala_apply_update(h, stream);
+}
+
+int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,
+                  const float* rho_tm1, int B, int L, float lambda_, float clip_rho_threshold,
+                  float clip_pg_rho_threshold, float* pg_advantage, float* td_error,
+                  float* q_estimate, void* stream) {
+  if (B < 1 || L < 1 || L > 64) return fail(IMPALA_E_INVALID, "need B >= 1 and 1 <= L <= 64");
+  if (!v_tm1 || !v_t || !r_t || !discount_t || !rho_tm1 || !pg_advantage || !td_error ||
+      !q_estimate)
+    return fail(IMPALA_E_INVALID, "null pointer");
+  const int S = next_pow2(L);
+  const int wgs = cdiv(B, 4 * (64 / S));
+  vtrace_kernel<<<wgs, 256, 0, (hipStream_t)stream>>>(v_tm1, v_t, r_t, discount_t, rho_tm1, B, L, S,
+                                                      lambda_, clip_rho_threshold,
+                                                      clip_pg_rho_threshold, pg_advantage,
+                                                      td_error, q_estimate);
+  CK_LAUNCH("vtrace");
+  return 0;
+}
+
+int impala_loss_head(const float* logits, const float* values, const int64_t* actions,
+                     const float* rewards, const float* discounts, const float* behaviour_logits,
+                     int B, int T, int A, float entropy_coeff, float lambda_, float clip_rho,
+                     float clip_pg_rho, float* dlogits, float* dvalues, float* metrics6,
+                     float* adv, float* err, float* q, float* rho, void* stream) {
+  if (B < 1 || T < 2 || T > 64 || A < 1 || A > net::MAX_A)
+    return fail(IMPALA_E_INVALID, "need B >= 1, 2 <= T <= 64, 1 <= A <= 15");
+  if (!logits || !values || !actions || !rewards || !discounts || !behaviour_logits || !dlogits ||
+      !dvalues || !metrics6)
+    return fail(IMPALA_E_INVALID, "null pointer");
+  const bool dbg = adv && err && q;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = next_pow2(T);
+  const int wgs = cdiv(B, 4 * (64 / S));
+  float* part = nullptr;
+  CK(hipMallocAsync((void**)&part, (size_t)wgs * 8 * 4, st));
+  LossArgs la{};
+  la.logits = logits; la.lg_ld = A; la.values = values; la.v_ld = 1;
+  la.act = actions; la.rew = rewards; la.disc = discounts; la.mu = behaviour_logits;
+  la.B = B; la.T = T; la.A = A; la.S = S;
+  la.lam = lambda_; la.crho = clip_rho; la.cpg = clip_pg_rho; la.ent_coef = entropy_coeff;
+  la.partials = part;
+  la.dbg_adv = dbg ? adv : nullptr; la.dbg_err = dbg ? err : nullptr; la.dbg_q = dbg ? q : nullptr;
+  la.dbg_rho = rho;
+  loss_head_kernel<float><<<wgs, 256, 0, st>>>(la, dlogits, A, dvalues, 1, 0);
+  CK_LAUNCH("loss_head");
+  finalize_loss_kernel<<<1, 64, 0, st>>>(part, wgs, B, T, entropy_coeff, metrics6);
+  CK_LAUNCH("finalize_loss");
+  CK(hipFreeAsync(part, st));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,534 @@
+// Non-GEMM kernels of the learner step: fused log-softmax / V-trace / loss head, LayerNorm
+// forward and backward, gradient-slab reduction, global-norm clip + Adam, weight repacking.
+#pragma once
+#include "common.h"
+#include "net.h"
+
+using namespace net;
+
+// =========================================================================================
+// V-trace as a segmented reverse linear-recurrence scan across the lanes of a wavefront.
+// Lane t of a segment holds (a_t, b_t) with e_t = b_t + a_t * e_{t+1}, e_L = 0.  Hillis-Steele
+// over __shfl_down: after the step with offset d every lane holds the composition of the maps
+// t .. t+2d-1, so log2(S) shuffle rounds give e_t on every lane (S = segment size <= 64).
+// (rlax/rlego vtrace_td_error_and_advantage; agents/impala/learning.py:15-26,150-153.)
+// =========================================================================================
+DEV float seg_rev_scan(float a, float b, int t, int L, int S) {
+  for (int d = 1; d < S; d <<= 1) {
+    const float a2 = __shfl_down(a, d, 64);
+    const float b2 = __shfl_down(b, d, 64);
+    if (t + d < L) {
+      b = fmaf(a, b2, b);
+      a = a * a2;
+    }
+  }
+  return b;
+}
+
+// Standalone batched V-trace on [B][L] inputs (impala_vtrace).
+__global__ __launch_bounds__(256) void vtrace_kernel(const float* __restrict__ v_tm1,
+                                                     const float* __restrict__ v_t,
+                                                     const float* __restrict__ r_t,
+                                                     const float* __restrict__ g_t,
+                                                     const float* __restrict__ rho_t, int B,
+                                                     int L, int S, float lam, float crho,
+                                                     float cpg, float* __restrict__ adv,
+                                                     float* __restrict__ err,
+                                                     float* __restrict__ q) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int traj = gw * (64 / S) + lane / S;
+  const int t = lane % S;
+  const bool in = traj < B && t < L;
+  const size_t i = (size_t)traj * L + t;
+  const float v = in ? v_tm1[i] : 0.f, vt = in ? v_t[i] : 0.f, r = in ? r_t[i] : 0.f,
+              g = in ? g_t[i] : 0.f, rho = in ? rho_t[i] : 0.f;
+  const float td = in ? fminf(crho, rho) * (r + g * vt - v) : 0.f;
+  const float aa = in ? g * (lam * fminf(1.f, rho)) : 0.f;
+  const float e = seg_rev_scan(aa, td, t, L, S);
+  const float tgt = e + v;
+  const float tgt_n = __shfl_down(tgt, 1, 64), v_n = __shfl_down(v, 1, 64);
+  const float boot = (t < L - 1) ? lam * tgt_n + (1.f - lam) * v_n : vt;
+  const float qq = r + g * boot;
+  if (in) {
+    err[i] = tgt - v;
+    q[i] = qq;
+    adv[i] = fminf(cpg, rho) * (qq - v);
+  }
+}
+
+// =========================================================================================
+// Fused loss head (agents/impala/learning.py:144-170): per (b,t) lane: log-softmax of the
+// policy and behaviour logits, log pi(a), rho, entropy, KL; per trajectory: V-trace scan over
+// T-1 (the last step is dropped from pg/value, kept for entropy/KL/ratio, learning.py:150-157);
+// analytic d loss / d logits and d loss / d value with rlax stop-gradient semantics
+// (targets and advantages are constants):
+//   loss = -mean_{B,T-1}(log pi(a) adv) + mean_{B,T-1}(err^2) - c_ent * mean_{B,T} H(pi)
+//   dlogit_j = c_ent/(BT) pi_j (log pi_j + H)  -  [t<T-1] adv/(B(T-1)) (1[j=a] - pi_j)
+//   dvalue   = -[t<T-1] 2 err/(B(T-1))
+// Per-workgroup partial sums of (log pi(a) adv, err^2, H, KL, rho) go to `partials`.
+// =========================================================================================
+struct LossArgs {
+  const float* logits; int lg_ld;
+  const float* values; int v_ld;
+  const int64_t* act; const float* rew; const float* disc; const float* mu;
+  int B, T, A, S;
+  float lam, crho, cpg, ent_coef;
+  float* partials;  // [gridDim.x][8]
+  float* dbg_adv; float* dbg_err; float* dbg_q; float* dbg_rho;
+};
+
+template <typename TO>
+__global__ __launch_bounds__(256) void loss_head_kernel(const LossArgs a, TO* __restrict__ dl,
+                                                        int dl_ld, TO* __restrict__ dv,
+                                                        int dv_ld, int zero_to) {
+  __shared__ float red[4][5];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + wave;
+  const int S = a.S, T = a.T, A = a.A, L = T - 1;
+  const int traj = gw * (64 / S) + lane / S;
+  const int t = lane % S;
+  const bool valid = traj < a.B && t < T;
+  const bool inL = valid && t < L;
+  const size_t n = (size_t)(valid ? traj : 0) * T + (valid ? t : 0);
+
+  float lg[MAX_A], logp[MAX_A];
+  float H = 0.f, kl = 0.f, logpa = 0.f, rho = 0.f, v = 0.f, r = 0.f, g = 0.f;
+  int act = 0;
+  if (valid) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      lg[j] = j < A ? a.logits[n * a.lg_ld + j] : -INFINITY;
+      m = fmaxf(m, lg[j]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) s += j < A ? expf(lg[j] - m) : 0.f;
+    const float lse = m + logf(s);
+    float mm = -INFINITY, mu[MAX_A];
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      mu[j] = j < A ? a.mu[n * A + j] : -INFINITY;
+      mm = fmaxf(mm, mu[j]);
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) sm += j < A ? expf(mu[j] - mm) : 0.f;
+    const float lse_mu = mm + logf(sm);
+    act = (int)a.act[n];
+    float logmua = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      if (j < A) {
+        logp[j] = lg[j] - lse;
+        const float p = expf(logp[j]);
+        const float lmu = mu[j] - lse_mu;
+        H -= p * logp[j];
+        kl += p * (logp[j] - lmu);
+        if (j == act) { logpa = logp[j]; logmua = lmu; }
+      } else {
+        logp[j] = 0.f;
+      }
+    }
+    rho = expf(logpa - logmua);
+    v = a.values[n * a.v_ld];
+    r = a.rew[n];
+    g = a.disc[n];
+  }
+  // ---- V-trace over the first T-1 steps of each trajectory segment ----
+  const float v_n = __shfl_down(v, 1, 64);  // values[:, 1:]
+  const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
+  const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
+  const float e = seg_rev_scan(aa, td, t, L, S);
+  const float tgt = e + v;
+  const float err = tgt - v;
+  const float tgt_n = __shfl_down(tgt, 1, 64);
+  const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
+  const float qq = r + g * boot;
+  const float adv = fminf(a.cpg, rho) * (qq - v);
+
+  if (valid) {
+    const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T);
+    const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      if (j < A) {
+        const float p = expf(logp[j]);
+        const float d = ke * p * (logp[j] + H) - kp * ((j == act ? 1.f : 0.f) - p);
+        dl[n * dl_ld + j] = (TO)d;
+      } else if (j < zero_to) {
+        dl[n * dl_ld + j] = (TO)0.f;
+      }
+    }
+    dv[n * dv_ld] = (TO)(inL ? -2.f * c_pg * err : 0.f);
+    if (a.dbg_rho) a.dbg_rho[n] = rho;
+    if (inL && a.dbg_adv) {
+      const size_t k = (size_t)traj * L + t;
+      a.dbg_adv[k] = adv;
+      a.dbg_err[k] = err;
+      a.dbg_q[k] = qq;
+    }
+  }
+  float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
+  float s2 = valid ? H : 0.f, s3 = valid ? kl : 0.f, s4 = valid ? rho : 0.f;
+  s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); s3 = wave_sum(s3); s4 = wave_sum(s4);
+  if (lane == 0) {
+    red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = s2; red[wave][3] = s3; red[wave][4] = s4;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    const int k = threadIdx.x;
+    a.partials[blockIdx.x * 8 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+// metrics[0..5] = loss, entropy, td, pg, kl, ratio from the loss-head partial sums
+DEV void finalize_loss_metrics(const float* part, int nparts, int B, int T, float ent_coef,
+                               float* metrics) {
+  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < nparts; ++p)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s[k] += part[p * 8 + k];
+  const float c_pg = 1.f / (float)(B * (T - 1)), c_ent = 1.f / (float)(B * T);
+  const float pg = s[0] * c_pg, td = s[1] * c_pg, ent = s[2] * c_ent;
+  metrics[0] = -pg + td - ent_coef * ent;
+  metrics[1] = ent;
+  metrics[2] = td;
+  metrics[3] = pg;
+  metrics[4] = s[3] * c_ent;
+  metrics[5] = s[4] * c_ent;
+}
+
+__global__ void finalize_loss_kernel(const float* part, int nparts, int B, int T, float ent_coef,
+                                     float* metrics) {
+  if (threadIdx.x == 0) finalize_loss_metrics(part, nparts, B, T, ent_coef, metrics);
+}
+
+// =========================================================================================
+// LayerNorm(1024, eps 1e-5) over the flattened conv features (models/models.py:66), one wave
+// per frame, 16 contiguous features per lane.  Features are in (p*64 + c) order; gamma/beta
+// are stored permuted to match.
+// =========================================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
+                                                     const float* __restrict__ gam,
+                                                     const float* __restrict__ bet,
+                                                     T* __restrict__ y, float* __restrict__ stats,
+                                                     int N) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const T* xr = x + (size_t)n * FLAT + lane * 16;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; i += 4) load4(xr + i, v + i);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.f / FLAT);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) q += (v[i] - mean) * (v[i] - mean);
+  const float var = wave_sum(q) * (1.f / FLAT);
+  const float rstd = 1.f / sqrtf(var + LN_EPS);
+  T* yr = y + (size_t)n * FLAT + lane * 16;
+#pragma unroll
+  for (int i = 0; i < 16; i += 4) {
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = (v[i + k] - mean) * rstd * gam[lane * 16 + i + k] + bet[lane * 16 + i + k];
+    store4(yr + i, o);
+  }
+  if (lane == 0) {
+    stats[2 * n] = mean;
+    stats[2 * n + 1] = rstd;
+  }
+}
+
+// LayerNorm backward + conv3 ReLU mask; per-workgroup partials of d gamma, d beta.
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy,
+                                                     const T* __restrict__ x,
+                                                     const float* __restrict__ stats,
+                                                     const float* __restrict__ gam,
+                                                     T* __restrict__ dx,
+                                                     float* __restrict__ slab, int N, int fpw) {
+  __shared__ float red[4][2][FLAT / 4];  // reused in 4 passes of 256 columns
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dg[16], db[16], gm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    dg[i] = 0.f;
+    db[i] = 0.f;
+    gm[i] = gam[lane * 16 + i];
+  }
+  for (int f = 0; f < fpw; ++f) {
+    const int n = (blockIdx.x * 4 + wave) * fpw + f;
+    if (n >= N) break;
+    const float mean = stats[2 * n], rstd = stats[2 * n + 1];
+    float xv[16], d[16], xh[16];
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      load4(x + (size_t)n * FLAT + lane * 16 + i, xv + i);
+      load4(dy + (size_t)n * FLAT + lane * 16 + i, d + i);
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      xh[i] = (xv[i] - mean) * rstd;
+      const float gd = d[i] * gm[i];
+      s1 += gd;
+      s2 += gd * xh[i];
+      dg[i] += d[i] * xh[i];
+      db[i] += d[i];
+    }
+    s1 = wave_sum(s1) * (1.f / FLAT);
+    s2 = wave_sum(s2) * (1.f / FLAT);
+    float o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float g = rstd * (d[i] * gm[i] - s1 - xh[i] * s2);
+      o[i] = xv[i] > 0.f ? g : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) store4(dx + (size_t)n * FLAT + lane * 16 + i, o + i);
+  }
+  // deterministic cross-wave reduction, 256 columns (16 lanes x 16) per pass
+  for (int pass = 0; pass < 4; ++pass) {
+    if ((lane >> 4) == pass) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        red[wave][0][(lane & 15) * 16 + i] = dg[i];
+        red[wave][1][(lane & 15) * 16 + i] = db[i];
+      }
+    }
+    __syncthreads();
+    const int c = threadIdx.x;  // 0..255
+    const float g = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    const float b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    slab[(size_t)blockIdx.x * 2 * FLAT + pass * 256 + c] = g;
+    slab[(size_t)blockIdx.x * 2 * FLAT + FLAT + pass * 256 + c] = b;
+    __syncthreads();
+  }
+}
+
+// =========================================================================================
+// Shadow-weight emission: canonical (state_dict) index -> kernel layouts (see net.h).
+// =========================================================================================
+struct ShadowPtrs {
+  void* base;   // T elements, layout net::shadow()
+  float* vecs;  // net::Vecs
+  int A;
+};
+
+template <typename T>
+DEV void write_shadow(const ShadowPtrs& sp, const Canon& cn, const Shadow& sh, size_t i, float p) {
+  T* w = reinterpret_cast<T*>(sp.base);
+  float* vv = sp.vecs;
+  const T pt = (T)p;
+  if (i < cn.b1) {
+    w[sh.w1 + i] = pt;
+  } else if (i < cn.w2) {
+    vv[Vecs::b1 + (i - cn.b1)] = p;
+  } else if (i < cn.b2) {
+    const int k = (int)(i - cn.w2), oc = k / K2, rem = k % K2, ci = rem >> 4, kh = (rem >> 2) & 3,
+              kw = rem & 3;
+    w[sh.w2 + oc * K2 + (kh * 4 + kw) * OC1 + ci] = pt;
+    const int cls = (kh & 1) * 2 + (kw & 1), t = (kh >> 1) * 2 + (kw >> 1);
+    w[sh.w2t + ((size_t)(cls * OC1 + ci) * 4 + t) * OC2 + oc] = pt;
+  } else if (i < cn.w3) {
+    vv[Vecs::b2 + (i - cn.b2)] = p;
+  } else if (i < cn.b3) {
+    const int k = (int)(i - cn.w3), oc = k / K3, rem = k % K3, ci = rem / 9, tap = rem % 9;
+    w[sh.w3 + oc * K3 + tap * OC2 + ci] = pt;
+    w[sh.w3t + ci * K3 + tap * OC3 + oc] = pt;
+  } else if (i < cn.lng) {
+    vv[Vecs::b3 + (i - cn.b3)] = p;
+  } else if (i < cn.lnb) {
+    const int j = (int)(i - cn.lng);
+    vv[Vecs::lng + (j & 15) * OC3 + (j >> 4)] = p;
+  } else if (i < cn.wfc) {
+    const int j = (int)(i - cn.lnb);
+    vv[Vecs::lnb + (j & 15) * OC3 + (j >> 4)] = p;
+  } else if (i < cn.bfc) {
+    const int k = (int)(i - cn.wfc), o = k >> 10, j = k & 1023;
+    const int jj = (j & 15) * OC3 + (j >> 4);
+    w[sh.wfc + (size_t)o * FLAT + jj] = pt;
+    w[sh.wfct + (size_t)jj * HID + o] = pt;
+  } else if (i < cn.wa) {
+    vv[Vecs::bfc + (i - cn.bfc)] = p;
+  } else if (i < cn.ba) {
+    const int k = (int)(i - cn.wa), ar = k >> 8, j = k & 255;
+    w[sh.wh + ar * HID + j] = pt;
+    w[sh.wht + j * HPAD + ar] = pt;
+  } else if (i < cn.wc) {
+    vv[Vecs::bh + (i - cn.ba)] = p;
+  } else if (i < cn.bc) {
+    const int j = (int)(i - cn.wc);
+    w[sh.wh + VCOL * HID + j] = pt;
+    w[sh.wht + j * HPAD + VCOL] = pt;
+  } else {
+    vv[Vecs::bh + VCOL] = p;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_params_kernel(const float* __restrict__ params,
+                                                          ShadowPtrs sp, Canon cn, Shadow sh) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < cn.total) write_shadow<T>(sp, cn, sh, i, params[i]);
+}
+
+// =========================================================================================
+// Gradient-slab reduction into the canonical (state_dict) gradient buffer, fixed split order.
+// Also: per-block sum of squares (for the clip norm), loss-metric finalisation and the Adam
+// step counter increment (block 0).
+// =========================================================================================
+struct RedArgs {
+  float* grads;
+  Canon cn;
+  const float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
+  int S1, S2, S3, Sln, Sfc, Sh;
+  float* sumsq_part;
+  const float* loss_part;
+  int n_loss_part, B, T;
+  float ent_coef;
+  float* metrics;
+  int64_t* step;
+};
+
+DEV float sum_splits(const float* s, int S, size_t stride, size_t k) {
+  float acc = 0.f;
+  for (int q = 0; q < S; ++q) acc += s[(size_t)q * stride + k];
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a) {
+  __shared__ float red[4];
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const Canon& cn = a.cn;
+  float g = 0.f;
+  if (i < cn.total) {
+    if (i < cn.b1) {
+      g = sum_splits(a.s_w1, a.S1, (size_t)OC1 * K1, i);
+    } else if (i < cn.w2) {
+      g = sum_splits(a.s_b1, a.S1, OC1, i - cn.b1);
+    } else if (i < cn.b2) {
+      const int k = (int)(i - cn.w2), oc = k / K2, rem = k % K2, ci = rem >> 4,
+                tap = rem & 15;
+      g = sum_splits(a.s_w2, a.S2, (size_t)OC2 * K2, (size_t)oc * K2 + tap * OC1 + ci);
+    } else if (i < cn.w3) {
+      g = sum_splits(a.s_b2, a.S2, OC2, i - cn.b2);
+    } else if (i < cn.b3) {
+      const int k = (int)(i - cn.w3), oc = k / K3, rem = k % K3, ci = rem / 9, tap = rem % 9;
+      g = sum_splits(a.s_w3, a.S3, (size_t)OC3 * K3, (size_t)oc * K3 + tap * OC2 + ci);
+    } else if (i < cn.lng) {
+      g = sum_splits(a.s_b3, a.S3, OC3, i - cn.b3);
+    } else if (i < cn.lnb) {
+      const int j = (int)(i - cn.lng);
+      g = sum_splits(a.s_ln, a.Sln, 2 * FLAT, (j & 15) * OC3 + (j >> 4));
+    } else if (i < cn.wfc) {
+      const int j = (int)(i - cn.lnb);
+      g = sum_splits(a.s_ln, a.Sln, 2 * FLAT, FLAT + (j & 15) * OC3 + (j >> 4));
+    } else if (i < cn.bfc) {
+      const int k = (int)(i - cn.wfc), o = k >> 10, j = k & 1023;
+      g = sum_splits(a.s_fc, a.Sfc, (size_t)HID * FLAT, (size_t)o * FLAT + (j & 15) * OC3 + (j >> 4));
+    } else if (i < cn.wa) {
+      g = sum_splits(a.s_bfc, a.Sfc, HID, i - cn.bfc);
+    } else if (i < cn.ba) {
+      g = sum_splits(a.s_h, a.Sh, (size_t)HEADS * HID, i - cn.wa);
+    } else if (i < cn.wc) {
+      g = sum_splits(a.s_bh, a.Sh, HEADS, i - cn.ba);
+    } else if (i < cn.bc) {
+      g = sum_splits(a.s_h, a.Sh, (size_t)HEADS * HID, VCOL * HID + (i - cn.wc));
+    } else {
+      g = sum_splits(a.s_bh, a.Sh, HEADS, VCOL);
+    }
+    a.grads[i] = g;
+  }
+  float q = wave_sum(g * g);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) a.sumsq_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (blockIdx.x == 0 && threadIdx.x == 64) {
+    finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
+    *a.step += 1;
+  }
+}
+
+// per-block sum of squares of an (all-reduced) gradient buffer
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, size_t n,
+                                                    float* __restrict__ part) {
+  __shared__ float red[4];
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const float v = i < n ? g[i] : 0.f;
+  const float q = wave_sum(v * v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// =========================================================================================
+// clip_grad_norm_(max_norm) + torch.optim.Adam (agents/impala/learning.py:172-176,
+// builder.py:43-44), then re-emission of the kernel-layout weights.  Every block re-sums
+// the sum-of-squares partials itself (deterministic, no grid barrier).
+// =========================================================================================
+struct AdamArgs {
+  float *params, *grads, *m, *v, *metrics;
+  const float* sumsq_part;
+  int n_part;
+  const int64_t* step;
+  double lr, b1, b2;
+  float eps, max_norm, inv_world;
+  ShadowPtrs sp;
+  Canon cn;
+  Shadow sh;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int p = threadIdx.x; p < a.n_part; p += 256) s += a.sumsq_part[p];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float norm = sqrtf(tot) * a.inv_world;
+  const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.f);
+  const double stepd = (double)*a.step;
+  const double bc1 = 1.0 - pow(a.b1, stepd), bc2 = 1.0 - pow(a.b2, stepd);
+  const float step_size = (float)(a.lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < a.cn.total) {
+    const float g = a.grads[i] * a.inv_world * coef;
+    a.grads[i] = g;
+    float m = a.m[i], v = a.v[i];
+    m = m + w1 * (g - m);
+    v = v * b2f + w2 * g * g;
+    const float denom = sqrtf(v) / bc2s + a.eps;
+    const float p = a.params[i] - step_size * (m / denom);
+    a.m[i] = m;
+    a.v[i] = v;
+    a.params[i] = p;
+    write_shadow<T>(a.sp, a.cn, a.sh, i, p);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.metrics[6] = norm;
+    a.metrics[7] = (float)stepd;
+  }
+}
+
+// heads output [n][16] -> logits [n][A], values [n]
+__global__ void split_heads_kernel(const float* __restrict__ heads, int n, int A,
+                                   float* __restrict__ logits, float* __restrict__ values) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * HEADS) return;
+  const int f = i / HEADS, j = i % HEADS;
+  if (j < A) logits[(size_t)f * A + j] = heads[i];
+  else if (j == VCOL) values[f] = heads[i];
+}

@@ -1,0 +1,206 @@
+"""Engine: one HIP learner handle (``impala_learner*``) bound to a model's flat buffers.
+
+Owns the Adam moments and the device metrics vector as torch tensors; the library owns its
+activation / slab / kernel-layout-weight workspace.  All calls are asynchronous on torch's
+current HIP stream (or an explicit one).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from impala_amd import _lib
+from impala_amd._lib import ImpalaBatch, ImpalaConfig, check, ptr, stream_ptr
+
+DTYPES = {"fp32": _lib.IMPALA_DTYPE_F32, "f32": _lib.IMPALA_DTYPE_F32,
+          "float32": _lib.IMPALA_DTYPE_F32, "bf16": _lib.IMPALA_DTYPE_BF16,
+          "bfloat16": _lib.IMPALA_DTYPE_BF16}
+
+
+class Engine:
+    def __init__(self, model, batch_size: int, rollout_length: int = 20, dtype: Optional[str] = None,
+                 lr: float = 1e-4, eps: float = 1e-5, betas: Tuple[float, float] = (0.9, 0.999),
+                 max_grad_norm: float = 0.5, entropy_coeff: float = 0.01, world_size: int = 1,
+                 vtrace_lambda: float = 1.0, clip_rho_threshold: float = 1.0,
+                 clip_pg_rho_threshold: float = 1.0, inference_only: bool = False):
+        if model.flat.device.type != "cuda":
+            raise RuntimeError("the IMPALA learner runs on the HIP path only (cuda device)")
+        self.model = model
+        self.device = model.flat.device
+        self.batch_size = int(batch_size)
+        self.rollout_length = int(rollout_length)
+        self.num_actions = model.action_dim
+        self.inference_only = inference_only
+        dtype = dtype or model.compute_dtype
+        if dtype not in DTYPES:
+            raise ValueError(f"unknown dtype {dtype!r}")
+        self.dtype = dtype
+        L = _lib.lib()
+        cfg = _lib.default_config()
+        cfg.batch_size = self.batch_size
+        cfg.rollout_length = self.rollout_length
+        cfg.num_actions = self.num_actions
+        cfg.dtype = DTYPES[dtype]
+        cfg.lr, cfg.adam_eps = lr, eps
+        cfg.adam_beta1, cfg.adam_beta2 = betas
+        cfg.max_grad_norm = max_grad_norm
+        cfg.entropy_coeff = entropy_coeff
+        cfg.vtrace_lambda = vtrace_lambda
+        cfg.clip_rho_threshold = clip_rho_threshold
+        cfg.clip_pg_rho_threshold = clip_pg_rho_threshold
+        cfg.world_size = int(world_size)
+        self.cfg = cfg
+        h = C.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        check(L.impala_create(C.byref(cfg), idx, C.byref(h)), "impala_create")
+        self._h = h
+        n = model.flat.numel()
+        assert n == _lib.param_count(self.num_actions)
+        if inference_only:
+            self.exp_avg = self.exp_avg_sq = self.metrics = None
+            check(L.impala_bind_state(h, ptr(model.flat), None, None, None, None,
+                                      stream_ptr(None)), "impala_bind_state")
+        else:
+            self.exp_avg = torch.zeros_like(model.flat)
+            self.exp_avg_sq = torch.zeros_like(model.flat)
+            self.metrics = torch.zeros(_lib.NUM_METRICS, dtype=torch.float32, device=self.device)
+            check(L.impala_bind_state(h, ptr(model.flat), ptr(model.flat_grad), ptr(self.exp_avg),
+                                      ptr(self.exp_avg_sq), ptr(self.metrics), stream_ptr(None)),
+                  "impala_bind_state")
+        self._version = model._version
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib().impala_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def frames(self) -> int:
+        return self.batch_size * self.rollout_length
+
+    def refresh_weights(self, stream=None):
+        check(_lib.lib().impala_refresh_weights(self._h, stream_ptr(stream)),
+              "impala_refresh_weights")
+        self._version = self.model._version
+
+    def _sync_weights(self, stream=None):
+        if self._version != self.model._version:
+            self.refresh_weights(stream)
+
+    def set_step(self, step: int, stream=None):
+        check(_lib.lib().impala_set_step(self._h, int(step), stream_ptr(stream)), "impala_set_step")
+
+    # ------------------------------------------------------------------ compute
+    def forward(self, obs: torch.Tensor, stream=None):
+        """obs u8 [N,3,64,64] (any N; chunked by the handle capacity) -> logits [N,A], v [N,1]."""
+        if obs.dtype != torch.uint8 or obs.shape[-3:] != (3, 64, 64):
+            raise ValueError("obs must be uint8 [..., 3, 64, 64]")
+        obs = obs.reshape(-1, 3, 64, 64)
+        if obs.device != self.device:
+            obs = obs.to(self.device, non_blocking=True)
+        obs = obs.contiguous()
+        self._sync_weights(stream)
+        n = obs.shape[0]
+        logits = torch.empty(n, self.num_actions, dtype=torch.float32, device=self.device)
+        values = torch.empty(n, 1, dtype=torch.float32, device=self.device)
+        cap = self.frames
+        L = _lib.lib()
+        sp = stream_ptr(stream)
+        for s in range(0, n, cap):
+            e = min(n, s + cap)
+            check(L.impala_forward(self._h, ptr(obs[s:e]), e - s, ptr(logits[s:e]), ptr(values[s:e]),
+                                   sp), "impala_forward")
+        return logits, values
+
+    def _batch(self, obs, actions, rewards, discounts, mu) -> ImpalaBatch:
+        B, T, A = self.batch_size, self.rollout_length, self.num_actions
+        exp = {"obs": ((B, T, 3, 64, 64), torch.uint8), "actions": ((B, T), torch.int64),
+               "rewards": ((B, T), torch.float32), "discounts": ((B, T), torch.float32),
+               "behaviour_logits": ((B, T, A), torch.float32)}
+        got = {"obs": obs, "actions": actions, "rewards": rewards, "discounts": discounts,
+               "behaviour_logits": mu}
+        for k, (shape, dt) in exp.items():
+            t = got[k]
+            if tuple(t.shape) != shape or t.dtype != dt:
+                raise ValueError(f"{k}: expected {dt} {shape}, got {t.dtype} {tuple(t.shape)}")
+            if t.device != self.device or not t.is_contiguous():
+                raise ValueError(f"{k}: must be a contiguous tensor on {self.device}")
+        return ImpalaBatch(ptr(obs), ptr(actions), ptr(rewards), ptr(discounts), ptr(mu))
+
+    def train_step(self, obs, actions, rewards, discounts, mu, stream=None):
+        """Full update (world_size 1): learning.py:140-177."""
+        b = self._batch(obs, actions, rewards, discounts, mu)
+        self._sync_weights(stream)
+        check(_lib.lib().impala_train_step(self._h, C.byref(b), stream_ptr(stream)),
+              "impala_train_step")
+        self._updated()
+
+    def compute_grads(self, obs, actions, rewards, discounts, mu, stream=None):
+        b = self._batch(obs, actions, rewards, discounts, mu)
+        self._sync_weights(stream)
+        check(_lib.lib().impala_compute_grads(self._h, C.byref(b), stream_ptr(stream)),
+              "impala_compute_grads")
+
+    def apply_update(self, stream=None):
+        check(_lib.lib().impala_apply_update(self._h, stream_ptr(stream)), "impala_apply_update")
+        self._updated()
+
+    def _updated(self):
+        # the Adam kernel rewrote params AND this handle's kernel-layout weights
+        self.model._version += 1
+        self._version = self.model._version
+
+
+# ---------------------------------------------------------------------- standalone kernels
+def vtrace(v_tm1, v_t, r_t, discount_t, rho_tm1, lambda_=1.0, clip_rho_threshold=1.0,
+           clip_pg_rho_threshold=1.0, stream=None):
+    """Batched V-trace on device tensors [B, L] -> (pg_advantage, td_error, q_estimate).
+    Same return order as the reference's ``adv, err, _ = batched_vtrace(...)``."""
+    ts = [t.contiguous().to(torch.float32) for t in (v_tm1, v_t, r_t, discount_t, rho_tm1)]
+    if ts[0].dim() == 1:
+        ts = [t.unsqueeze(0) for t in ts]
+        squeeze = True
+    else:
+        squeeze = False
+    B, Lh = ts[0].shape
+    for t in ts:
+        if t.shape != (B, Lh) or t.device.type != "cuda":
+            raise ValueError("vtrace inputs must be [B, L] cuda tensors of one shape")
+    adv, err, q = (torch.empty_like(ts[0]) for _ in range(3))
+    check(_lib.lib().impala_vtrace(*[ptr(t) for t in ts], B, Lh, lambda_, clip_rho_threshold,
+                                   clip_pg_rho_threshold, ptr(adv), ptr(err), ptr(q),
+                                   stream_ptr(stream)), "impala_vtrace")
+    if squeeze:
+        return adv[0], err[0], q[0]
+    return adv, err, q
+
+
+def loss_head(logits, values, actions, rewards, discounts, mu, entropy_coeff=0.01, lambda_=1.0,
+              clip_rho=1.0, clip_pg_rho=1.0, stream=None):
+    """Fused loss head (learning.py:144-170) on device tensors; returns a dict."""
+    B, T, A = logits.shape
+    dev = logits.device
+    f = lambda t: t.contiguous().to(torch.float32)  # noqa: E731
+    lg, v, r, g, m = f(logits), f(values), f(rewards), f(discounts), f(mu)
+    a = actions.contiguous().to(torch.int64)
+    dl = torch.empty_like(lg)
+    dv = torch.empty_like(v)
+    met = torch.empty(6, dtype=torch.float32, device=dev)
+    adv = torch.empty(B, T - 1, dtype=torch.float32, device=dev)
+    err, q = torch.empty_like(adv), torch.empty_like(adv)
+    rho = torch.empty(B, T, dtype=torch.float32, device=dev)
+    check(_lib.lib().impala_loss_head(ptr(lg), ptr(v), ptr(a), ptr(r), ptr(g), ptr(m), B, T, A,
+                                      entropy_coeff, lambda_, clip_rho, clip_pg_rho, ptr(dl),
+                                      ptr(dv), ptr(met), ptr(adv), ptr(err), ptr(q), ptr(rho),
+                                      stream_ptr(stream)), "impala_loss_head")
+    return dict(dlogits=dl, dvalues=dv, metrics=met, adv=adv, err=err, q=q, rho=rho)

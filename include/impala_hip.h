@@ -1,0 +1,142 @@
+/* impala_hip.h — C-ABI of the MI355X-native IMPALA learner (libimpala_hip.so).
+ *
+ * Drop-in boundary for the reference's learner path.  Every entry point replaces a piece of
+ * the reference's PyTorch learner (paths relative to the d3sm0/impala repository):
+ *
+ *   impala_train_step      agents/impala/learning.py:140-177  ImpalaLearner._train_step
+ *                          (forward, Categorical log-prob / ratio, batched V-trace, pg/value/
+ *                          entropy loss, backward, clip_grad_norm_(0.5), Adam.step)
+ *   impala_compute_grads   learning.py:141-170 (zero_grad .. loss.backward + metrics)
+ *   impala_apply_update    learning.py:172-176 (clip_grad_norm_ + optimizer.step), after the
+ *                          caller's gradient all-reduce in the data-parallel learner
+ *   impala_forward         models/distributed_models.py:17-19 AtariPPOModel.forward
+ *                          (also the actor's batched act(), :21-32)
+ *   impala_vtrace          rlego.vtrace_td_error_and_advantage as called through
+ *                          learning.py:15-26,150-153 (returns pg_advantage, td_error, q)
+ *   impala_loss_head       learning.py:144-170 given network outputs (loss, metrics, d/dlogits,
+ *                          d/dvalues)
+ *   impala_bind_state      the optimizer/parameter ownership of agents/impala/builder.py:42-59
+ *
+ * Conventions: plain pointers and sizes, no torch types.  All tensor pointers are DEVICE
+ * pointers on the learner's device; `stream` is a hipStream_t passed as void* (NULL = the
+ * legacy default stream).  Every call returns 0 on success or a non-zero status (a hipError_t
+ * value, or IMPALA_E_* below); impala_last_error() describes the last failure of the calling
+ * thread.  Calls are asynchronous on `stream` (no host synchronisation inside), except
+ * impala_create / impala_destroy.  No exceptions or aborts cross the ABI.
+ *
+ * Layouts (batch-major, as agents/impala/learning.py:142-145):
+ *   obs               uint8  [B][T][3][64][64]
+ *   actions           int64  [B][T]
+ *   rewards, discounts float [B][T]
+ *   behaviour_logits  float  [B][T][A]
+ * Parameters: one flat fp32 buffer in torch state_dict order of AtariPPOModel
+ * (model.body.body.{0,2,4}.{weight,bias}, model.projection.{0,1}.{weight,bias},
+ *  model.actor.{weight,bias}, model.critic.{weight,bias}); grads / Adam moments alike.
+ */
+#ifndef IMPALA_HIP_H_
+#define IMPALA_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IMPALA_ABI_VERSION 1
+
+#define IMPALA_OK 0
+#define IMPALA_E_INVALID 1001   /* bad argument / shape */
+#define IMPALA_E_STATE 1002     /* state not bound / wrong call order */
+#define IMPALA_E_UNSUPPORTED 1003
+
+#define IMPALA_DTYPE_F32 0      /* fp32 operands, f32 MFMA (parity mode) */
+#define IMPALA_DTYPE_BF16 1     /* bf16 operands, fp32 accumulate / master weights */
+
+/* metric slots written to the bound metrics buffer (names as learning.py:161-174) */
+#define IMPALA_M_LOSS 0
+#define IMPALA_M_ENTROPY 1
+#define IMPALA_M_TD 2
+#define IMPALA_M_PG 3
+#define IMPALA_M_KL 4
+#define IMPALA_M_RATIO 5
+#define IMPALA_M_GRAD_NORM 6
+#define IMPALA_M_STEP 7
+#define IMPALA_NUM_METRICS 8
+
+typedef struct impala_learner impala_learner;
+
+typedef struct {
+  int batch_size;              /* B per replica (conf/agent/impala.yaml batch_size)          */
+  int rollout_length;          /* T (conf/agent/impala.yaml rollout_length), 2..64           */
+  int num_actions;             /* A (procgen 15), 1..15                                      */
+  int dtype;                   /* IMPALA_DTYPE_*                                             */
+  float lr, adam_beta1, adam_beta2, adam_eps;   /* builder.py:43-44: lr 1e-4, eps 1e-5     */
+  float max_grad_norm;         /* learning.py:93: 0.5                                        */
+  float entropy_coeff;         /* learning.py:94: 0.01                                       */
+  float vtrace_lambda;         /* rlego default 1.0                                          */
+  float clip_rho_threshold;    /* rlego default 1.0                                          */
+  float clip_pg_rho_threshold; /* rlego default 1.0                                          */
+  int world_size;              /* data-parallel replicas (gradient average divisor)          */
+} impala_config;
+
+typedef struct {
+  const uint8_t* obs;
+  const int64_t* actions;
+  const float* rewards;
+  const float* discounts;
+  const float* behaviour_logits;
+} impala_batch;
+
+int impala_abi_version(void);
+const char* impala_last_error(void);
+int impala_config_default(impala_config* cfg);
+/* number of fp32 parameters of AtariPPOModel for `num_actions` (344,496 for A = 15) */
+size_t impala_param_count(int num_actions);
+
+int impala_create(const impala_config* cfg, int device, impala_learner** out);
+int impala_destroy(impala_learner* h);
+
+/* Bind caller-owned device buffers (each impala_param_count() floats; metrics 8 floats).
+ * Only `params` is required for impala_forward (inference-only handles); the training calls
+ * need all five.
+ * The library reads/writes them in place: params and Adam moments are updated by
+ * impala_apply_update, grads hold the post-clip gradient afterwards (as p.grad does). */
+int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp_avg,
+                      float* exp_avg_sq, float* metrics, void* stream);
+/* Re-derive the kernel-layout weights after the caller changed `params` (load_state_dict). */
+int impala_refresh_weights(impala_learner* h, void* stream);
+/* Adam step counter (torch state['step']); for checkpoint resume. */
+int impala_set_step(impala_learner* h, int64_t step, void* stream);
+
+/* Policy/value forward of n frames (n <= B*T): logits [n][A], values [n]. */
+int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, float* values,
+                   void* stream);
+
+/* Full learner update for one batch (world_size must be 1). */
+int impala_train_step(impala_learner* h, const impala_batch* batch, void* stream);
+/* Data-parallel split: gradients of the local batch into `grads` (local mean) ... */
+int impala_compute_grads(impala_learner* h, const impala_batch* batch, void* stream);
+/* ... caller all-reduces (sums) `grads` across replicas ... then: average (1/world_size),
+ * global-norm clip and Adam. */
+int impala_apply_update(impala_learner* h, void* stream);
+
+/* Standalone batched V-trace, [B][L] row-major, L <= 64 (test / reuse entry point). */
+int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,
+                  const float* rho_tm1, int B, int L, float lambda_, float clip_rho_threshold,
+                  float clip_pg_rho_threshold, float* pg_advantage, float* td_error,
+                  float* q_estimate, void* stream);
+
+/* Standalone fused loss head given network outputs: logits [B][T][A], values [B][T].
+ * Writes dlogits [B][T][A], dvalues [B][T], metrics[6] (loss, entropy, td, pg, kl, ratio),
+ * and optionally (nullable) adv/err/q [B][T-1], rho [B][T]. */
+int impala_loss_head(const float* logits, const float* values, const int64_t* actions,
+                     const float* rewards, const float* discounts, const float* behaviour_logits,
+                     int B, int T, int A, float entropy_coeff, float lambda_, float clip_rho,
+                     float clip_pg_rho, float* dlogits, float* dvalues, float* metrics6,
+                     float* adv, float* err, float* q, float* rho, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IMPALA_HIP_H_ */

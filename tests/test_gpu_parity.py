@@ -1,0 +1,254 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the golden fixtures.
+
+Tolerances (fp32 parity mode): V-trace / loss head on identical inputs 1e-5 rel (north_star);
+network forward 1e-4 rel (f32 MFMA fma-chain vs MKLDNN summation order); full train step
+metrics 1e-4 rel, post-clip gradients 1e-3 relative L2, post-Adam params 1e-6 abs (the
+Adam update itself is ~1e-4).  bf16 perf mode: loose bounds stated per test.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu, vtrace as ovt
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def _rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+# ----------------------------------------------------------------------------- V-trace
+@pytest.mark.parametrize("tag,lam", [("l100", 1.0), ("l095", 0.95)])
+def test_vtrace_matches_golden(tag, lam):
+    from impala_amd.engine import vtrace
+    dev = _dev()
+    d = _load("vtrace_random.npz")
+    adv, err, q = vtrace(*[_t(d[k], dev) for k in ("v_tm1", "v_t", "r", "g", "rho")], lambda_=lam)
+    np.testing.assert_allclose(adv.cpu().numpy(), d[f"adv_{tag}"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(err.cpu().numpy(), d[f"err_{tag}"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(q.cpu().numpy(), d[f"q_{tag}"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,L", [(1, 1), (3, 7), (5, 19), (2, 33), (4, 64)])
+def test_vtrace_ragged_shapes(B, L):
+    from impala_amd.engine import vtrace
+    dev = _dev()
+    rng = np.random.default_rng(B * 100 + L)
+    v_tm1 = rng.standard_normal((B, L)).astype(np.float32)
+    v_t = rng.standard_normal((B, L)).astype(np.float32)
+    r = rng.standard_normal((B, L)).astype(np.float32)
+    g = (0.99 * (rng.random((B, L)) > 0.1)).astype(np.float32)
+    rho = rng.uniform(0.0, 3.0, (B, L)).astype(np.float32)
+    exp = ovt.vtrace_numpy(v_tm1.astype(np.float64), v_t, r, g, rho, lambda_=0.9,
+                           clip_rho_threshold=1.2, clip_pg_rho_threshold=0.8)
+    got = vtrace(*[_t(x, dev) for x in (v_tm1, v_t, r, g, rho)], lambda_=0.9,
+                 clip_rho_threshold=1.2, clip_pg_rho_threshold=0.8)
+    for gt, ex in zip(got, exp):
+        np.testing.assert_allclose(gt.cpu().numpy(), ex, rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- loss head
+def test_loss_head_matches_golden():
+    from impala_amd.engine import loss_head
+    dev = _dev()
+    d = _load("head_loss.npz")
+    out = loss_head(*[_t(d[k], dev) for k in ("logits", "values", "act", "rew", "disc", "mu")])
+    # O(1) quantities: 1e-5 rel + 1e-6 abs (a few fp32 ulps near zero); gradients are
+    # O(1e-4): 1e-5 rel + 1e-9 abs
+    for k, atol in (("adv", 1e-6), ("err", 1e-6), ("q", 1e-6), ("rho", 1e-6),
+                    ("dlogits", 1e-9), ("dvalues", 1e-9)):
+        np.testing.assert_allclose(out[k].cpu().numpy(), d[k], rtol=1e-5, atol=atol, err_msg=k)
+    np.testing.assert_allclose(out["metrics"].cpu().numpy(), d["scalars"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("B,T,A", [(1, 2, 1), (3, 5, 6), (2, 33, 15), (1, 64, 4)])
+def test_loss_head_edge_shapes(B, T, A):
+    from impala_amd.engine import loss_head
+    dev = _dev()
+    rng = np.random.default_rng(B + 10 * T + 100 * A)
+    logits = (3 * rng.standard_normal((B, T, A))).astype(np.float32)
+    values = rng.standard_normal((B, T)).astype(np.float32)
+    act = rng.integers(0, A, (B, T)).astype(np.int64)
+    rew = rng.standard_normal((B, T)).astype(np.float32)
+    disc = (0.99 * (rng.random((B, T)) > 0.2)).astype(np.float32)
+    mu = rng.standard_normal((B, T, A)).astype(np.float32)
+    exp = ref_cpu.loss_from_outputs(logits, values, act, rew, disc, mu)
+    out = loss_head(*[_t(x, dev) for x in (logits, values, act, rew, disc, mu)])
+    for k, atol in (("adv", 1e-5), ("err", 1e-5), ("q", 1e-5), ("rho", 1e-6),
+                    ("dlogits", 1e-8), ("dvalues", 1e-8)):
+        np.testing.assert_allclose(out[k].cpu().numpy(), exp[k], rtol=1e-5, atol=atol, err_msg=k)
+    got = out["metrics"].cpu().numpy()
+    want = [exp[k] for k in ("loss", "entropy", "td", "pg", "kl", "ratio")]
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
+
+
+# ----------------------------------------------------------------------------- forward
+def _model(dev, dtype="fp32", A=15, flat=None, seed=0):
+    from impala_amd.model import AtariPPOModel
+    m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=dtype, seed=seed)
+    if flat is not None:
+        m.load_flat(flat)
+    return m
+
+
+def test_seed_init_matches_reference():
+    dev = _dev()
+    d = _load("model_forward.npz")
+    m = _model(dev, seed=0)
+    # same RNG stream; torch-CPU trunc_normal_ may differ by 1 ulp across host ISAs
+    np.testing.assert_allclose(m.flat.cpu().numpy(), d["params"], rtol=1e-6, atol=1e-9)
+    assert list(m.state_dict().keys()) == [str(k) for k in d["keys"]]
+
+
+def test_forward_fp32_matches_reference():
+    dev = _dev()
+    d = _load("model_forward.npz")
+    m = _model(dev, flat=d["params"])
+    lg, v = m(_t(d["obs"], dev))
+    np.testing.assert_allclose(lg.cpu().numpy(), d["logits"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), d["values"], rtol=1e-4, atol=1e-5)
+
+
+def test_forward_bf16_close_to_reference():
+    dev = _dev()
+    d = _load("model_forward.npz")
+    m = _model(dev, "bf16", flat=d["params"])
+    lg, v = m(_t(d["obs"], dev))
+    assert _rel_l2(lg.cpu().numpy(), d["logits"]) < 3e-2
+    assert _rel_l2(v.cpu().numpy(), d["values"]) < 5e-2
+
+
+@pytest.mark.parametrize("n", [1, 7, 129, 300])
+def test_forward_ragged_frames(n):
+    dev = _dev()
+    rng = np.random.default_rng(n)
+    obs = rng.integers(0, 256, (n, 3, 64, 64), dtype=np.uint8)
+    ref = ref_cpu.make_model(3)
+    m = _model(dev, flat=ref_cpu.flat_params(ref))
+    lg, v = m(_t(obs, dev))
+    elg, ev = ref_cpu.forward_numpy(ref, obs)
+    np.testing.assert_allclose(lg.cpu().numpy(), elg, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), ev, rtol=1e-4, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- train step
+def _engine(m, B, T, **kw):
+    from impala_amd.engine import Engine
+    e = Engine(m, batch_size=B, rollout_length=T, **kw)
+    m._train_engine = e
+    return e
+
+
+def test_train_steps_fp32_match_reference():
+    dev = _dev()
+    d = _load("train_step.npz")
+    m = _model(dev, flat=d["params0"])
+    e = _engine(m, 2, 20)
+    names = ("loss", "entropy", "td", "pg", "kl", "ratio", "grad_norm")
+    for i in range(3):
+        batch = [_t(d[f"{k}{i}"], dev) for k in ("obs", "act", "rew", "disc", "mu")]
+        e.train_step(*batch)
+        met = e.metrics.cpu().numpy()
+        np.testing.assert_allclose(met[:7], [d[k][i] for k in names], rtol=1e-4, atol=1e-6,
+                                   err_msg=f"metrics step {i}")
+        assert met[7] == i + 1
+        if i == 0:
+            assert _rel_l2(m.flat_grad.cpu().numpy(), d["grads1"]) < 1e-3
+            np.testing.assert_allclose(m.flat.cpu().numpy(), d["params1"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(m.flat.cpu().numpy(), d["params3"], rtol=0, atol=2e-6)
+
+
+def _oracle_step(flat, batch_np, A=15):
+    ref = ref_cpu.RefModel(A)
+    ref_cpu.load_flat(ref, flat)
+    opt = ref_cpu.make_optimizer(ref)
+    obs, act, rew, disc, mu = batch_np
+    met = ref_cpu.train_step(ref, opt, [torch.from_numpy(x) for x in batch_np], collated=True)
+    return ref, {k: float(v) for k, v in met.items()}
+
+
+@pytest.mark.parametrize("B,T,A", [(1, 2, 15), (3, 7, 6), (5, 20, 15)])
+def test_train_step_edge_shapes_fp32(B, T, A):
+    dev = _dev()
+    batch = ref_cpu.synthetic_batch(B, T, A, seed=B * T + A)
+    ref0 = ref_cpu.make_model(1, A)
+    flat0 = ref_cpu.flat_params(ref0)
+    ref, met = _oracle_step(flat0, batch, A)
+    m = _model(dev, A=A, flat=flat0)
+    e = _engine(m, B, T)
+    e.train_step(*[_t(x, dev) for x in batch])
+    got = e.metrics.cpu().numpy()
+    names = ("loss", "entropy", "td", "pg", "kl", "ratio", "grad_norm")
+    np.testing.assert_allclose(got[:7], [met["train/" + k] for k in names], rtol=1e-4, atol=1e-6)
+    assert _rel_l2(m.flat_grad.cpu().numpy(), ref_cpu.flat_grads(ref)) < 1e-3
+    np.testing.assert_allclose(m.flat.cpu().numpy(), ref_cpu.flat_params(ref), atol=1e-6)
+
+
+def test_train_step_bf16_tracks_reference():
+    dev = _dev()
+    d = _load("train_step.npz")
+    m = _model(dev, "bf16", flat=d["params0"])
+    e = _engine(m, 2, 20)
+    batch = [_t(d[f"{k}0"], dev) for k in ("obs", "act", "rew", "disc", "mu")]
+    e.train_step(*batch)
+    met = e.metrics.cpu().numpy()
+    names = ("loss", "entropy", "td", "pg", "kl", "ratio", "grad_norm")
+    exp = np.array([d[k][0] for k in names])
+    assert np.all(np.abs(met[:7] - exp) <= 5e-2 * np.abs(exp) + 5e-3), (met, exp)
+    g, gr = m.flat_grad.cpu().numpy(), d["grads1"]
+    cos = float(np.dot(g, gr) / (np.linalg.norm(g) * np.linalg.norm(gr)))
+    assert cos > 0.99, cos
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_train_step_deterministic(dtype):
+    dev = _dev()
+    batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(8, 20, 15, seed=5)]
+    flats = []
+    for _ in range(2):
+        m = _model(dev, dtype, seed=0)
+        e = _engine(m, 8, 20)
+        for _ in range(2):
+            e.train_step(*batch)
+        torch.cuda.synchronize()
+        flats.append((m.flat.cpu().numpy().copy(), e.metrics.cpu().numpy().copy()))
+    np.testing.assert_array_equal(flats[0][0], flats[1][0])
+    np.testing.assert_array_equal(flats[0][1], flats[1][1])
+
+
+def test_full_size_bf16_step_properties():
+    """B=64, T=20 (BASELINE config 2): finite, loss decreases on a repeated batch,
+    grad norm positive, params move by <= ~lr per step (Adam bound)."""
+    dev = _dev()
+    batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(64, 20, 15, seed=1234)]
+    m = _model(dev, "bf16", seed=0)
+    e = _engine(m, 64, 20)
+    p0 = m.flat.clone()
+    losses = []
+    for _ in range(20):
+        e.train_step(*batch)
+        losses.append(float(e.metrics[0]))
+    torch.cuda.synchronize()
+    assert np.all(np.isfinite(losses))
+    assert losses[-1] < losses[0]
+    delta = (m.flat - p0).abs().max().item()
+    assert 0 < delta <= 20 * 1e-4 * 3  # Adam: |step| ~ lr (bias-corrected ratio can exceed 1)
