@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Learner throughput bench: env-frames/s of the IMPALA learner step on MI355X.
+
+``python bench.py --gpus N --steps K --warmup W``  (N > 1: launched by torch.distributed.run).
+
+Workload = BASELINE.json configs[1]: IMPALA procgen learner, B=64 trajectories x T=20 steps
+per replica, 15 actions, obs (3,64,64) u8, bf16 operands / fp32 accumulation + fp32 master
+weights.  One step = the full learner update (NatureCNN forward, log-softmax, V-trace, losses,
+backward, [RCCL gradient all-reduce], clip_grad_norm_(0.5), Adam) on a synthetic batch that
+is resident in HBM before the timed region.  Multi-GPU: data-parallel
+replicas, B=64 per GPU (weak scaling), one flat fp32 gradient bucket all-reduced over RCCL.
+
+Also reported: the dominant kernel's roofline (algorithmic FLOPs / its live HIP-event launch
+duration vs the dense MFMA peak) and the reference CPU learner (the oracle's torch-CPU
+restatement of agents/impala/learning.py:140-177) timed on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# algorithmic FLOPs per frame of each kernel (2*MACs)
+FLOPS_PER_FRAME = {
+    "conv1_fwd": 2 * 225 * 32 * 192, "conv2_fwd": 2 * 36 * 64 * 512, "conv3_fwd": 2 * 16 * 64 * 576,
+    "fc_fwd": 2 * 256 * 1024, "heads_fwd": 2 * 16 * 256,
+    "heads_dgrad": 2 * 16 * 256, "fc_dgrad": 2 * 256 * 1024, "conv3_dgrad": 2 * 16 * 64 * 576,
+    "conv2_dgrad": 2 * 36 * 64 * 512, "heads_wgrad": 2 * 16 * 256, "fc_wgrad": 2 * 256 * 1024,
+    "conv3_wgrad": 2 * 16 * 64 * 576, "conv2_wgrad": 2 * 36 * 64 * 512,
+    "conv1_wgrad": 2 * 225 * 32 * 192,
+}
+STEP_FLOPS_PER_FRAME = 17_743_872  # fwd 6,836,224 + bwd 10,907,648 (no conv1 dgrad)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA, MI355X_MICROARCH.md
+
+
+def synthetic_batch(B, T, A, seed, device):
+    """obs u8 uniform; a ~ U[0,A); r ~ N(0,1) clipped; g = 0.99*(u>0.05);
+    mu ~ N(0,1).  Built on the host once, copied to HBM before timing."""
+    rng = np.random.default_rng(seed)
+    obs = rng.integers(0, 256, size=(B, T, 3, 64, 64), dtype=np.uint8)
+    act = rng.integers(0, A, size=(B, T), dtype=np.int64)
+    rew = np.clip(rng.standard_normal((B, T)), -10, 10).astype(np.float32)
+    disc = (0.99 * (rng.random((B, T)) > 0.05)).astype(np.float32)
+    mu = rng.standard_normal((B, T, A)).astype(np.float32)
+    return [torch.from_numpy(x).to(device) for x in (obs, act, rew, disc, mu)]
+
+
+def cpu_baseline(B, T, A, seconds):
+    """The reference CPU learner (oracle port of learning.py:140-177), timed on host cores."""
+    from oracle import ref_cpu
+    threads = torch.get_num_threads()
+    batch = [torch.from_numpy(x) for x in ref_cpu.synthetic_batch(B, T, A, seed=1234)]
+    model = ref_cpu.make_model(0, A)
+    opt = ref_cpu.make_optimizer(model)
+    for _ in range(2):
+        ref_cpu.train_step(model, opt, batch, collated=True)
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        ref_cpu.train_step(model, opt, batch, collated=True)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    try:
+        cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
+    except Exception:
+        cpu = "unknown"
+    return {"value": B * T / med, "unit": "env-frames/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} oracle learner steps (B={B},T={T},fp32 torch-CPU, "
+                      f"{threads} threads, {cpu}) after 2 warm-up; median step {med * 1e3:.1f} ms"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=64, help="trajectories per GPU")
+    ap.add_argument("--rollout", type=int, default=20)
+    ap.add_argument("--actions", type=int, default=15)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--roofline-kernel", default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from impala_amd.engine import Engine
+    from impala_amd.model import AtariPPOModel
+
+    B, T, A = args.batch, args.rollout, args.actions
+    model = AtariPPOModel((3, 64, 64), A, device=dev, dtype=args.dtype, seed=0)
+    eng = Engine(model, batch_size=B, rollout_length=T, world_size=world)
+    model._train_engine = eng
+    batch = synthetic_batch(B, T, A, 1234 + rank, dev)
+    if dist is not None:  # identical initial weights on every replica
+        dist.broadcast(model.flat, 0)
+        model.params_changed()
+
+    def step():
+        if dist is None:
+            eng.train_step(*batch)
+        else:
+            eng.compute_grads(*batch)
+            dist.all_reduce(model.flat_grad)
+            eng.apply_update()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rk = args.roofline_kernel or ("conv2_wgrad" if False else None)
+    # dominant kernel: pick the one with the largest measured time in a short probe
+    probe = {}
+    if rk is None:
+        for kname in FLOPS_PER_FRAME:
+            eng.timer_start(kname, 3)
+            for _ in range(3):
+                step()
+            ms, n = eng.timer_read()
+            probe[kname] = ms / max(n, 1)
+        rk = max(probe, key=probe.get)
+    torch.cuda.synchronize()
+
+    eng.timer_start(rk, args.steps)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    k_ms, k_n = eng.timer_read()
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    met = eng.metrics.cpu().numpy()
+    if not np.all(np.isfinite(met)):
+        raise RuntimeError(f"non-finite metrics {met}")
+
+    frames = world * B * T * args.steps
+    value = frames / elapsed
+    ms_step = elapsed * 1e3 / args.steps
+    k_avg_ms = k_ms / max(k_n, 1)
+    achieved = FLOPS_PER_FRAME[rk] * B * T / (k_avg_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    out = {
+        "metric": "learner env-frames/sec (IMPALA procgen T=20 B=64) at 1/2/4/8 MI355X",
+        "value": round(value, 1), "unit": "env-frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic rollouts resident in HBM (obs u8 uniform, BASELINE.md §3); "
+                "random-init weights (reference layer_init_truncated, seed 0)",
+        "config": {"workload": f"IMPALA procgen learner step, NatureCNN actor-critic, "
+                               f"B={B}/GPU T={T} A={A}, global B={B * world}",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": rk, "achieved": round(achieved, 2),
+                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                     "traffic": None, "avg_launch_us": round(k_avg_ms * 1e3, 2),
+                     "launches": k_n},
+        "step_tflops": round(STEP_FLOPS_PER_FRAME * value / world / 1e12, 2),
+    }
+    if probe:
+        out["kernel_probe_us"] = {k: round(v * 1e3, 2) for k, v in sorted(probe.items(), key=lambda kv: -kv[1])}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(B, T, A, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

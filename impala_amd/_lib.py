@@ -24,7 +24,8 @@ EXPORTS = (
     "impala_abi_version", "impala_last_error", "impala_config_default", "impala_param_count",
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
     "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
-    "impala_apply_update", "impala_vtrace", "impala_loss_head",
+    "impala_apply_update", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
+    "impala_kernel_name", "impala_timer_start", "impala_timer_read",
 )
 
 
@@ -69,8 +70,12 @@ def _declare(lib):
     lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
                                      C.c_float, C.c_float, C.c_float, C.c_float, _P, _P, _P,
                                      _P, _P, _P, _P, _P]
+    lib.impala_kernel_name.argtypes = [C.c_int]
+    lib.impala_kernel_name.restype = C.c_char_p
+    lib.impala_timer_start.argtypes = [_P, C.c_int, C.c_int]
+    lib.impala_timer_read.argtypes = [_P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     for name in EXPORTS:
-        if name not in ("impala_last_error", "impala_param_count"):
+        if name not in ("impala_last_error", "impala_param_count", "impala_kernel_name"):
             getattr(lib, name).restype = C.c_int
 
 

@@ -71,6 +71,18 @@ Split plan_split(long M, int tiles, int target_wgs) {
 
 }  // namespace
 
+// kernel ids for the live launch timer (impala_timer_*)
+enum KernelId {
+  K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV3_FWD, K_LN_FWD, K_FC_FWD, K_HEADS_FWD, K_LOSS,
+  K_HEADS_DGRAD, K_FC_DGRAD, K_LN_BWD, K_CONV3_DGRAD, K_CONV2_DGRAD, K_HEADS_WGRAD,
+  K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV1_WGRAD, K_REDUCE, K_SUMSQ, K_ADAM,
+  K_COUNT
+};
+const char* const kKernelNames[K_COUNT] = {
+    "conv1_fwd", "conv2_fwd", "conv3_fwd", "ln_fwd", "fc_fwd", "heads_fwd", "loss_head",
+    "heads_dgrad", "fc_dgrad", "ln_bwd", "conv3_dgrad", "conv2_dgrad", "heads_wgrad",
+    "fc_wgrad", "conv3_wgrad", "conv2_wgrad", "conv1_wgrad", "reduce_grads", "sumsq", "adam"};
+
 struct impala_learner {
   impala_config cfg;
   int device = 0;
@@ -94,7 +106,23 @@ struct impala_learner {
   int64_t* step;
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0;
+  // live launch timer: hipEvent pairs around every launch of one kernel id
+  int timer_kernel = -1, timer_cap = 0, timer_n = 0;
+  hipEvent_t* timer_ev = nullptr;
 };
+
+namespace {
+inline void timer_begin(impala_learner* h, int kid, hipStream_t st) {
+  if (h->timer_kernel == kid && h->timer_n < h->timer_cap)
+    (void)hipEventRecord(h->timer_ev[2 * h->timer_n], st);
+}
+inline void timer_end(impala_learner* h, int kid, hipStream_t st) {
+  if (h->timer_kernel == kid && h->timer_n < h->timer_cap) {
+    (void)hipEventRecord(h->timer_ev[2 * h->timer_n + 1], st);
+    h->timer_n++;
+  }
+}
+}  // namespace
 
 namespace {
 
@@ -106,30 +134,42 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
   const float* vv = h->vecs;
   {
     Conv1Fwd<T> op{n * P1, sw + sh.w1, vv + Vecs::b1, obs, (T*)h->act1};
+    timer_begin(h, K_CONV1_FWD, st);
     gemm_rc<T, 2, 2><<<dim3(cdiv((long)n * P1, 128), 1), 256, 0, st>>>(op);
+    timer_end(h, K_CONV1_FWD, st);
     CK_LAUNCH("conv1_fwd");
   }
   {
     Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
+    timer_begin(h, K_CONV2_FWD, st);
     gemm_rc<T, 4, 1><<<dim3(cdiv((long)n * P2, 64), 1), 256, 0, st>>>(op);
+    timer_end(h, K_CONV2_FWD, st);
     CK_LAUNCH("conv2_fwd");
   }
   {
     Conv3Fwd<T> op{n * P3, sw + sh.w3, vv + Vecs::b3, (const T*)h->act2, (T*)h->act3};
+    timer_begin(h, K_CONV3_FWD, st);
     gemm_rc<T, 4, 1><<<dim3(cdiv((long)n * P3, 64), 1), 256, 0, st>>>(op);
+    timer_end(h, K_CONV3_FWD, st);
     CK_LAUNCH("conv3_fwd");
   }
+  timer_begin(h, K_LN_FWD, st);
   ln_fwd_kernel<T><<<cdiv(n, 4), 256, 0, st>>>((const T*)h->act3, vv + Vecs::lng, vv + Vecs::lnb,
                                                (T*)h->y, h->lnstat, n);
+  timer_end(h, K_LN_FWD, st);
   CK_LAUNCH("ln_fwd");
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
+    timer_begin(h, K_FC_FWD, st);
     gemm_rc<T, 4, 1><<<dim3(cdiv(n, 64), HID / 64), 256, 0, st>>>(op);
+    timer_end(h, K_FC_FWD, st);
     CK_LAUNCH("fc_fwd");
   }
   {
     HeadsFwd<T> op{n, sw + sh.wh, vv + Vecs::bh, (const T*)h->h, h->heads};
+    timer_begin(h, K_HEADS_FWD, st);
     gemm_rc<T, 1, 1><<<dim3(cdiv(n, 64), 1), 256, 0, st>>>(op);
+    timer_end(h, K_HEADS_FWD, st);
     CK_LAUNCH("heads_fwd");
   }
   return 0;
@@ -153,68 +193,90 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     la.cpg = h->cfg.clip_pg_rho_threshold; la.ent_coef = h->cfg.entropy_coeff;
     la.partials = h->loss_part;
     T* dH = (T*)h->dH;
+    timer_begin(h, K_LOSS, st);
     loss_head_kernel<T><<<h->n_loss_wg, 256, 0, st>>>(la, dH, HPAD, dH + VCOL, HPAD, VCOL);
+    timer_end(h, K_LOSS, st);
     CK_LAUNCH("loss_head");
   }
   {
     HeadsDgrad<T> op{N, sw + sh.wht, (const T*)h->dH, h->z, (T*)h->dz};
+    timer_begin(h, K_HEADS_DGRAD, st);
     gemm_rc<T, 4, 1><<<dim3(cdiv(N, 64), HID / 64), 256, 0, st>>>(op);
+    timer_end(h, K_HEADS_DGRAD, st);
     CK_LAUNCH("heads_dgrad");
   }
   {
     FcDgrad<T> op{N, sw + sh.wfct, (const T*)h->dz, h->dy};
+    timer_begin(h, K_FC_DGRAD, st);
     gemm_rc<T, 4, 1><<<dim3(cdiv(N, 64), FLAT / 64), 256, 0, st>>>(op);
+    timer_end(h, K_FC_DGRAD, st);
     CK_LAUNCH("fc_dgrad");
   }
+  timer_begin(h, K_LN_BWD, st);
   ln_bwd_kernel<T><<<h->n_ln_wg, 256, 0, st>>>(h->dy, (const T*)h->act3, h->lnstat,
                                                 h->vecs + Vecs::lng, (T*)h->dact3, h->s_ln, N,
                                                 h->ln_fpw);
+  timer_end(h, K_LN_BWD, st);
   CK_LAUNCH("ln_bwd");
   {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3t, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
+    timer_begin(h, K_CONV3_DGRAD, st);
     gemm_rc<T, 4, 1><<<dim3(cdiv((long)N * P2, 64), 1), 256, 0, st>>>(op);
+    timer_end(h, K_CONV3_DGRAD, st);
     CK_LAUNCH("conv3_dgrad");
   }
   {
     Conv2Dgrad<T> op{4 * N * 64, N * 64, sw + sh.w2t, (const T*)h->dact2, (const T*)h->act1,
                      (T*)h->dact1};
+    timer_begin(h, K_CONV2_DGRAD, st);
     gemm_rc<T, 2, 1><<<dim3(4 * N, 1), 256, 0, st>>>(op);
+    timer_end(h, K_CONV2_DGRAD, st);
     CK_LAUNCH("conv2_dgrad");
   }
   // ---- weight gradients (split-M partial slabs) ----
   {
     HeadsWgrad<T> op{};
     op.M = N; op.dH = (const T*)h->dH; op.h = (const T*)h->h;
+    timer_begin(h, K_HEADS_WGRAD, st);
     gemm_wg<T, 16, 64, 1, 4><<<dim3(HID / 64, 1, h->sph.S), 256, 0, st>>>(op, h->s_h, h->s_bh,
                                                                           h->sph.mps);
+    timer_end(h, K_HEADS_WGRAD, st);
     CK_LAUNCH("heads_wgrad");
   }
   {
     FcWgrad<T> op{};
     op.M = N; op.dz = (const T*)h->dz; op.y = (const T*)h->y;
+    timer_begin(h, K_FC_WGRAD, st);
     gemm_wg<T, 64, 64, 2, 2><<<dim3(FLAT / 64, HID / 64, h->spfc.S), 256, 0, st>>>(
         op, h->s_fc, h->s_bfc, h->spfc.mps);
+    timer_end(h, K_FC_WGRAD, st);
     CK_LAUNCH("fc_wgrad");
   }
   {
     Conv3Wgrad<T> op{};
     op.M = N * P3; op.dy = (const T*)h->dact3; op.x = (const T*)h->act2;
+    timer_begin(h, K_CONV3_WGRAD, st);
     gemm_wg<T, 64, 64, 2, 2><<<dim3(K3 / 64, 1, h->sp3.S), 256, 0, st>>>(op, h->s_w3, h->s_b3,
                                                                          h->sp3.mps);
+    timer_end(h, K_CONV3_WGRAD, st);
     CK_LAUNCH("conv3_wgrad");
   }
   {
     Conv2Wgrad<T> op{};
     op.M = N * P2; op.dy = (const T*)h->dact2; op.x = (const T*)h->act1;
+    timer_begin(h, K_CONV2_WGRAD, st);
     gemm_wg<T, 64, 64, 2, 2><<<dim3(K2 / 64, 1, h->sp2.S), 256, 0, st>>>(op, h->s_w2, h->s_b2,
                                                                          h->sp2.mps);
+    timer_end(h, K_CONV2_WGRAD, st);
     CK_LAUNCH("conv2_wgrad");
   }
   {
     Conv1Wgrad<T> op{};
     op.M = N * P1; op.dy = (const T*)h->dact1; op.x = b->obs;
+    timer_begin(h, K_CONV1_WGRAD, st);
     gemm_wg<T, 32, 64, 2, 2><<<dim3(K1 / 64, 1, h->sp1.S), 256, 0, st>>>(op, h->s_w1, h->s_b1,
                                                                          h->sp1.mps);
+    timer_end(h, K_CONV1_WGRAD, st);
     CK_LAUNCH("conv1_wgrad");
   }
   // ---- slab reduction -> canonical grads, sum of squares, loss metrics, step += 1 ----
@@ -229,7 +291,9 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     ra.sumsq_part = h->sumsq_part; ra.loss_part = h->loss_part; ra.n_loss_part = h->n_loss_wg;
     ra.B = B; ra.T = Tl; ra.ent_coef = h->cfg.entropy_coeff; ra.metrics = h->metrics;
     ra.step = h->step;
+    timer_begin(h, K_REDUCE, st);
     reduce_grads_kernel<<<h->n_red_wg, 256, 0, st>>>(ra);
+    timer_end(h, K_REDUCE, st);
     CK_LAUNCH("reduce_grads");
   }
   return 0;
@@ -246,7 +310,9 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.inv_world = 1.f / (float)h->cfg.world_size;
   aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
   aa.cn = h->cn; aa.sh = h->sh;
+  timer_begin(h, K_ADAM, st);
   adam_kernel<T><<<h->n_red_wg, 256, 0, st>>>(aa);
+  timer_end(h, K_ADAM, st);
   CK_LAUNCH("adam");
   return 0;
 }
@@ -407,6 +473,10 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
 int impala_destroy(impala_learner* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
+  if (h->timer_ev) {
+    for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
+    delete[] h->timer_ev;
+  }
   if (h->ws) (void)hipFree(h->ws);
   delete h;
   return 0;
@@ -471,7 +541,9 @@ int impala_apply_update(impala_learner* h, void* stream) {
   CK(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->cfg.world_size > 1) {
+    timer_begin(h, K_SUMSQ, st);
     sumsq_kernel<<<h->n_red_wg, 256, 0, st>>>(h->grads, h->cn.total, h->sumsq_part);
+    timer_end(h, K_SUMSQ, st);
     CK_LAUNCH("sumsq");
   }
   return h->bf16 ? launch_adam<__bf16>(h, st) : launch_adam<float>(h, st);
@@ -483,6 +555,46 @@ int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
     return fail(IMPALA_E_STATE, "world_size > 1: use compute_grads + all-reduce + apply_update");
   if (int r = impala_compute_grads(h, b, stream)) return r;
   return impala_apply_update(h, stream);
+}
+
+int impala_kernel_count(void) { return K_COUNT; }
+const char* impala_kernel_name(int kernel_id) {
+  return (kernel_id >= 0 && kernel_id < K_COUNT) ? kKernelNames[kernel_id] : "";
+}
+
+int impala_timer_start(impala_learner* h, int kernel_id, int max_launches) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (kernel_id < -1 || kernel_id >= K_COUNT || max_launches < 0)
+    return fail(IMPALA_E_INVALID, "bad kernel id / capacity");
+  CK(hipSetDevice(h->device));
+  if (max_launches > h->timer_cap) {
+    if (h->timer_ev) {
+      for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
+      delete[] h->timer_ev;
+    }
+    h->timer_ev = new hipEvent_t[2 * max_launches];
+    for (int i = 0; i < 2 * max_launches; ++i) CK(hipEventCreate(&h->timer_ev[i]));
+    h->timer_cap = max_launches;
+  }
+  h->timer_kernel = kernel_id;
+  h->timer_n = 0;
+  return 0;
+}
+
+int impala_timer_read(impala_learner* h, float* total_ms, int* launches) {
+  if (!h || !total_ms || !launches) return fail(IMPALA_E_INVALID, "null argument");
+  CK(hipSetDevice(h->device));
+  float tot = 0.f;
+  for (int i = 0; i < h->timer_n; ++i) {
+    CK(hipEventSynchronize(h->timer_ev[2 * i + 1]));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, h->timer_ev[2 * i], h->timer_ev[2 * i + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *launches = h->timer_n;
+  h->timer_kernel = -1;
+  return 0;
 }
 
 int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,

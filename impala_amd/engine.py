@@ -155,6 +155,22 @@ class Engine:
         check(_lib.lib().impala_apply_update(self._h, stream_ptr(stream)), "impala_apply_update")
         self._updated()
 
+    # ------------------------------------------------------------------ live launch timer
+    @staticmethod
+    def kernel_names():
+        L = _lib.lib()
+        return [L.impala_kernel_name(i).decode() for i in range(L.impala_kernel_count())]
+
+    def timer_start(self, kernel: str, max_launches: int):
+        kid = self.kernel_names().index(kernel)
+        check(_lib.lib().impala_timer_start(self._h, kid, int(max_launches)), "impala_timer_start")
+
+    def timer_read(self):
+        """-> (summed launch duration in ms, launches) of the kernel armed by timer_start."""
+        ms, n = C.c_float(), C.c_int()
+        check(_lib.lib().impala_timer_read(self._h, C.byref(ms), C.byref(n)), "impala_timer_read")
+        return float(ms.value), int(n.value)
+
     def _updated(self):
         # the Adam kernel rewrote params AND this handle's kernel-layout weights
         self.model._version += 1

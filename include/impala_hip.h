@@ -121,6 +121,14 @@ int impala_compute_grads(impala_learner* h, const impala_batch* batch, void* str
  * global-norm clip and Adam. */
 int impala_apply_update(impala_learner* h, void* stream);
 
+/* Live launch timer (bench / roofline): record a hipEvent pair around each of the next
+ * `max_launches` launches of kernel `kernel_id` (see impala_kernel_name), on the stream it is
+ * launched on; impala_timer_read() synchronises on them and returns the summed duration. */
+int impala_kernel_count(void);
+const char* impala_kernel_name(int kernel_id);
+int impala_timer_start(impala_learner* h, int kernel_id, int max_launches);
+int impala_timer_read(impala_learner* h, float* total_ms, int* launches);
+
 /* Standalone batched V-trace, [B][L] row-major, L <= 64 (test / reuse entry point). */
 int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,
                   const float* rho_tm1, int B, int L, float lambda_, float clip_rho_threshold,

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (rocprofv3 CSVs under gpurun_out/prof_<tag>) into
+profiles/<tag>/: kernel_stats.csv (copied), summary.json and summary.md.
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB
+(x1024); on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled;
+FETCH and WRITE come from separate --pmc passes.
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+STEP_KERNELS = None
+
+
+def short(name):
+    n = name.split("(")[0]
+    for tag in ("Conv1Fwd", "Conv2Fwd", "Conv3Fwd", "FcFwd", "HeadsFwd", "HeadsDgrad", "FcDgrad",
+                "Conv3Dgrad", "Conv2Dgrad", "HeadsWgrad", "FcWgrad", "Conv3Wgrad", "Conv2Wgrad",
+                "Conv1Wgrad", "ln_fwd", "ln_bwd", "loss_head", "reduce_grads", "adam", "sumsq",
+                "pack_params", "conv_fwd", "conv_dgrad", "conv_wgrad", "fused"):
+        if tag in n:
+            return tag
+    return n[:60]
+
+
+def main(tag, src_root="gpurun_out", dst_root="profiles"):
+    src = os.path.join(src_root, f"prof_{tag}")
+    dst = os.path.join(dst_root, tag)
+    os.makedirs(dst, exist_ok=True)
+    stats = list(csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv"))))
+    shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    ctr = collections.defaultdict(lambda: collections.defaultdict(list))
+    for sub, cname in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        p = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            if r["Counter_Name"] == cname:
+                ctr[r["Kernel_Name"]][cname].append(float(r["Counter_Value"]))
+    out = []
+    total_ns = sum(float(r["TotalDurationNs"]) for r in stats)
+    for r in stats:
+        name = r["Name"]
+        c = ctr.get(name, {})
+        fetch = c.get("FETCH_SIZE")
+        write = c.get("WRITE_SIZE")
+        fb = 2 * 1024 * sum(fetch) / len(fetch) if fetch else None
+        wb = 1024 * sum(write) / len(write) if write else None
+        out.append({"kernel": short(name), "name": name[:200], "calls": int(r["Calls"]),
+                    "avg_us": float(r["AverageNs"]) / 1e3, "pct": float(r["Percentage"]),
+                    "hbm_read_bytes": fb, "hbm_write_bytes": wb,
+                    "hbm_bytes": (fb or 0) + (wb or 0) if (fb is not None or wb is not None) else None})
+    for k in ("bench_stats.json",):
+        p = os.path.join(src, k)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, k))
+    json.dump({"tag": tag, "total_kernel_ns": total_ns, "kernels": out}, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    with open(os.path.join(dst, "summary.md"), "w") as f:
+        f.write(f"# rocprofv3 summary `{tag}`\n\n`tools/profile.sh {tag}` = `rocprofv3 --kernel-trace --stats` "
+                "over `bench.py --steps 20 --warmup 3` (23 learner steps), then separate `--pmc FETCH_SIZE` "
+                "and `--pmc WRITE_SIZE` passes. HBM bytes per launch: FETCH_SIZE×1024×2 (gfx950 half-count "
+                "correction) + WRITE_SIZE×1024.\n\n")
+        f.write("| kernel | calls | avg µs | % time | HBM read MB | HBM write MB |\n|---|---|---|---|---|---|\n")
+        for o in out:
+            rd = f"{o['hbm_read_bytes'] / 1e6:.2f}" if o["hbm_read_bytes"] is not None else "-"
+            wr = f"{o['hbm_write_bytes'] / 1e6:.2f}" if o["hbm_write_bytes"] is not None else "-"
+            f.write(f"| {o['kernel']} | {o['calls']} | {o['avg_us']:.2f} | {o['pct']:.2f} | {rd} | {wr} |\n")
+    print(open(os.path.join(dst, "summary.md")).read())
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
