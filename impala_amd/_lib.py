@@ -25,7 +25,7 @@ EXPORTS = (
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
     "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
     "impala_apply_update", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
-    "impala_kernel_name", "impala_timer_start", "impala_timer_read",
+    "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
 )
 
 
@@ -70,6 +70,8 @@ def _declare(lib):
     lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
                                      C.c_float, C.c_float, C.c_float, C.c_float, _P, _P, _P,
                                      _P, _P, _P, _P, _P]
+    lib.impala_gather_rows.argtypes = [C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_size_t),
+                                       C.c_int, _P, C.c_int, _P]
     lib.impala_kernel_name.argtypes = [C.c_int]
     lib.impala_kernel_name.restype = C.c_char_p
     lib.impala_timer_start.argtypes = [_P, C.c_int, C.c_int]

@@ -557,6 +557,27 @@ int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
   return impala_apply_update(h, stream);
 }
 
+int impala_gather_rows(const void* const* src, void* const* dst, const size_t* row_bytes,
+                       int nfields, const int64_t* idx, int n, void* stream) {
+  if (nfields < 1 || nfields > 8 || n < 0 || !src || !dst || !row_bytes || (n > 0 && !idx))
+    return fail(IMPALA_E_INVALID, "bad gather arguments");
+  if (n == 0) return 0;
+  GatherArgs ga{};
+  for (int f = 0; f < nfields; ++f) {
+    if (!src[f] || !dst[f] || row_bytes[f] % 4 != 0)
+      return fail(IMPALA_E_INVALID, "gather: null field or row size not a multiple of 4");
+    ga.src[f] = (const char*)src[f];
+    ga.dst[f] = (char*)dst[f];
+    ga.row_bytes[f] = (long long)row_bytes[f];
+  }
+  ga.nfields = nfields;
+  ga.idx = idx;
+  ga.n = n;
+  gather_rows_kernel<<<dim3(n, nfields), 256, 0, (hipStream_t)stream>>>(ga);
+  CK_LAUNCH("gather_rows");
+  return 0;
+}
+
 int impala_kernel_count(void) { return K_COUNT; }
 const char* impala_kernel_name(int kernel_id) {
   return (kernel_id >= 0 && kernel_id < K_COUNT) ? kKernelNames[kernel_id] : "";

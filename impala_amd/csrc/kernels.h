@@ -532,3 +532,34 @@ __global__ void split_heads_kernel(const float* __restrict__ heads, int n, int A
   if (j < A) logits[(size_t)f * A + j] = heads[i];
   else if (j == VCOL) values[f] = heads[i];
 }
+
+// =========================================================================================
+// Replay gather: dst_f[i] = src_f[idx[i]] for up to 8 fields of fixed row size (bytes, multiple
+// of 4).  One workgroup per (row, field); 16-byte vector copies for the aligned bulk.
+// =========================================================================================
+struct GatherArgs {
+  const char* src[8];
+  char* dst[8];
+  long long row_bytes[8];
+  int nfields;
+  const int64_t* idx;
+  int n;
+};
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
+  const int i = blockIdx.x, f = blockIdx.y;
+  if (i >= a.n || f >= a.nfields) return;
+  const long long rb = a.row_bytes[f];
+  const char* s = a.src[f] + (size_t)a.idx[i] * rb;
+  char* d = a.dst[f] + (size_t)i * rb;
+  const bool al16 = ((((uintptr_t)s) | ((uintptr_t)d) | (uintptr_t)rb) & 15) == 0;
+  if (al16) {
+    const long long nv = rb >> 4;
+    for (long long v = threadIdx.x; v < nv; v += 256)
+      reinterpret_cast<f32x4*>(d)[v] = reinterpret_cast<const f32x4*>(s)[v];
+  } else {
+    const long long nw = rb >> 2;
+    for (long long v = threadIdx.x; v < nw; v += 256)
+      reinterpret_cast<float*>(d)[v] = reinterpret_cast<const float*>(s)[v];
+  }
+}

@@ -220,3 +220,18 @@ def loss_head(logits, values, actions, rewards, discounts, mu, entropy_coeff=0.0
                                       ptr(dv), ptr(met), ptr(adv), ptr(err), ptr(q), ptr(rho),
                                       stream_ptr(stream)), "impala_loss_head")
     return dict(dlogits=dl, dvalues=dv, metrics=met, adv=adv, err=err, q=q, rho=rho)
+
+
+def gather_rollouts(fields, idx, stream=None):
+    """HIP gather of replay rows: ``[f[idx] for f in fields]`` for device tensors whose first
+    dim indexes slots (impala_gather_rows)."""
+    n = int(idx.numel())
+    outs = [torch.empty((n,) + tuple(f.shape[1:]), dtype=f.dtype, device=f.device) for f in fields]
+    k = len(fields)
+    src = (C.c_void_p * k)(*[ptr(f) for f in fields])
+    dst = (C.c_void_p * k)(*[ptr(o) for o in outs])
+    rb = (C.c_size_t * k)(*[f[0].numel() * f.element_size() for f in fields])
+    idx = idx.to(torch.int64).contiguous()
+    check(_lib.lib().impala_gather_rows(src, dst, rb, k, ptr(idx), n, stream_ptr(stream)),
+          "impala_gather_rows")
+    return tuple(outs)

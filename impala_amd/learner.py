@@ -1,0 +1,153 @@
+"""ImpalaLearner — drop-in for ``agents/impala/learning.py:86-177`` on MI355X.
+
+Same constructor signature, same ``prepare`` / ``train_step`` / ``connect`` behaviour, same
+metric keys; ``_train_step`` is one HIP call (forward, V-trace, loss, backward, clip, Adam —
+``impala_train_step``) or, for data-parallel replicas, ``impala_compute_grads`` + an RCCL
+all-reduce of the flat gradient + ``impala_apply_update``.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Dict, Optional, Sequence, Tuple
+
+import torch
+
+from impala_amd import _lib
+from impala_amd.core import Learner
+from impala_amd.engine import Engine
+
+
+@dataclass
+class ImpalaAdam:
+    """Optimizer descriptor: torch.optim.Adam(lr, eps) of agents/impala/builder.py:43-44,
+    executed by the fused HIP clip+Adam kernel over the model's flat parameter buffer."""
+    lr: float = 1e-4
+    eps: float = 1e-5
+    betas: Tuple[float, float] = (0.9, 0.999)
+
+    @staticmethod
+    def from_torch(opt: torch.optim.Optimizer) -> "ImpalaAdam":
+        if not isinstance(opt, torch.optim.Adam):
+            raise TypeError("the HIP learner implements torch.optim.Adam only")
+        g = opt.param_groups[0]
+        if g.get("weight_decay", 0) or g.get("amsgrad", False) or g.get("maximize", False):
+            raise ValueError("weight_decay / amsgrad / maximize are not used by the reference")
+        return ImpalaAdam(lr=float(g["lr"]), eps=float(g["eps"]), betas=tuple(g["betas"]))
+
+
+def _collate(batch, device) -> Tuple[torch.Tensor, ...]:
+    """learning.py:123,142: list of B trajectories [s, a, r, g, mu] -> (B,T,...) device tensors.
+    Accepts an already collated tuple (DeviceReplayBuffer.sample) unchanged."""
+    if isinstance(batch, (tuple, list)) and len(batch) == 5 and isinstance(batch[0], torch.Tensor) \
+            and batch[0].dim() == 5:
+        return tuple(t if t.device == device else t.to(device, non_blocking=True) for t in batch)
+    fields = []
+    for j in range(5):
+        xs = [item[j] for item in batch]
+        if xs[0].device.type == "cpu":
+            host = torch.stack(xs)
+            if torch.cuda.is_available():
+                host = host.pin_memory()
+            t = host.to(device, non_blocking=True)
+        else:
+            t = torch.stack([x.to(device) for x in xs])
+        if j in (1, 2, 3) and t.dim() == 3:
+            t = t.squeeze(-1)
+        fields.append(t.contiguous())
+    obs, act, rew, disc, mu = fields
+    return obs, act.to(torch.int64), rew.float(), disc.float(), mu.float()
+
+
+class ImpalaLearner(Learner):
+    def __init__(self, model, replay_buffer, optimizer=None, batch_size: int = 8,
+                 max_grad_norm: float = 0.5, entropy_coeff: float = 0.01,
+                 learning_starts: Optional[int] = None, model_push_period: int = 4,
+                 rollout_length: int = 20, dtype: Optional[str] = None,
+                 process_group=None, world_size: Optional[int] = None):
+        self._model = model
+        self._replay_buffer = replay_buffer
+        if optimizer is None:
+            optimizer = ImpalaAdam()
+        elif isinstance(optimizer, torch.optim.Optimizer):
+            optimizer = ImpalaAdam.from_torch(optimizer)
+        self._optimizer = optimizer
+        self._batch_size = batch_size
+        self._max_grad_norm = max_grad_norm
+        self._entropy_coeff = entropy_coeff
+        self._learning_starts = learning_starts
+        self._model_push_period = model_push_period
+        self._rollout_length = rollout_length
+        self._pg = process_group
+        if world_size is None:
+            world_size = 1
+            if process_group is not None:
+                import torch.distributed as dist
+                world_size = dist.get_world_size(process_group)
+        self._world_size = int(world_size)
+        self._device = None
+        self._step_count = 0
+        self._step_counter = 0
+        self.can_train = True
+        self._engine = Engine(model, batch_size=batch_size, rollout_length=rollout_length,
+                              dtype=dtype, lr=optimizer.lr, eps=optimizer.eps,
+                              betas=optimizer.betas, max_grad_norm=max_grad_norm,
+                              entropy_coeff=entropy_coeff, world_size=self._world_size)
+        model._train_engine = self._engine
+
+    @property
+    def engine(self) -> Engine:
+        return self._engine
+
+    def device(self) -> torch.device:
+        if self._device is None:
+            self._device = self._model.flat.device
+        return self._device
+
+    def prepare(self):  # learning.py:116-117
+        self._replay_buffer.warm_up(self._learning_starts)
+
+    def train_step(self):  # learning.py:119-138
+        t0 = time.perf_counter()
+        _, batch, _ = self._replay_buffer.sample(self._batch_size)
+        batch = _collate(batch, self.device())
+        n_samples = self._batch_size * batch[0].shape[1]
+        t1 = time.perf_counter()
+        metrics = self._train_step(batch)
+        t2 = time.perf_counter()
+        update_time = 0
+        self._step_count += 1
+        self._step_counter = self._step_count
+        if self._step_count % self._model_push_period == 0:
+            start = time.perf_counter()
+            self._model.push()
+            update_time = time.perf_counter() - start
+        # same definitions (and units) as the reference, learning.py:133-137
+        metrics["debug/replay_sample_per_second"] = (n_samples / ((t1 - t0) * 1000))
+        metrics["debug/gradient_per_second"] = (n_samples / ((t2 - t1) * 1000))
+        metrics["debug/total_time"] = (time.perf_counter() - t0) * 1000
+        metrics["debug/forward_dt"] = (t2 - t1) * 1000 / self._batch_size
+        metrics["debug/update_time"] = update_time
+        return metrics
+
+    def _train_step(self, batch) -> Dict[str, torch.Tensor]:  # learning.py:140-177
+        e = self._engine
+        if self._world_size == 1:
+            e.train_step(*batch)
+        else:
+            import torch.distributed as dist
+            e.compute_grads(*batch)
+            dist.all_reduce(self._model.flat_grad, group=self._pg)
+            e.apply_update()
+        m = e.metrics.clone()  # device scalars; float(v) synchronises lazily
+        return {name: m[i] for i, name in enumerate(_lib.METRIC_NAMES)}
+
+    # ---------------------------------------------------------------- checkpoint
+    def optimizer_state(self) -> dict:
+        return {"step": int(self._engine.metrics[7].item()), "exp_avg": self._engine.exp_avg.clone(),
+                "exp_avg_sq": self._engine.exp_avg_sq.clone()}
+
+    def load_optimizer_state(self, st: dict) -> None:
+        self._engine.exp_avg.copy_(st["exp_avg"])
+        self._engine.exp_avg_sq.copy_(st["exp_avg_sq"])
+        self._engine.set_step(int(st["step"]))

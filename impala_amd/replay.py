@@ -1,0 +1,165 @@
+"""Rollout storage feeding the learner.
+
+Reference: ``agents/impala/builder.py:30-36`` builds ``ReplayBuffer(CircularBuffer(1000),
+UniformSampler())``; actors ``async_append`` one trajectory ``[s, a, r, discount, logits]``
+(``agents/impala/learning.py:71-80``); the learner calls ``warm_up(learning_starts)`` and
+``sample(batch_size) -> (keys, batch, probs)`` (``learning.py:116-121``).
+
+Two implementations with that interface:
+
+* ``ReplayBuffer``        host memory, returns the reference's list-of-trajectories batch.
+* ``DeviceReplayBuffer``  MI355X-first: the circular store lives in HBM (1000 x 247 KB =
+  247 MB of 288 GB); an appended trajectory is written into a pinned-host staging ring and
+  copied to its HBM slot with an async H2D on a side stream, so each trajectory crosses PCIe
+  once however often it is replayed; ``sample`` gathers B slots on the device with the HIP
+  gather kernel and returns the collated ``(B,T,...)`` batch already resident in HBM.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+class ReplayBuffer:
+    """CircularBuffer + UniformSampler semantics on the host (reference-compatible)."""
+
+    def __init__(self, capacity: int = 1000, seed: Optional[int] = None):
+        self.capacity = int(capacity)
+        self._data: List[Optional[list]] = [None] * self.capacity
+        self._keys = np.zeros(self.capacity, dtype=np.int64)
+        self._next_key = 0
+        self._size = 0
+        self._cursor = 0
+        self._rng = np.random.default_rng(seed)
+        self._cv = threading.Condition()
+
+    def __len__(self):
+        return self._size
+
+    def reset(self, seed: Optional[int] = None):
+        self._rng = np.random.default_rng(seed)
+
+    def append(self, item: Sequence[torch.Tensor]) -> int:
+        with self._cv:
+            slot = self._cursor
+            self._data[slot] = list(item)
+            key = self._next_key
+            self._keys[slot] = key
+            self._next_key += 1
+            self._cursor = (self._cursor + 1) % self.capacity
+            self._size = min(self._size + 1, self.capacity)
+            self._cv.notify_all()
+            return key
+
+    def extend(self, items) -> List[int]:
+        return [self.append(x) for x in items]
+
+    async def async_append(self, item):
+        return self.append(item)
+
+    def warm_up(self, learning_starts: Optional[int] = None, timeout: float = 240.0) -> None:
+        """Block until ``learning_starts`` items are stored (rlmeta ReplayBuffer.warm_up)."""
+        if not learning_starts:
+            return
+        need = min(int(learning_starts), self.capacity)
+        deadline = time.monotonic() + timeout
+        with self._cv:
+            while self._size < need:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise TimeoutError(f"replay warm_up: {self._size}/{need} after {timeout}s")
+                self._cv.wait(left)
+
+    def _indices(self, batch_size: int) -> np.ndarray:
+        if self._size == 0:
+            raise RuntimeError("sample from an empty replay buffer")
+        replace = batch_size > self._size
+        return self._rng.choice(self._size, size=batch_size, replace=replace)
+
+    def sample(self, batch_size: int):
+        with self._cv:
+            idx = self._indices(batch_size)
+            batch = [self._data[i] for i in idx]
+            keys = self._keys[idx].copy()
+        probs = np.full(batch_size, 1.0 / self._size)
+        return keys, batch, probs
+
+
+class DeviceReplayBuffer(ReplayBuffer):
+    """HBM-resident circular rollout store with pinned-host staging (see module doc)."""
+
+    def __init__(self, capacity: int = 1000, rollout_length: int = 20, num_actions: int = 15,
+                 device="cuda", seed: Optional[int] = None, staging_slots: int = 64):
+        super().__init__(capacity, seed)
+        self.device = torch.device(device)
+        C, T, A = self.capacity, int(rollout_length), int(num_actions)
+        self.T, self.A = T, A
+        d = self.device
+        self.obs = torch.empty(C, T, 3, 64, 64, dtype=torch.uint8, device=d)
+        self.act = torch.zeros(C, T, dtype=torch.int64, device=d)
+        self.rew = torch.zeros(C, T, dtype=torch.float32, device=d)
+        self.disc = torch.zeros(C, T, dtype=torch.float32, device=d)
+        self.mu = torch.zeros(C, T, A, dtype=torch.float32, device=d)
+        S = int(staging_slots)
+        pin = torch.cuda.is_available()
+        self._st_obs = torch.empty(S, T, 3, 64, 64, dtype=torch.uint8, pin_memory=pin)
+        self._st_small = torch.empty(S, T, 3 + A, dtype=torch.float32, pin_memory=pin)
+        self._st_act = torch.empty(S, T, dtype=torch.int64, pin_memory=pin)
+        self._st_events = [None] * S
+        self._st_next = 0
+        self._stream = torch.cuda.Stream(device=d)
+        self._pending: List[torch.cuda.Event] = []
+
+    def append(self, item: Sequence[torch.Tensor]) -> int:
+        s, a, r, g, mu = item
+        T = self.T
+        with self._cv:
+            j = self._st_next
+            self._st_next = (j + 1) % len(self._st_events)
+            ev = self._st_events[j]
+            if ev is not None:
+                ev.synchronize()  # staging slot reuse: its previous H2D has finished
+            self._st_obs[j].copy_(s.reshape(T, 3, 64, 64))
+            self._st_act[j].copy_(a.reshape(T))
+            sm = self._st_small[j]
+            sm[:, 0].copy_(r.reshape(T))
+            sm[:, 1].copy_(g.reshape(T))
+            sm[:, 3:].copy_(mu.reshape(T, self.A))
+            slot = self._cursor
+            with torch.cuda.stream(self._stream):
+                self.obs[slot].copy_(self._st_obs[j], non_blocking=True)
+                self.act[slot].copy_(self._st_act[j], non_blocking=True)
+                small = sm.to(self.device, non_blocking=True)
+                self.rew[slot].copy_(small[:, 0])
+                self.disc[slot].copy_(small[:, 1])
+                self.mu[slot].copy_(small[:, 3:])
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+            self._st_events[j] = ev
+            self._pending.append(ev)
+            key = self._next_key
+            self._keys[slot] = key
+            self._next_key += 1
+            self._cursor = (slot + 1) % self.capacity
+            self._size = min(self._size + 1, self.capacity)
+            self._cv.notify_all()
+            return key
+
+    def sample(self, batch_size: int, stream=None):
+        """-> (keys, (obs, act, rew, disc, mu) collated on the device, probs)."""
+        from impala_amd.engine import gather_rollouts
+        with self._cv:
+            idx = self._indices(batch_size)
+            keys = self._keys[idx].copy()
+            pending, self._pending = self._pending, []
+        cur = torch.cuda.current_stream(self.device) if stream is None else stream
+        for ev in pending:  # the learner's stream waits for every staged H2D
+            cur.wait_event(ev)
+        idx_t = torch.from_numpy(idx.astype(np.int64)).to(self.device, non_blocking=True)
+        batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx_t, stream)
+        probs = np.full(batch_size, 1.0 / self._size)
+        return keys, batch, probs

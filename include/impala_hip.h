@@ -121,6 +121,12 @@ int impala_compute_grads(impala_learner* h, const impala_batch* batch, void* str
  * global-norm clip and Adam. */
 int impala_apply_update(impala_learner* h, void* stream);
 
+/* Replay gather (agents/impala/builder.py:30-36 UniformSampler.sample + learning.py:121-123
+ * collate/H2D, done in HBM): for each field f < nfields (<= 8), copy row idx[i] of src[f] to
+ * row i of dst[f], rows of row_bytes[f] bytes (multiple of 4); idx is a device int64 [n]. */
+int impala_gather_rows(const void* const* src, void* const* dst, const size_t* row_bytes,
+                       int nfields, const int64_t* idx, int n, void* stream);
+
 /* Live launch timer (bench / roofline): record a hipEvent pair around each of the next
  * `max_launches` launches of kernel `kernel_id` (see impala_kernel_name), on the stream it is
  * launched on; impala_timer_read() synchronises on them and returns the summed duration. */

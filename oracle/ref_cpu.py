@@ -187,6 +187,24 @@ def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
     return metrics
 
 
+def local_grads(model: nn.Module, batch_collated, entropy_coeff: float = 0.01) -> np.ndarray:
+    """Loss + backward only (learning.py:141-160), no clip / Adam: the per-replica gradient of
+    the data-parallel learner (mean over the LOCAL batch)."""
+    model.zero_grad(set_to_none=True)
+    s, a, r, discount_t, pi_ref = batch_collated
+    pi, values = model.forward(s.flatten(0, 1))
+    pi = torch.distributions.Categorical(logits=pi.reshape(s.shape[0], s.shape[1], -1))
+    values = values.reshape(s.shape[0], s.shape[1])
+    pim = torch.distributions.Categorical(logits=pi_ref)
+    rho = torch.exp(pi.log_prob(a) - pim.log_prob(a))
+    adv, err, _ = batched_vtrace(values[:, :-1], values[:, 1:], r[:, :-1], discount_t[:, :-1],
+                                 rho[:, :-1])
+    loss = -(pi.log_prob(a)[:, :-1] * adv).mean() + err.pow(2).mean() \
+        - entropy_coeff * pi.entropy().mean()
+    loss.backward()
+    return flat_grads(model)
+
+
 def make_optimizer(model: nn.Module, lr: float = 1e-4, eps: float = 1e-5):
     """agents/impala/builder.py:43-44."""
     return torch.optim.Adam(model.parameters(), lr=lr, eps=eps)
@@ -242,7 +260,7 @@ def loss_from_outputs(logits, values, act, rew, disc, mu, entropy_coeff=0.01,
     loss.backward()
     kl = torch.distributions.kl_divergence(pi, pim).mean()
     out = dict(adv=adv.detach().numpy(), err=err.detach().numpy(), q=q.detach().numpy(),
-               rho=rho.detach().numpy(), loss=float(loss.detach()), pg=float(pg), td=float(vl),
-               entropy=float(ent), kl=float(kl), ratio=float(rho.mean()),
+               rho=rho.detach().numpy(), loss=float(loss.detach()), pg=float(pg.detach()), td=float(vl.detach()),
+               entropy=float(ent.detach()), kl=float(kl.detach()), ratio=float(rho.detach().mean()),
                dlogits=lg.grad.numpy().copy(), dvalues=v.grad.numpy().copy())
     return out

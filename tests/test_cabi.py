@@ -1,0 +1,73 @@
+"""The C-ABI library loads here (no GPU) and exports every symbol include/impala_hip.h
+declares; host-only entry points and argument validation work without a device."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from impala_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "impala_hip.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(impala_\w+)\s*\(", src)))
+
+
+def test_header_declares_what_the_binding_expects():
+    assert _declared() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\b(impala_\w+)\b", out))
+    for name in _declared():
+        assert name in exported, name
+        assert hasattr(lib, name)
+
+
+def test_host_only_entry_points():
+    lib = _lib.lib()
+    assert lib.impala_abi_version() == 1
+    assert _lib.param_count(15) == 344496
+    assert _lib.param_count(6) == 344496 - 9 * 257
+    cfg = _lib.default_config()
+    assert (cfg.batch_size, cfg.rollout_length, cfg.num_actions) == (8, 20, 15)
+    assert abs(cfg.lr - 1e-4) < 1e-9 and abs(cfg.adam_eps - 1e-5) < 1e-12
+    assert abs(cfg.max_grad_norm - 0.5) < 1e-9 and abs(cfg.entropy_coeff - 0.01) < 1e-9
+    names = [lib.impala_kernel_name(i).decode() for i in range(lib.impala_kernel_count())]
+    assert "conv1_wgrad" in names and "adam" in names and len(names) == len(set(names))
+
+
+@pytest.mark.parametrize("field,value", [("batch_size", 0), ("rollout_length", 1),
+                                         ("rollout_length", 65), ("num_actions", 16),
+                                         ("num_actions", 0), ("dtype", 7), ("world_size", 0)])
+def test_create_rejects_bad_config_without_touching_the_device(field, value):
+    lib = _lib.lib()
+    cfg = _lib.default_config()
+    setattr(cfg, field, value)
+    h = C.c_void_p()
+    st = lib.impala_create(C.byref(cfg), 0, C.byref(h))
+    assert st in (1001, 1003)
+    assert not h.value
+    assert lib.impala_last_error().decode()
+
+
+def test_kernel_entry_points_validate_before_launch():
+    lib = _lib.lib()
+    assert lib.impala_vtrace(None, None, None, None, None, 4, 0, 1.0, 1.0, 1.0, None, None,
+                             None, None) == 1001
+    assert lib.impala_vtrace(None, None, None, None, None, 4, 65, 1.0, 1.0, 1.0, None, None,
+                             None, None) == 1001
+    assert lib.impala_loss_head(*([None] * 6), 2, 1, 15, 0.01, 1.0, 1.0, 1.0,
+                                *([None] * 8)) == 1001
+    assert lib.impala_train_step(None, None, None) == 1001
+    assert lib.impala_forward(None, None, 1, None, None, None) == 1001
+    assert lib.impala_gather_rows(None, None, None, 0, None, 0, None) == 1001

@@ -1,0 +1,146 @@
+"""GPU: the reference-shaped host API (ImpalaBuilder / ImpalaLearner / replay / model.act /
+push / checkpoint) drives the HIP path and agrees with the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+class _FixedReplay:
+    def __init__(self, batches):
+        self.batches = list(batches)
+        self.warm = None
+
+    def warm_up(self, n):
+        self.warm = n
+
+    def sample(self, b):
+        return None, self.batches.pop(0), None
+
+
+def _cfg(**over):
+    from impala_amd.config import load_config
+    o = {"learner": {"dtype": "fp32"}}
+    for k, v in over.items():
+        o.setdefault(k, {}).update(v)
+    return load_config(o)
+
+
+def test_builder_learner_step_matches_oracle():
+    _dev()
+    from impala_amd.builder import ImpalaBuilder
+    B, T = 4, 20
+    cfg = _cfg(agent={"batch_size": B})
+    b = ImpalaBuilder(cfg)
+    torch.manual_seed(0)
+    model = b.make_network(None)
+    flat0 = model.flat.cpu().numpy().copy()
+    batch_np = ref_cpu.synthetic_batch(B, T, 15, seed=3)
+    rb = _FixedReplay([ref_cpu.to_trajectories(*batch_np) for _ in range(4)])
+    learner = b.make_learner(model, rb)
+    learner.prepare()
+    assert rb.warm == cfg.agent.learning_starts
+    ref = ref_cpu.RefModel(15)
+    ref_cpu.load_flat(ref, flat0)
+    opt = ref_cpu.make_optimizer(ref)
+    for step in range(4):
+        met = learner.train_step()
+        exp = ref_cpu.train_step(ref, opt, ref_cpu.to_trajectories(*batch_np))
+        for k in ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl",
+                  "train/ratio", "train/grad_norm"):
+            np.testing.assert_allclose(float(met[k]), float(exp[k]), rtol=2e-4, atol=1e-6,
+                                       err_msg=f"{k} step {step}")
+        for k in ("debug/replay_sample_per_second", "debug/gradient_per_second",
+                  "debug/total_time", "debug/forward_dt", "debug/update_time"):
+            assert k in met
+    np.testing.assert_allclose(model.flat.cpu().numpy(), ref_cpu.flat_params(ref), atol=5e-6)
+    # push every model_push_period (4) steps: the actor copy now equals the learner weights
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(b.actor_model.flat.cpu().numpy(), model.flat.cpu().numpy())
+
+
+def test_device_replay_gather_and_learn():
+    dev = _dev()
+    from impala_amd.replay import DeviceReplayBuffer
+    T, A = 20, 15
+    rb = DeviceReplayBuffer(capacity=16, rollout_length=T, num_actions=A, device=dev, seed=5)
+    trajs = []
+    for i in range(20):
+        obs, act, rew, disc, mu = ref_cpu.synthetic_batch(1, T, A, seed=100 + i)
+        item = [torch.from_numpy(obs[0]), torch.from_numpy(act[0]).unsqueeze(-1),
+                torch.from_numpy(rew[0]).unsqueeze(-1), torch.from_numpy(disc[0]).unsqueeze(-1),
+                torch.from_numpy(mu[0])]
+        rb.append(item)
+        trajs.append(item)
+    rb.warm_up(10)
+    keys, batch, probs = rb.sample(8)
+    torch.cuda.synchronize()
+    assert len(set(keys.tolist())) == 8 and all(k >= 4 for k in keys)
+    for j, k in enumerate(keys.tolist()):
+        src = trajs[k]
+        np.testing.assert_array_equal(batch[0][j].cpu().numpy(), src[0].numpy())
+        np.testing.assert_array_equal(batch[1][j].cpu().numpy(), src[1].squeeze(-1).numpy())
+        np.testing.assert_array_equal(batch[2][j].cpu().numpy(), src[2].squeeze(-1).numpy())
+        np.testing.assert_array_equal(batch[4][j].cpu().numpy(), src[4].numpy())
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="bf16", seed=0)
+    ln = ImpalaLearner(m, rb, batch_size=8, rollout_length=T, learning_starts=10)
+    ln.prepare()
+    for _ in range(3):
+        met = ln.train_step()
+    assert np.isfinite(float(met["train/loss"]))
+
+
+def test_model_act_and_checkpoint_roundtrip(tmp_path):
+    dev = _dev()
+    from impala_amd.model import AtariPPOModel
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=1)
+    obs = torch.randint(0, 256, (130, 3, 64, 64), dtype=torch.uint8)
+    a, lg, v = m.act(obs, torch.tensor([True]))
+    assert a.shape == (130, 1) and lg.shape == (130, 15) and v.shape == (130, 1)
+    assert torch.equal(a.squeeze(-1), lg.argmax(-1))
+    a2, _, _ = m.act(obs, torch.tensor([False]))
+    assert a2.shape == (130, 1) and int(a2.max()) < 15
+    torch.save(m.state_dict(), tmp_path / "ck.pt")
+    m2 = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=2)
+    m2.load_state_dict(torch.load(tmp_path / "ck.pt", weights_only=True))
+    lg1, v1 = m(obs.to(dev))
+    lg2, v2 = m2(obs.to(dev))
+    torch.testing.assert_close(lg1, lg2, rtol=0, atol=0)
+    torch.testing.assert_close(v1, v2, rtol=0, atol=0)
+
+
+def test_optimizer_state_resume_matches_uninterrupted():
+    dev = _dev()
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    batches = [[torch.from_numpy(x).to(dev) for x in ref_cpu.synthetic_batch(2, 20, 15, seed=s)]
+               for s in range(4)]
+
+    def run(bs, model=None, state=None):
+        m = model or AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+        ln = ImpalaLearner(m, _FixedReplay([tuple(b) for b in bs]), batch_size=2)
+        if state is not None:
+            ln.load_optimizer_state(state)
+        for _ in range(len(bs)):
+            ln.train_step()
+        return m, ln
+
+    m_full, _ = run(batches)
+    m_a, ln_a = run(batches[:2])
+    st = ln_a.optimizer_state()
+    sd = {k: v.clone() for k, v in m_a.state_dict().items()}
+    m_b = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=9)
+    m_b.load_state_dict(sd)
+    m_b, _ = run(batches[2:], m_b, st)
+    torch.testing.assert_close(m_b.flat, m_full.flat, rtol=0, atol=0)

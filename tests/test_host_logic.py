@@ -1,0 +1,133 @@
+"""Host-side logic on CPU: model parameter layout / init vs the reference fixtures, config
+surface, replay semantics, collate, optimizer descriptor, actor trajectory format."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from impala_amd.config import load_config
+from impala_amd.model import AtariPPOModel, param_count, param_specs
+from impala_amd.replay import ReplayBuffer
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_param_specs_match_reference_state_dict():
+    d = np.load(os.path.join(G, "model_forward.npz"), allow_pickle=False)
+    assert [k for k, _ in param_specs(15)] == [str(k) for k in d["keys"]]
+    assert param_count(15) == 344496
+
+
+def test_model_views_and_reference_init_on_cpu():
+    d = np.load(os.path.join(G, "model_forward.npz"), allow_pickle=False)
+    m = AtariPPOModel((3, 64, 64), 15, device="cpu", seed=0)
+    np.testing.assert_array_equal(m.flat.numpy(), d["params"])
+    sd = m.state_dict()
+    assert list(sd.keys()) == [str(k) for k in d["keys"]]
+    # parameters and grads are views of the flat buffers
+    w = m.model.body.body[0].weight if hasattr(m.model.body.body, "__getitem__") else \
+        getattr(m.model.body.body, "0").weight
+    assert w.data_ptr() == m.flat.data_ptr()
+    assert w.grad.data_ptr() == m.flat_grad.data_ptr()
+    # load_state_dict round trip writes through to the flat buffer
+    sd2 = {k: torch.full_like(v, 0.5) for k, v in sd.items()}
+    v0 = m._version
+    m.load_state_dict(sd2)
+    assert torch.all(m.flat == 0.5) and m._version > v0
+
+
+def test_forward_refuses_cpu():
+    m = AtariPPOModel((3, 64, 64), 15, device="cpu", seed=0)
+    with pytest.raises(RuntimeError, match="HIP path only"):
+        m(torch.zeros(1, 3, 64, 64, dtype=torch.uint8))
+
+
+def test_model_rejects_non_64x64_observations():
+    with pytest.raises(ValueError):
+        AtariPPOModel((3, 84, 84), 15, device="cpu")
+
+
+def test_config_surface_matches_reference_keys():
+    c = load_config()
+    assert c.agent.batch_size == 8 and c.agent.rollout_length == 20
+    assert c.agent.learning_starts == 500  # deploy/local.yaml overlay
+    assert c.agent.optimizer.lr == 1e-4 and c.agent.optimizer.eps == 1e-5
+    assert c.agent.max_grad_norm == 40 and c.training.steps_per_epoch == 1000
+    assert c.distributed.train_device == "cuda:0"
+    c2 = load_config({"agent": {"batch_size": 64}, "learner": {"dtype": "fp32"}})
+    assert c2.agent.batch_size == 64 and c2.learner.dtype == "fp32"
+
+
+def _traj(T=20, A=15, fill=0):
+    return [torch.full((T, 3, 64, 64), fill, dtype=torch.uint8),
+            torch.zeros(T, 1, dtype=torch.int64), torch.zeros(T, 1), torch.zeros(T, 1),
+            torch.zeros(T, A)]
+
+
+def test_replay_circular_uniform_sampling():
+    rb = ReplayBuffer(capacity=5, seed=1)
+    for i in range(7):
+        rb.append(_traj(fill=i))
+    assert len(rb) == 5
+    keys, batch, probs = rb.sample(4)
+    assert len(set(keys.tolist())) == 4  # without replacement
+    assert all(k >= 2 for k in keys)     # oldest two overwritten
+    assert np.allclose(probs, 0.2)
+    fills = sorted(int(b[0][0, 0, 0, 0]) for b in batch)
+    assert all(2 <= f <= 6 for f in fills)
+
+
+def test_replay_warm_up_times_out():
+    rb = ReplayBuffer(capacity=4)
+    rb.append(_traj())
+    rb.warm_up(1)
+    with pytest.raises(TimeoutError):
+        rb.warm_up(3, timeout=0.05)
+
+
+def test_collate_list_of_trajectories_on_cpu():
+    from impala_amd.learner import _collate
+    batch = [_traj(fill=i) for i in range(3)]
+    obs, act, rew, disc, mu = _collate(batch, torch.device("cpu"))
+    assert obs.shape == (3, 20, 3, 64, 64) and obs.dtype == torch.uint8
+    assert act.shape == (3, 20) and act.dtype == torch.int64
+    assert rew.shape == (3, 20) and disc.shape == (3, 20) and mu.shape == (3, 20, 15)
+    assert int(obs[2, 0, 0, 0, 0]) == 2
+
+
+def test_adam_descriptor_from_torch():
+    from impala_amd.learner import ImpalaAdam
+    p = torch.nn.Parameter(torch.zeros(3))
+    a = ImpalaAdam.from_torch(torch.optim.Adam([p], lr=3e-4, eps=1e-5))
+    assert a.lr == 3e-4 and a.eps == 1e-5 and a.betas == (0.9, 0.999)
+    with pytest.raises(TypeError):
+        ImpalaAdam.from_torch(torch.optim.SGD([p], lr=0.1))
+
+
+def test_actor_make_replay_format():
+    from impala_amd.builder import ImpalaActor
+
+    class _RB:
+        items = []
+
+        def append(self, x):
+            self.items.append(x)
+
+    rb = _RB()
+    actor = ImpalaActor(model=None, replay_buffer=rb, rollout_length=3)
+    actor._last_transition = (torch.zeros(3, 64, 64, dtype=torch.uint8), 0.0, False)
+    for t in range(3):
+        nxt = (torch.full((3, 64, 64), t + 1, dtype=torch.uint8), 1.0, t == 1)
+        actor.observe((torch.tensor([t]), {"logpi": torch.zeros(15)}), nxt)
+    s, a, r, g, mu = rb.items[0]
+    assert s.shape == (3, 3, 64, 64) and a.shape == (3, 1) and r.shape == (3, 1)
+    assert mu.shape == (3, 15) and a.dtype == torch.int64
+    np.testing.assert_allclose(g.squeeze(-1).numpy(), [0.99, 0.0, 0.99])  # (not done)*gamma
+
+
+def test_shard_range():
+    from impala_amd.distributed import shard_range
+    assert shard_range(512, 8, 3) == (192, 256)
+    with pytest.raises(ValueError):
+        shard_range(10, 4, 0)
