@@ -78,6 +78,36 @@ def cpu_baseline(B, T, A, seconds):
                       f"{threads} threads, {cpu}) after 2 warm-up; median step {med * 1e3:.1f} ms"}
 
 
+PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3Fwd",
+                 "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "heads_dgrad": "HeadsDgrad",
+                 "fc_dgrad": "FcDgrad", "conv3_dgrad": "Conv3Dgrad", "conv2_dgrad": "Conv2Dgrad",
+                 "heads_wgrad": "HeadsWgrad", "fc_wgrad": "FcWgrad", "conv3_wgrad": "Conv3Wgrad",
+                 "conv2_wgrad": "Conv2Wgrad", "conv1_wgrad": "Conv1Wgrad"}
+
+
+def profiled_traffic(kernel, dtype):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>/summary.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+    root = os.path.join(HERE, "profiles")
+    if not os.path.isdir(root):
+        return None, None
+    best = None
+    for tag in sorted(os.listdir(root)):
+        p = os.path.join(root, tag, "summary.json")
+        if not os.path.exists(p):
+            continue
+        try:
+            js = json.load(open(p))
+        except Exception:
+            continue
+        if js.get("dtype", "bf16") != dtype:
+            continue
+        for k in js.get("kernels", []):
+            if k.get("kernel") == PROFILE_NAMES.get(kernel) and k.get("hbm_bytes"):
+                best = (float(k["hbm_bytes"]), tag)
+    return best if best else (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,7 +157,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    rk = args.roofline_kernel or ("conv2_wgrad" if False else None)
+    rk = args.roofline_kernel
     # dominant kernel: pick the one with the largest measured time in a short probe
     probe = {}
     if rk is None:
@@ -166,6 +196,9 @@ def main():
     k_avg_ms = k_ms / max(k_n, 1)
     achieved = FLOPS_PER_FRAME[rk] * B * T / (k_avg_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
+    traffic, tsrc = profiled_traffic(rk, args.dtype)
+    traffic_src = (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+WRITE_SIZE, "
+                   "bytes per launch)") if tsrc else None
     out = {
         "metric": "learner env-frames/sec (IMPALA procgen T=20 B=64) at 1/2/4/8 MI355X",
         "value": round(value, 1), "unit": "env-frames/s", "n_gpus": world, "steps": args.steps,
@@ -178,7 +211,8 @@ def main():
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": rk, "achieved": round(achieved, 2),
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                     "traffic": None, "avg_launch_us": round(k_avg_ms * 1e3, 2),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "avg_launch_us": round(k_avg_ms * 1e3, 2),
                      "launches": k_n},
         "step_tflops": round(STEP_FLOPS_PER_FRAME * value / world / 1e12, 2),
     }
