@@ -161,13 +161,14 @@ def main():
     # dominant kernel: pick the one with the largest measured time in a short probe
     probe = {}
     if rk is None:
-        for kname in FLOPS_PER_FRAME:
+        for kname in eng.kernel_names():
             eng.timer_start(kname, 3)
             for _ in range(3):
                 step()
             ms, n = eng.timer_read()
-            probe[kname] = ms / max(n, 1)
-        rk = max(probe, key=probe.get)
+            if n:
+                probe[kname] = ms / n
+        rk = max((k for k in probe if k in FLOPS_PER_FRAME), key=probe.get)
     torch.cuda.synchronize()
 
     eng.timer_start(rk, args.steps)

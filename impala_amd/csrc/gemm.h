@@ -56,23 +56,59 @@ __global__ __launch_bounds__(256) void gemm_rc(const Op op) {
   }
 }
 
-template <typename T, int BR, int BC, int WR, int WC, class Op>
-__global__ __launch_bounds__(256) void gemm_wg(const Op op, float* __restrict__ slab,
-                                               float* __restrict__ slab_bias, int m_per_split) {
+// LDS fragment read along the k (= m) dimension of a row-major [m][col] tile:
+//  bf16: two ds_read_b64_tr_b16 (hardware transpose, 4 rows x 16 cols per 16-lane group):
+//        lane l gets S[k0 + 8*(l>>4) + j][c0 + (l&15)], j = 0..7.
+//  f32 : four ds_read_b32 for the lane-permuted k of Frag<float>: S[k0 + 4*(l>>4) + j][...].
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
+
+DEV Frag<__bf16>::vec lds_frag_k(const __bf16* tile, int ld, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const __bf16* a0 = tile + (8 * g + q) * ld + 4 * pp;
+  const bf16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+  const bf16x4_t y = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0 + 4 * ld));
+  Frag<__bf16>::vec v;
+  v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+  v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
+  return v;
+}
+DEV Frag<float>::vec lds_frag_k(const float* tile, int ld, int lane) {
+  const float* a0 = tile + 4 * (lane >> 4) * ld + (lane & 15);
+  return f32x4{a0[0], a0[ld], a0[2 * ld], a0[3 * ld]};
+}
+
+// Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split
+// blockIdx.z.  X is a row-major [M][x_ld] matrix (the channels-last output gradient); Y is a
+// gather (im2col of the layer input) returning 16-byte runs along c.  Each BM-row chunk of both
+// is staged row-major into LDS with 16-byte stores and the MFMA fragments are read along m
+// with the hardware transpose read (bf16).  A workgroup holds G independent 4-wave groups
+// working on interleaved chunks (G x the loads in flight per CU without more partial slabs);
+// their accumulators are summed in a fixed order at the end.  Output: fp32 partial slab
+// [split][R][C] (+ per-split bias sums).
+template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op>
+__global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restrict__ slab,
+                                                   float* __restrict__ slab_bias,
+                                                   int m_per_split) {
   using F = Frag<T>;
-  constexpr int BMK = 32;
-  constexpr int LD = BMK + 16 / (int)sizeof(T);  // +16 B per row
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int LDX = BR + VEC, LDY = BC + VEC;
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
-  static_assert(WR * WC == 4, "4 waves");
-  static_assert(TRW >= 1 && TCW >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) T Xs[BR * LD];
-  __shared__ __attribute__((aligned(16))) T Ys[BC * LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NACC = TRW * TCW * 4;
+  constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per group
+  static_assert(WR * WC == 4, "4 waves per group");
+  static_assert(TRW >= 1 && TCW >= 1 && BR % 16 == 0 && BC % 16 == 0, "tile");
+  static_assert(BM % F::KSTEP == 0, "chunk");
+  static_assert((size_t)STAGE * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
+                "LDS reuse for the group reduction");
+  __shared__ __attribute__((aligned(16))) T smem[STAGE * G];
+  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  T* Xs = smem + grp * STAGE;
+  T* Ys = Xs + BM * LDX;
   const int c0 = blockIdx.x * BC, r0 = blockIdx.y * BR, split = blockIdx.z;
   const int m_beg = split * m_per_split;
   const int m_end = min(op.M, m_beg + m_per_split);
   const int wr = wave / WC, wc = wave % WC;
-  const int kl = F::KPL * (lane >> 4);
   const bool do_bias = slab_bias != nullptr && blockIdx.x == 0;
   f32x4 acc[TRW][TCW];
 #pragma unroll
@@ -80,41 +116,78 @@ __global__ __launch_bounds__(256) void gemm_wg(const Op op, float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bias_acc = 0.f;
-  for (int m0 = m_beg; m0 < m_end; m0 += BMK) {
-    for (int e = tid; e < BR * BMK / 4; e += 256) {
-      const int mm = e / (BR / 4), rr = (e % (BR / 4)) * 4;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (m0 + mm < m_end) op.load_x4(m0 + mm, r0 + rr, v);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Xs[(rr + i) * LD + mm] = (T)v[i];
-    }
-    for (int e = tid; e < BC * BMK / 4; e += 256) {
-      const int mm = e / (BC / 4), cc = (e % (BC / 4)) * 4;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (m0 + mm < m_end && c0 + cc < op.C) op.load_y4(m0 + mm, c0 + cc, v);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Ys[(cc + i) * LD + mm] = (T)v[i];
+  typedef typename F::vec V;  // 16 bytes of T
+  const int n_it = (m_end - m_beg + BM * G - 1) / (BM * G);
+  for (int it = 0; it < n_it; ++it) {
+    const int m0 = m_beg + (it * G + grp) * BM;
+    const bool active = m0 < m_end;
+    if (active) {
+      for (int e = tid; e < BM * (BR / VEC); e += 256) {
+        const int mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
+        V v;
+        if (m0 + mm < m_end)
+          v = *reinterpret_cast<const V*>(op.x + (size_t)(m0 + mm) * op.x_ld + r0 + rr);
+        else
+          v = F::zero();
+        *reinterpret_cast<V*>(Xs + mm * LDX + rr) = v;
+      }
+      for (int e = tid; e < BM * (BC / VEC); e += 256) {
+        const int mm = e / (BC / VEC), cc = (e % (BC / VEC)) * VEC;
+        V v;
+        if (m0 + mm < m_end && c0 + cc < op.C) v = op.load_y(m0 + mm, c0 + cc);
+        else v = F::zero();
+        *reinterpret_cast<V*>(Ys + mm * LDY + cc) = v;
+      }
     }
     __syncthreads();
-    if (do_bias && tid < BR) {
+    if (active) {
+      if (do_bias && tid < BR) {
 #pragma unroll 8
-      for (int mm = 0; mm < BMK; ++mm) bias_acc += (float)Xs[tid * LD + mm];
-    }
+        for (int mm = 0; mm < BM; ++mm) bias_acc += (float)Xs[mm * LDX + tid];
+      }
 #pragma unroll
-    for (int kk = 0; kk < BMK; kk += F::KSTEP) {
-      typename F::vec a[TRW], b[TCW];
+      for (int kk = 0; kk < BM; kk += F::KSTEP) {
+        V a[TRW], b[TCW];
 #pragma unroll
-      for (int i = 0; i < TRW; ++i)
-        a[i] = F::load(&Xs[((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl]);
+        for (int i = 0; i < TRW; ++i)
+          a[i] = lds_frag_k(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
 #pragma unroll
-      for (int j = 0; j < TCW; ++j)
-        b[j] = F::load(&Ys[((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl]);
+        for (int j = 0; j < TCW; ++j)
+          b[j] = lds_frag_k(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
 #pragma unroll
-      for (int i = 0; i < TRW; ++i)
+        for (int i = 0; i < TRW; ++i)
 #pragma unroll
-        for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+          for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+      }
     }
     __syncthreads();
+  }
+  // fixed-order reduction of the G groups' accumulators through (reused) LDS
+  if constexpr (G > 1) {
+    float* red = reinterpret_cast<float*>(smem);
+    for (int g = 1; g < G; ++g) {
+      if (grp == g) {
+#pragma unroll
+        for (int i = 0; i < TRW; ++i)
+#pragma unroll
+          for (int j = 0; j < TCW; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[((i * TCW + j) * 4 + q) * 256 + tid] = acc[i][j][q];
+        red[NACC * 256 + tid] = bias_acc;
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int i = 0; i < TRW; ++i)
+#pragma unroll
+          for (int j = 0; j < TCW; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * TCW + j) * 4 + q) * 256 + tid];
+        bias_acc += red[NACC * 256 + tid];
+      }
+      __syncthreads();
+    }
+    if (grp != 0) return;
   }
   const float sc = op.out_scale;
 #pragma unroll

@@ -57,13 +57,13 @@ inline double dec(float x) {
 struct Split {
   int S = 1, mps = 32;  // splits, m per split
 };
-Split plan_split(long M, int tiles, int target_wgs) {
+Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
   Split s;
-  const long chunks = (M + 31) / 32;
+  const long chunks = (M + chunk - 1) / chunk;
   long S = (target_wgs + tiles - 1) / tiles;
   if (S < 1) S = 1;
   if (S > chunks) S = chunks;
-  long mps = ((M + S - 1) / S + 31) / 32 * 32;
+  long mps = ((M + S - 1) / S + chunk - 1) / chunk * chunk;
   s.mps = (int)mps;
   s.S = (int)((M + mps - 1) / mps);
   return s;
@@ -105,7 +105,8 @@ struct impala_learner {
   float *loss_part, *sumsq_part;
   int64_t* step;
   Split sp1, sp2, sp3, spfc, sph;
-  int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0;
+  int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
+  RedArgs red{};
   // live launch timer: hipEvent pairs around every launch of one kernel id
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
   hipEvent_t* timer_ev = nullptr;
@@ -234,68 +235,57 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     CK_LAUNCH("conv2_dgrad");
   }
   // ---- weight gradients (split-M partial slabs) ----
+  constexpr int WBM = sizeof(T) == 4 ? 32 : 64;  // m-chunk (LDS budget of the f32 mode)
   {
     HeadsWgrad<T> op{};
-    op.M = N; op.dH = (const T*)h->dH; op.h = (const T*)h->h;
+    op.M = N; op.x = (const T*)h->dH; op.h = (const T*)h->h;
     timer_begin(h, K_HEADS_WGRAD, st);
-    gemm_wg<T, 16, 64, 1, 4><<<dim3(HID / 64, 1, h->sph.S), 256, 0, st>>>(op, h->s_h, h->s_bh,
-                                                                          h->sph.mps);
+    gemm_wg<T, 16, 256, 1, 4, WBM, 1><<<dim3(1, 1, h->sph.S), 256, 0, st>>>(op, h->s_h, h->s_bh,
+                                                                        h->sph.mps);
     timer_end(h, K_HEADS_WGRAD, st);
     CK_LAUNCH("heads_wgrad");
   }
   {
     FcWgrad<T> op{};
-    op.M = N; op.dz = (const T*)h->dz; op.y = (const T*)h->y;
+    op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
     timer_begin(h, K_FC_WGRAD, st);
-    gemm_wg<T, 64, 64, 2, 2><<<dim3(FLAT / 64, HID / 64, h->spfc.S), 256, 0, st>>>(
+    gemm_wg<T, 64, 256, 1, 4, WBM, 2><<<dim3(FLAT / 256, HID / 64, h->spfc.S), 512, 0, st>>>(
         op, h->s_fc, h->s_bfc, h->spfc.mps);
     timer_end(h, K_FC_WGRAD, st);
     CK_LAUNCH("fc_wgrad");
   }
   {
     Conv3Wgrad<T> op{};
-    op.M = N * P3; op.dy = (const T*)h->dact3; op.x = (const T*)h->act2;
+    op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
     timer_begin(h, K_CONV3_WGRAD, st);
-    gemm_wg<T, 64, 64, 2, 2><<<dim3(K3 / 64, 1, h->sp3.S), 256, 0, st>>>(op, h->s_w3, h->s_b3,
-                                                                         h->sp3.mps);
+    gemm_wg<T, 64, 192, 1, 4, WBM, 4><<<dim3(K3 / 192, 1, h->sp3.S), 1024, 0, st>>>(
+        op, h->s_w3, h->s_b3, h->sp3.mps);
     timer_end(h, K_CONV3_WGRAD, st);
     CK_LAUNCH("conv3_wgrad");
   }
   {
     Conv2Wgrad<T> op{};
-    op.M = N * P2; op.dy = (const T*)h->dact2; op.x = (const T*)h->act1;
+    op.M = N * P2; op.x = (const T*)h->dact2; op.in = (const T*)h->act1;
     timer_begin(h, K_CONV2_WGRAD, st);
-    gemm_wg<T, 64, 64, 2, 2><<<dim3(K2 / 64, 1, h->sp2.S), 256, 0, st>>>(op, h->s_w2, h->s_b2,
-                                                                         h->sp2.mps);
+    gemm_wg<T, 64, 128, 1, 4, WBM, 4><<<dim3(K2 / 128, 1, h->sp2.S), 1024, 0, st>>>(
+        op, h->s_w2, h->s_b2, h->sp2.mps);
     timer_end(h, K_CONV2_WGRAD, st);
     CK_LAUNCH("conv2_wgrad");
   }
   {
     Conv1Wgrad<T> op{};
-    op.M = N * P1; op.dy = (const T*)h->dact1; op.x = b->obs;
+    op.M = N * P1; op.x = (const T*)h->dact1; op.img = b->obs;
     timer_begin(h, K_CONV1_WGRAD, st);
-    gemm_wg<T, 32, 64, 2, 2><<<dim3(K1 / 64, 1, h->sp1.S), 256, 0, st>>>(op, h->s_w1, h->s_b1,
-                                                                         h->sp1.mps);
+    gemm_wg<T, 32, 192, 1, 4, WBM, 4><<<dim3(1, 1, h->sp1.S), 1024, 0, st>>>(op, h->s_w1, h->s_b1,
+                                                                        h->sp1.mps);
     timer_end(h, K_CONV1_WGRAD, st);
     CK_LAUNCH("conv1_wgrad");
   }
   // ---- slab reduction -> canonical grads, sum of squares, loss metrics, step += 1 ----
-  {
-    RedArgs ra{};
-    ra.grads = h->grads; ra.cn = h->cn;
-    ra.s_w1 = h->s_w1; ra.s_b1 = h->s_b1; ra.s_w2 = h->s_w2; ra.s_b2 = h->s_b2;
-    ra.s_w3 = h->s_w3; ra.s_b3 = h->s_b3; ra.s_ln = h->s_ln; ra.s_fc = h->s_fc;
-    ra.s_bfc = h->s_bfc; ra.s_h = h->s_h; ra.s_bh = h->s_bh;
-    ra.S1 = h->sp1.S; ra.S2 = h->sp2.S; ra.S3 = h->sp3.S; ra.Sln = h->n_ln_wg;
-    ra.Sfc = h->spfc.S; ra.Sh = h->sph.S;
-    ra.sumsq_part = h->sumsq_part; ra.loss_part = h->loss_part; ra.n_loss_part = h->n_loss_wg;
-    ra.B = B; ra.T = Tl; ra.ent_coef = h->cfg.entropy_coeff; ra.metrics = h->metrics;
-    ra.step = h->step;
-    timer_begin(h, K_REDUCE, st);
-    reduce_grads_kernel<<<h->n_red_wg, 256, 0, st>>>(ra);
-    timer_end(h, K_REDUCE, st);
-    CK_LAUNCH("reduce_grads");
-  }
+  timer_begin(h, K_REDUCE, st);
+  reduce_grads_kernel<<<h->n_red_wg, 256, 0, st>>>(h->red);
+  timer_end(h, K_REDUCE, st);
+  CK_LAUNCH("reduce_grads");
   return 0;
 }
 
@@ -311,7 +301,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
   aa.cn = h->cn; aa.sh = h->sh;
   timer_begin(h, K_ADAM, st);
-  adam_kernel<T><<<h->n_red_wg, 256, 0, st>>>(aa);
+  adam_kernel<T><<<h->n_adam_wg, 256, 0, st>>>(aa);
   timer_end(h, K_ADAM, st);
   CK_LAUNCH("adam");
   return 0;
@@ -319,7 +309,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
 
 template <typename T>
 int launch_pack(impala_learner* h, hipStream_t st) {
-  pack_params_kernel<T><<<h->n_red_wg, 256, 0, st>>>(h->params, ShadowPtrs{h->shadow, h->vecs, h->A},
+  pack_params_kernel<T><<<cdiv((long)h->cn.total, 256), 256, 0, st>>>(h->params, ShadowPtrs{h->shadow, h->vecs, h->A},
                                                      h->cn, h->sh);
   CK_LAUNCH("pack_params");
   return 0;
@@ -395,12 +385,14 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->S_seg = next_pow2(cfg->rollout_length);
   h->n_loss_wg = cdiv(cfg->batch_size, 4 * (64 / h->S_seg));
   h->n_ln_wg = cdiv(N, 4 * h->ln_fpw);
-  h->n_red_wg = cdiv((long)h->cn.total, 256);
-  h->sph = plan_split(N, HID / 64, 128);
-  h->spfc = plan_split(N, (FLAT / 64) * (HID / 64), 256);
-  h->sp3 = plan_split((long)N * P3, K3 / 64, 512);
-  h->sp2 = plan_split((long)N * P2, K2 / 64, 512);
-  h->sp1 = plan_split((long)N * P1, K1 / 64, 768);
+
+  h->n_red_wg = cdiv((OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT + HID * FLAT +
+                      HID + HEADS * HID + HEADS) / 4, 256);
+  h->sph = plan_split(N, 1, 16);
+  h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), 96);
+  h->sp3 = plan_split((long)N * P3, K3 / 192, 192);
+  h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
+  h->sp1 = plan_split((long)N * P1, 1, 256);
 
   // ---- one workspace allocation, 256-byte aligned carve ----
   size_t off = 0;
@@ -466,6 +458,37 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->s_h = (float*)(w + o_sh); h->s_bh = (float*)(w + o_sbh);
   h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
   h->step = (int64_t*)(w + o_step);
+  {
+    RedArgs& ra = h->red;
+    int ns = 0;
+    auto add = [&](const float* slab, int S, int count, int kind, long long canon) {
+      ra.seg[ns] = RedSeg{slab, S, count, kind, canon};
+      ra.start4[ns + 1] = ra.start4[ns] + count / 4;
+      ++ns;
+    };
+    ra.start4[0] = 0;
+    add(h->s_w1, h->sp1.S, OC1 * K1, RK_ID, (long long)h->cn.w1);
+    add(h->s_b1, h->sp1.S, OC1, RK_ID, (long long)h->cn.b1);
+    add(h->s_w2, h->sp2.S, OC2 * K2, RK_CONV2, (long long)h->cn.w2);
+    add(h->s_b2, h->sp2.S, OC2, RK_ID, (long long)h->cn.b2);
+    add(h->s_w3, h->sp3.S, OC3 * K3, RK_CONV3, (long long)h->cn.w3);
+    add(h->s_b3, h->sp3.S, OC3, RK_ID, (long long)h->cn.b3);
+    add(h->s_ln, h->n_ln_wg, 2 * FLAT, RK_LN, (long long)h->cn.lng);
+    add(h->s_fc, h->spfc.S, HID * FLAT, RK_FC, (long long)h->cn.wfc);
+    add(h->s_bfc, h->spfc.S, HID, RK_ID, (long long)h->cn.bfc);
+    add(h->s_h, h->sph.S, HEADS * HID, RK_HEADS_W, 0);
+    add(h->s_bh, h->sph.S, HEADS, RK_HEADS_B, 0);
+    ra.nseg = ns;
+    ra.cn = h->cn;
+    ra.sumsq_part = h->sumsq_part;
+    ra.loss_part = h->loss_part;
+    ra.n_loss_part = h->n_loss_wg;
+    ra.B = cfg->batch_size;
+    ra.T = cfg->rollout_length;
+    ra.A = h->A;
+    ra.ent_coef = cfg->entropy_coeff;
+    ra.step = h->step;
+  }
   *out = h;
   return 0;
 }
@@ -488,6 +511,8 @@ int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp
   if (!params) return fail(IMPALA_E_INVALID, "null params pointer");
   h->params = params; h->grads = grads; h->exp_avg = exp_avg; h->exp_avg_sq = exp_avg_sq;
   h->metrics = metrics;
+  h->red.grads = grads;
+  h->red.metrics = metrics;
   return impala_refresh_weights(h, stream);
 }
 

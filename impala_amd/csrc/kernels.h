@@ -382,74 +382,101 @@ __global__ __launch_bounds__(256) void pack_params_kernel(const float* __restric
 }
 
 // =========================================================================================
-// Gradient-slab reduction into the canonical (state_dict) gradient buffer, fixed split order.
-// Also: per-block sum of squares (for the clip norm), loss-metric finalisation and the Adam
-// step counter increment (block 0).
+// Gradient-slab reduction into the canonical (state_dict) gradient buffer.  Work is laid out
+// in KERNEL order (slab-contiguous: one float4 per thread, coalesced across the wave, all
+// splits summed in a fixed order -> deterministic); the canonical index of each element is
+// computed on the write side.  Also: per-block sum of squares (clip norm), loss-metric
+// finalisation and the Adam step counter increment (block 0).
 // =========================================================================================
+enum RedKind { RK_ID = 0, RK_CONV2, RK_CONV3, RK_LN, RK_FC, RK_HEADS_W, RK_HEADS_B };
+constexpr int MAX_RED_SEGS = 12;
+struct RedSeg {
+  const float* slab;  // [S][count]
+  int S, count, kind;
+  long long canon;    // canonical offset (for RK_LN: lng offset; lnb follows)
+};
 struct RedArgs {
+  RedSeg seg[MAX_RED_SEGS];
+  int start4[MAX_RED_SEGS + 1];  // prefix sums of count/4
+  int nseg;
   float* grads;
   Canon cn;
-  const float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
-  int S1, S2, S3, Sln, Sfc, Sh;
   float* sumsq_part;
   const float* loss_part;
-  int n_loss_part, B, T;
+  int n_loss_part, B, T, A;
   float ent_coef;
   float* metrics;
   int64_t* step;
 };
 
-DEV float sum_splits(const float* s, int S, size_t stride, size_t k) {
-  float acc = 0.f;
-  for (int q = 0; q < S; ++q) acc += s[(size_t)q * stride + k];
-  return acc;
+DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
+  switch (sg.kind) {
+    case RK_CONV2: {  // k = oc*512 + tap*32 + ci  ->  oc*512 + ci*16 + tap
+      const int oc = k >> 9, rem = k & 511, tap = rem >> 5, ci = rem & 31;
+      return sg.canon + oc * K2 + ci * 16 + tap;
+    }
+    case RK_CONV3: {  // k = oc*576 + tap*64 + ci  ->  oc*576 + ci*9 + tap
+      const int oc = k / K3, rem = k - oc * K3, tap = rem >> 6, ci = rem & 63;
+      return sg.canon + oc * K3 + ci * 9 + tap;
+    }
+    case RK_LN: {  // k = which*1024 + p*64 + c  ->  lng/lnb + c*16 + p
+      const int which = k >> 10, j = k & 1023, p = j >> 6, c = j & 63;
+      return sg.canon + which * FLAT + c * 16 + p;
+    }
+    case RK_FC: {  // k = o*1024 + p*64 + c  ->  o*1024 + c*16 + p
+      const int o = k >> 10, j = k & 1023, p = j >> 6, c = j & 63;
+      return sg.canon + (long long)o * FLAT + c * 16 + p;
+    }
+    case RK_HEADS_W: {  // k = row*256 + j; rows 0..A-1 actor, row 15 critic, else padding
+      const int row = k >> 8, j = k & 255;
+      if (row < a.A) return (long long)a.cn.wa + row * HID + j;
+      if (row == VCOL) return (long long)a.cn.wc + j;
+      return -1;
+    }
+    case RK_HEADS_B: {
+      if (k < a.A) return (long long)a.cn.ba + k;
+      if (k == VCOL) return (long long)a.cn.bc;
+      return -1;
+    }
+    default:
+      return sg.canon + k;
+  }
 }
 
 __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a) {
   __shared__ float red[4];
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const Canon& cn = a.cn;
-  float g = 0.f;
-  if (i < cn.total) {
-    if (i < cn.b1) {
-      g = sum_splits(a.s_w1, a.S1, (size_t)OC1 * K1, i);
-    } else if (i < cn.w2) {
-      g = sum_splits(a.s_b1, a.S1, OC1, i - cn.b1);
-    } else if (i < cn.b2) {
-      const int k = (int)(i - cn.w2), oc = k / K2, rem = k % K2, ci = rem >> 4,
-                tap = rem & 15;
-      g = sum_splits(a.s_w2, a.S2, (size_t)OC2 * K2, (size_t)oc * K2 + tap * OC1 + ci);
-    } else if (i < cn.w3) {
-      g = sum_splits(a.s_b2, a.S2, OC2, i - cn.b2);
-    } else if (i < cn.b3) {
-      const int k = (int)(i - cn.w3), oc = k / K3, rem = k % K3, ci = rem / 9, tap = rem % 9;
-      g = sum_splits(a.s_w3, a.S3, (size_t)OC3 * K3, (size_t)oc * K3 + tap * OC2 + ci);
-    } else if (i < cn.lng) {
-      g = sum_splits(a.s_b3, a.S3, OC3, i - cn.b3);
-    } else if (i < cn.lnb) {
-      const int j = (int)(i - cn.lng);
-      g = sum_splits(a.s_ln, a.Sln, 2 * FLAT, (j & 15) * OC3 + (j >> 4));
-    } else if (i < cn.wfc) {
-      const int j = (int)(i - cn.lnb);
-      g = sum_splits(a.s_ln, a.Sln, 2 * FLAT, FLAT + (j & 15) * OC3 + (j >> 4));
-    } else if (i < cn.bfc) {
-      const int k = (int)(i - cn.wfc), o = k >> 10, j = k & 1023;
-      g = sum_splits(a.s_fc, a.Sfc, (size_t)HID * FLAT, (size_t)o * FLAT + (j & 15) * OC3 + (j >> 4));
-    } else if (i < cn.wa) {
-      g = sum_splits(a.s_bfc, a.Sfc, HID, i - cn.bfc);
-    } else if (i < cn.ba) {
-      g = sum_splits(a.s_h, a.Sh, (size_t)HEADS * HID, i - cn.wa);
-    } else if (i < cn.wc) {
-      g = sum_splits(a.s_bh, a.Sh, HEADS, i - cn.ba);
-    } else if (i < cn.bc) {
-      g = sum_splits(a.s_h, a.Sh, (size_t)HEADS * HID, VCOL * HID + (i - cn.wc));
-    } else {
-      g = sum_splits(a.s_bh, a.Sh, HEADS, VCOL);
+  const int g4 = blockIdx.x * 256 + threadIdx.x;
+  float sq = 0.f;
+  if (g4 < a.start4[a.nseg]) {
+    int s = 0;
+    while (g4 >= a.start4[s + 1]) ++s;
+    const RedSeg& sg = a.seg[s];
+    const int k = (g4 - a.start4[s]) * 4;
+    const float* p = sg.slab + k;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    int q = 0;
+    for (; q + 4 <= sg.S; q += 4) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 0) * sg.count);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 1) * sg.count);
+      const f32x4 v2 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 2) * sg.count);
+      const f32x4 v3 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 3) * sg.count);
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
     }
-    a.grads[i] = g;
+    for (; q < sg.S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (size_t)q * sg.count);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long c = canon_index(a, sg, k + i);
+      if (c >= 0) {
+        a.grads[c] = acc[i];
+        sq += acc[i] * acc[i];
+      }
+    }
   }
-  float q = wave_sum(g * g);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
   if (threadIdx.x == 0) a.sumsq_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
   if (blockIdx.x == 0 && threadIdx.x == 64) {
@@ -462,9 +489,10 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a) {
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, size_t n,
                                                     float* __restrict__ part) {
   __shared__ float red[4];
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const float v = i < n ? g[i] : 0.f;
-  const float q = wave_sum(v * v);
+  float acc = 0.f;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    acc += g[i] * g[i];
+  const float q = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
   __syncthreads();
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
@@ -503,8 +531,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   const float step_size = (float)(a.lr / bc1);
   const float bc2s = (float)sqrt(bc2);
   const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < a.cn.total) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < a.cn.total;
+       i += (size_t)gridDim.x * 256) {
     const float g = a.grads[i] * a.inv_world * coef;
     a.grads[i] = g;
     float m = a.m[i], v = a.v[i];

@@ -247,59 +247,74 @@ template <typename T> struct Conv2Dgrad {
 };
 
 // ------------------------------- backward (wgrad) ---------------------------------------
-// D[r][c] = sum_m X(m, r) * Y(m, c); load_x4 / load_y4 return 4 consecutive r / c.
+// D[r][c] = sum_m X[m][r] * Y(m, c); X row-major [M][x_ld]; load_y returns 16 bytes of T
+// (VEC consecutive c of one run: channels for conv2/3/FC/heads, kw for conv1).
 template <typename T> struct HeadsWgrad {  // dWh[o'][j] = sum_n dH[n][o'] h[n][j]
-  int M, R = HEADS, C = HID;
+  static constexpr int R = HEADS, C = HID;
+  int M;
   float out_scale = 1.f;
-  const T* dH;
+  const T* x;  // dH [n][32]
+  int x_ld = HPAD;
   const T* h;
-  DEV void load_x4(int m, int r, float v[4]) const { load4(dH + (size_t)m * HPAD + r, v); }
-  DEV void load_y4(int m, int c, float v[4]) const { load4(h + (size_t)m * HID + c, v); }
+  DEV typename Frag<T>::vec load_y(int m, int c) const {
+    return *reinterpret_cast<const typename Frag<T>::vec*>(h + (size_t)m * HID + c);
+  }
 };
 template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
-  int M, R = HID, C = FLAT;
+  static constexpr int R = HID, C = FLAT;
+  int M;
   float out_scale = 1.f;
-  const T* dz;
+  const T* x;  // dz
+  int x_ld = HID;
   const T* y;
-  DEV void load_x4(int m, int r, float v[4]) const { load4(dz + (size_t)m * HID + r, v); }
-  DEV void load_y4(int m, int c, float v[4]) const { load4(y + (size_t)m * FLAT + c, v); }
+  DEV typename Frag<T>::vec load_y(int m, int c) const {
+    return *reinterpret_cast<const typename Frag<T>::vec*>(y + (size_t)m * FLAT + c);
+  }
 };
 template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3+kw)*64 + ci
-  int M, R = OC3, C = K3;
+  static constexpr int R = OC3, C = K3;
+  int M;
   float out_scale = 1.f;
-  const T* dy;  // dact3
-  const T* x;   // act2
-  DEV void load_x4(int m, int r, float v[4]) const { load4(dy + (size_t)m * OC3 + r, v); }
-  DEV void load_y4(int m, int c, float v[4]) const {
+  const T* x;  // dact3
+  int x_ld = OC3;
+  const T* in;  // act2
+  DEV typename Frag<T>::vec load_y(int m, int c) const {
     const int n = m / P3, p = m - n * P3, oy = p / H3, ox = p - oy * H3;
     const int tap = c >> 6, ci = c & 63, kh = tap / 3, kw = tap - kh * 3;
-    load4(x + ((size_t)(n * H2 + oy + kh) * H2 + ox + kw) * OC2 + ci, v);
+    return *reinterpret_cast<const typename Frag<T>::vec*>(
+        in + ((size_t)(n * H2 + oy + kh) * H2 + ox + kw) * OC2 + ci);
   }
 };
 template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4+kw)*32 + ci
-  int M, R = OC2, C = K2;
+  static constexpr int R = OC2, C = K2;
+  int M;
   float out_scale = 1.f;
-  const T* dy;  // dact2
-  const T* x;   // act1
-  DEV void load_x4(int m, int r, float v[4]) const { load4(dy + (size_t)m * OC2 + r, v); }
-  DEV void load_y4(int m, int c, float v[4]) const {
+  const T* x;  // dact2
+  int x_ld = OC2;
+  const T* in;  // act1
+  DEV typename Frag<T>::vec load_y(int m, int c) const {
     const int n = m / P2, p = m - n * P2, oy = p / H2, ox = p - oy * H2;
     const int tap = c >> 5, ci = c & 31, kh = tap >> 2, kw = tap & 3;
-    load4(x + ((size_t)(n * H1 + ST2 * oy + kh) * H1 + ST2 * ox + kw) * OC1 + ci, v);
+    return *reinterpret_cast<const typename Frag<T>::vec*>(
+        in + ((size_t)(n * H1 + ST2 * oy + kh) * H1 + ST2 * ox + kw) * OC1 + ci);
   }
 };
 template <typename T> struct Conv1Wgrad {  // m = (n, oy, ox) in N*225; c = ci*64 + kh*8 + kw
-  int M, R = OC1, C = K1;
+  static constexpr int R = OC1, C = K1;
+  int M;
   float out_scale = 1.f / 255.f;
-  const T* dy;  // dact1
-  const uint8_t* x;
-  DEV void load_x4(int m, int r, float v[4]) const { load4(dy + (size_t)m * OC1 + r, v); }
-  DEV void load_y4(int m, int c, float v[4]) const {
+  const T* x;  // dact1
+  int x_ld = OC1;
+  const uint8_t* img;
+  DEV typename Frag<T>::vec load_y(int m, int c) const {
     const int n = m / P1, p = m - n * P1, oy = p / H1, ox = p - oy * H1;
     const int ci = c >> 6, kh = (c >> 3) & 7, kw = c & 7;
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(
-        x + (size_t)n * IMG + ci * (H0 * H0) + (ST1 * oy + kh) * H0 + ST1 * ox + kw);
-    v[0] = (float)(w & 255u); v[1] = (float)((w >> 8) & 255u);
-    v[2] = (float)((w >> 16) & 255u); v[3] = (float)(w >> 24);
+    const uint8_t* q = img + (size_t)n * IMG + ci * (H0 * H0) + (ST1 * oy + kh) * H0 + ST1 * ox + kw;
+    if constexpr (sizeof(T) == 4) {
+      return Frag<float>::from_u8(*reinterpret_cast<const uint32_t*>(q));
+    } else {
+      return Frag<__bf16>::from_u8_2(*reinterpret_cast<const uint32_t*>(q),
+                                     *reinterpret_cast<const uint32_t*>(q + 4));
+    }
   }
 };
