@@ -130,27 +130,28 @@ namespace {
 template <typename T>
 int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st) {
   using namespace net;
+  constexpr int TBK = sizeof(T) == 4 ? 32 : 64;  // K chunk of the LDS-staged tile GEMM
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
   {
     Conv1Fwd<T> op{n * P1, sw + sh.w1, vv + Vecs::b1, obs, (T*)h->act1};
     timer_begin(h, K_CONV1_FWD, st);
-    gemm_rc<T, 2, 2><<<dim3(cdiv((long)n * P1, 128), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 32, 128, TBK, 1, 4><<<dim3(cdiv((long)n * P1, 128), 1), 256, 0, st>>>(op);
     timer_end(h, K_CONV1_FWD, st);
     CK_LAUNCH("conv1_fwd");
   }
   {
     Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
     timer_begin(h, K_CONV2_FWD, st);
-    gemm_rc<T, 4, 1><<<dim3(cdiv((long)n * P2, 64), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 128, TBK, 1, 4><<<dim3(cdiv((long)n * P2, 128), 1), 256, 0, st>>>(op);
     timer_end(h, K_CONV2_FWD, st);
     CK_LAUNCH("conv2_fwd");
   }
   {
     Conv3Fwd<T> op{n * P3, sw + sh.w3, vv + Vecs::b3, (const T*)h->act2, (T*)h->act3};
     timer_begin(h, K_CONV3_FWD, st);
-    gemm_rc<T, 4, 1><<<dim3(cdiv((long)n * P3, 64), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv((long)n * P3, 64), 1), 256, 0, st>>>(op);
     timer_end(h, K_CONV3_FWD, st);
     CK_LAUNCH("conv3_fwd");
   }
@@ -162,7 +163,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
     timer_begin(h, K_FC_FWD, st);
-    gemm_rc<T, 4, 1><<<dim3(cdiv(n, 64), HID / 64), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv(n, 64), HID / 64), 256, 0, st>>>(op);
     timer_end(h, K_FC_FWD, st);
     CK_LAUNCH("fc_fwd");
   }
@@ -179,6 +180,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
 template <typename T>
 int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   using namespace net;
+  constexpr int TBK = sizeof(T) == 4 ? 32 : 64;
   const int N = h->N, B = h->cfg.batch_size, Tl = h->cfg.rollout_length;
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
@@ -209,7 +211,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   {
     FcDgrad<T> op{N, sw + sh.wfct, (const T*)h->dz, h->dy};
     timer_begin(h, K_FC_DGRAD, st);
-    gemm_rc<T, 4, 1><<<dim3(cdiv(N, 64), FLAT / 64), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv(N, 64), FLAT / 64), 256, 0, st>>>(op);
     timer_end(h, K_FC_DGRAD, st);
     CK_LAUNCH("fc_dgrad");
   }
@@ -222,15 +224,16 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3t, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
     timer_begin(h, K_CONV3_DGRAD, st);
-    gemm_rc<T, 4, 1><<<dim3(cdiv((long)N * P2, 64), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 128, TBK, 1, 4><<<dim3(cdiv((long)N * P2, 128), 1), 256, 0, st>>>(op);
     timer_end(h, K_CONV3_DGRAD, st);
     CK_LAUNCH("conv3_dgrad");
   }
   {
-    Conv2Dgrad<T> op{4 * N * 64, N * 64, sw + sh.w2t, (const T*)h->dact2, (const T*)h->act1,
+    const int NC = (N * 64 + 127) / 128 * 128;  // class stride, multiple of the tile width
+    Conv2Dgrad<T> op{4 * NC, NC, N * 64, sw + sh.w2t, (const T*)h->dact2, (const T*)h->act1,
                      (T*)h->dact1};
     timer_begin(h, K_CONV2_DGRAD, st);
-    gemm_rc<T, 2, 1><<<dim3(4 * N, 1), 256, 0, st>>>(op);
+    gemm_tile<T, 32, 128, TBK, 1, 4><<<dim3(4 * NC / 128, 1), 256, 0, st>>>(op);
     timer_end(h, K_CONV2_DGRAD, st);
     CK_LAUNCH("conv2_dgrad");
   }

@@ -209,21 +209,23 @@ template <typename T> struct Conv3Dgrad {
 };
 
 // conv2 dgrad by stride-parity class (sub-pixel decomposition, no zero taps inside):
-// cols = cls*(N*64) + n*64 + iy'*8 + ix'  with ih = 2*iy' + py, iw = 2*ix' + px, cls = py*2+px;
-// rows ci (32); k = (j1*2+j2)*64 + oc with kh = py + 2*j1, kw = px + 2*j2, oh = iy' - j1.
+// cols = cls*NC + n*64 + iy'*8 + ix'  with ih = 2*iy' + py, iw = 2*ix' + px, cls = py*2+px;
+// NC = N*64 rounded up to the tile width so no tile straddles two classes (columns
+// q >= N*64 of a class are padding); rows ci (32); k = (j1*2+j2)*64 + oc with
+// kh = py + 2*j1, kw = px + 2*j2, oh = iy' - j1.
 // Epilogue applies conv1's ReLU mask (act1 > 0); ih/iw == 15 are outside the 15x15 map.
 template <typename T> struct Conv2Dgrad {
   static constexpr int K = 4 * OC2;
-  int C;        // 4 * N * 64
-  int NC;       // N * 64 (columns per class)
+  int C;        // 4 * NC
+  int NC;       // columns per class (multiple of the tile width)
+  int NQ;       // valid columns per class = N * 64
   const T* wt;  // w2t [4][32][256]
   const T* dy;  // dact2 [n][36][64]
   const T* act; // act1 (mask)
   T* dx;        // dact1
   struct ColCtx { const T* p; int iy, ix; };
   DEV ColCtx col_ctx(int c) const {
-    const int cl = c / NC, q = c - cl * NC, n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
-    (void)cl;
+    const int cl = c / NC, q = min(c - cl * NC, NQ - 1), n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
     return ColCtx{dy + (size_t)n * P2 * OC2, iy, ix};
   }
   DEV const T* a_row(int r, int cw) const { return wt + ((size_t)(cw / NC) * OC1 + r) * K; }
@@ -234,7 +236,9 @@ template <typename T> struct Conv2Dgrad {
     return Frag<T>::load(cc.p + (oy * H2 + ox) * OC2 + oc);
   }
   DEV void store(int r, int c, float v[4]) const {
-    const int cl = c / NC, q = c - cl * NC, n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
+    const int cl = c / NC, q = c - cl * NC;
+    if (q >= NQ) return;
+    const int n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
     const int ih = 2 * iy + (cl >> 1), iw = 2 * ix + (cl & 1);
     if (ih >= H1 || iw >= H1) return;
     const size_t o = ((size_t)(n * H1 + ih) * H1 + iw) * OC1 + r;
