@@ -56,95 +56,6 @@ __global__ __launch_bounds__(256) void gemm_rc(const Op op) {
   }
 }
 
-// LDS-staged tile GEMM for the same operand definitions as gemm_rc:
-//   D[r][c] = sum_k A[r][k] * B(c, k),  WG tile BR x BC, K chunk BK.
-// Each K chunk of A (weights, row-major) and B (im2col / activation gather, 16-byte runs along
-// k) is loaded into registers one chunk ahead, stored k-contiguous into one of two LDS
-// buffers with 16-byte writes (rows padded by 16 B), and every wave reads its fragments with
-// ds_read_b128 -- operand reuse across the WG's waves comes from LDS instead of L1.
-// WR x WC waves, each owning (BR/WR) x (BC/WC) of the tile.  K % BK == 0, BR % (16*WR) == 0.
-template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
-__global__ __launch_bounds__(256) void gemm_tile(const Op op) {
-  using F = Frag<T>;
-  typedef typename F::vec V;
-  constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int KV = BK / VEC;            // 16-byte vectors per tile row per chunk
-  constexpr int LD = BK + VEC;            // padded row (elements)
-  constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
-  constexpr int NA = BR * KV / 256, NB = BC * KV / 256;
-  constexpr int RPP = 256 / KV;           // tile rows covered per staging pass
-  static_assert(WR * WC == 4 && TRW >= 1 && TCW >= 1, "tile");
-  static_assert(BR * KV % 256 == 0 && BC * KV % 256 == 0, "staging");
-  static_assert(Op::K % BK == 0 && BK % F::KSTEP == 0, "K chunking");
-  __shared__ __attribute__((aligned(16))) T smem[2 * (BR + BC) * LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WC, wc = wave % WC;
-  const int r0 = blockIdx.y * BR, c0 = blockIdx.x * BC;
-  const int kv = tid % KV, rl = tid / KV;
-  // per-thread staging contexts (fixed rows / columns for the whole K loop)
-  const T* arow[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) arow[i] = op.a_row(r0 + rl + i * RPP, min(c0, op.C - 1));
-  typename Op::ColCtx bctx[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(c0 + rl + i * RPP, op.C - 1));
-  V ra[NA], rb[NB];
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = F::load(arow[i] + k0 + kv * VEC);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = op.load_b(bctx[i], k0 + kv * VEC);
-  };
-  auto stash = [&](int buf) {
-    T* As = smem + buf * (BR + BC) * LD;
-    T* Bs = As + BR * LD;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + (rl + i * RPP) * LD + kv * VEC) = ra[i];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + (rl + i * RPP) * LD + kv * VEC) = rb[i];
-  };
-  f32x4 acc[TRW][TCW];
-#pragma unroll
-  for (int i = 0; i < TRW; ++i)
-#pragma unroll
-    for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kl = F::KPL * (lane >> 4);
-  fetch(0);
-  constexpr int NK = Op::K / BK;
-  for (int kc = 0; kc < NK; ++kc) {
-    const int buf = kc & 1;
-    stash(buf);
-    __syncthreads();
-    if (kc + 1 < NK) fetch((kc + 1) * BK);
-    const T* As = smem + buf * (BR + BC) * LD;
-    const T* Bs = As + BR * LD;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += F::KSTEP) {
-      V a[TRW], b[TCW];
-#pragma unroll
-      for (int i = 0; i < TRW; ++i)
-        a[i] = *reinterpret_cast<const V*>(As + ((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl);
-#pragma unroll
-      for (int j = 0; j < TCW; ++j)
-        b[j] = *reinterpret_cast<const V*>(Bs + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
-#pragma unroll
-      for (int i = 0; i < TRW; ++i)
-#pragma unroll
-        for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < TCW; ++j) {
-    const int c = c0 + (wc * TCW + j) * 16 + (lane & 15);
-    if (c >= op.C) continue;
-#pragma unroll
-    for (int i = 0; i < TRW; ++i) {
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      op.store(r0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
-    }
-  }
-}
-
 // LDS fragment read along the k (= m) dimension of a row-major [m][col] tile:
 //  bf16: two ds_read_b64_tr_b16 (hardware transpose, 4 rows x 16 cols per 16-lane group):
 //        lane l gets S[k0 + 8*(l>>4) + j][c0 + (l&15)], j = 0..7.
@@ -165,6 +76,125 @@ DEV Frag<__bf16>::vec lds_frag_k(const __bf16* tile, int ld, int lane) {
 DEV Frag<float>::vec lds_frag_k(const float* tile, int ld, int lane) {
   const float* a0 = tile + 4 * (lane >> 4) * ld + (lane & 15);
   return f32x4{a0[0], a0[ld], a0[2 * ld], a0[3 * ld]};
+}
+
+// LDS-staged tile GEMM for the same operand definitions as gemm_rc:
+//   D[r][c] = sum_k A[r][k] * B(c, k),  WG tile BR x BC, K chunk BK.
+// Each K chunk of A (weights, row-major) and B (im2col / activation gather, 16-byte runs along
+// k) is loaded into registers one chunk ahead, stored k-contiguous into one of two LDS
+// buffers with 16-byte writes (rows padded by 16 B), and every wave reads its fragments with
+// ds_read_b128 -- operand reuse across the WG's waves comes from LDS instead of L1.
+// WR x WC waves, each owning (BR/WR) x (BC/WC) of the tile.  K % BK == 0, BR % (16*WR) == 0.
+// Op::A_KMAJOR: A is stored transposed (a_kptr(k, r, c0) -> 16-byte run along r; e.g. the
+// forward weight consumed by a dgrad); its chunk is staged [k][r] and the A fragments are
+// read with the LDS transpose read, so no transposed weight copy is kept in HBM.
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
+__global__ __launch_bounds__(256) void gemm_tile(const Op op) {
+  constexpr bool AK = Op::A_KMAJOR;
+  using F = Frag<T>;
+  typedef typename F::vec V;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int KV = BK / VEC;            // 16-byte vectors per tile row per chunk
+  constexpr int LD = BK + VEC;            // padded row (elements)
+  constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
+  constexpr int NA = BR * KV / 256, NB = BC * KV / 256;
+  constexpr int RPP = 256 / KV;           // tile rows covered per staging pass
+  constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
+  constexpr int LDA = AK ? BR + VEC : LD; // A tile row length (elements)
+  constexpr int ASZ = AK ? BK * LDA : BR * LD;
+  static_assert(WR * WC == 4 && TRW >= 1 && TCW >= 1, "tile");
+  static_assert(BR * KV % 256 == 0 && BC * KV % 256 == 0, "staging");
+  static_assert(Op::K % BK == 0 && BK % F::KSTEP == 0, "K chunking");
+  __shared__ __attribute__((aligned(16))) T smem[2 * (ASZ + BC * LD)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WC, wc = wave % WC;
+  const int r0 = blockIdx.y * BR, c0 = blockIdx.x * BC;
+  const int kv = tid % KV, rl = tid / KV;
+  // per-thread staging contexts (fixed rows / columns for the whole K loop)
+  const T* arow[NA];
+  const int cw = min(c0, op.C - 1);
+  if constexpr (!AK) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) arow[i] = op.a_row(r0 + rl + i * RPP, cw);
+  }
+  typename Op::ColCtx bctx[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(c0 + rl + i * RPP, op.C - 1));
+  V ra[NA], rb[NB];
+  auto fetch = [&](int k0) {
+    if constexpr (AK) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, kr = e / RV, rv = e % RV;
+        ra[i] = F::load(op.a_kptr(k0 + kr, r0 + rv * VEC, cw));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) ra[i] = F::load(arow[i] + k0 + kv * VEC);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = op.load_b(bctx[i], k0 + kv * VEC);
+  };
+  auto stash = [&](int buf) {
+    T* As = smem + buf * (ASZ + BC * LD);
+    T* Bs = As + ASZ;
+    if constexpr (AK) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, kr = e / RV, rv = e % RV;
+        *reinterpret_cast<V*>(As + kr * LDA + rv * VEC) = ra[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + (rl + i * RPP) * LD + kv * VEC) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + (rl + i * RPP) * LD + kv * VEC) = rb[i];
+  };
+  f32x4 acc[TRW][TCW];
+#pragma unroll
+  for (int i = 0; i < TRW; ++i)
+#pragma unroll
+    for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kl = F::KPL * (lane >> 4);
+  fetch(0);
+  constexpr int NK = Op::K / BK;
+  for (int kc = 0; kc < NK; ++kc) {
+    const int buf = kc & 1;
+    stash(buf);
+    __syncthreads();
+    if (kc + 1 < NK) fetch((kc + 1) * BK);
+    const T* As = smem + buf * (ASZ + BC * LD);
+    const T* Bs = As + ASZ;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += F::KSTEP) {
+      V a[TRW], b[TCW];
+#pragma unroll
+      for (int i = 0; i < TRW; ++i) {
+        if constexpr (AK)
+          a[i] = lds_frag_k(As + kk * LDA + (wr * TRW + i) * 16, LDA, lane);
+        else
+          a[i] = *reinterpret_cast<const V*>(As + ((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl);
+      }
+#pragma unroll
+      for (int j = 0; j < TCW; ++j)
+        b[j] = *reinterpret_cast<const V*>(Bs + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
+#pragma unroll
+      for (int i = 0; i < TRW; ++i)
+#pragma unroll
+        for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TCW; ++j) {
+    const int c = c0 + (wc * TCW + j) * 16 + (lane & 15);
+    if (c >= op.C) continue;
+#pragma unroll
+    for (int i = 0; i < TRW; ++i) {
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      op.store(r0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
+    }
+  }
 }
 
 // Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split

@@ -209,7 +209,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     CK_LAUNCH("heads_dgrad");
   }
   {
-    FcDgrad<T> op{N, sw + sh.wfct, (const T*)h->dz, h->dy};
+    FcDgrad<T> op{N, sw + sh.wfc, (const T*)h->dz, h->dy};
     timer_begin(h, K_FC_DGRAD, st);
     gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv(N, 64), FLAT / 64), 256, 0, st>>>(op);
     timer_end(h, K_FC_DGRAD, st);
@@ -222,7 +222,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   timer_end(h, K_LN_BWD, st);
   CK_LAUNCH("ln_bwd");
   {
-    Conv3Dgrad<T> op{N * P2, sw + sh.w3t, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
+    Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
     timer_begin(h, K_CONV3_DGRAD, st);
     gemm_tile<T, 64, 128, TBK, 1, 4><<<dim3(cdiv((long)N * P2, 128), 1), 256, 0, st>>>(op);
     timer_end(h, K_CONV3_DGRAD, st);
@@ -230,7 +230,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   }
   {
     const int NC = (N * 64 + 127) / 128 * 128;  // class stride, multiple of the tile width
-    Conv2Dgrad<T> op{4 * NC, NC, N * 64, sw + sh.w2t, (const T*)h->dact2, (const T*)h->act1,
+    Conv2Dgrad<T> op{4 * NC, NC, N * 64, sw + sh.w2, (const T*)h->dact2, (const T*)h->act1,
                      (T*)h->dact1};
     timer_begin(h, K_CONV2_DGRAD, st);
     gemm_tile<T, 32, 128, TBK, 1, 4><<<dim3(4 * NC / 128, 1), 256, 0, st>>>(op);
@@ -389,8 +389,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->n_loss_wg = cdiv(cfg->batch_size, 4 * (64 / h->S_seg));
   h->n_ln_wg = cdiv(N, 4 * h->ln_fpw);
 
-  h->n_red_wg = cdiv((OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT + HID * FLAT +
-                      HID + HEADS * HID + HEADS) / 4, 256);
+  // upper bound on the reduce workgroups (each segment: count/4 float4 columns, >= 16 per WG)
+  h->n_red_wg = 11 + (OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT + HID * FLAT +
+                      HID + HEADS * HID + HEADS) / 4 / 16;
   h->sph = plan_split(N, 1, 16);
   h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), 96);
   h->sp3 = plan_split((long)N * P3, K3 / 192, 192);
@@ -465,11 +466,13 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     RedArgs& ra = h->red;
     int ns = 0;
     auto add = [&](const float* slab, int S, int count, int kind, long long canon) {
-      ra.seg[ns] = RedSeg{slab, S, count, kind, canon};
-      ra.start4[ns + 1] = ra.start4[ns] + count / 4;
+      int sg = 1;
+      while (sg < 16 && sg * 4 < S) sg <<= 1;  // ~4+ loads per thread, <= 16 groups
+      ra.seg[ns] = RedSeg{slab, S, count, kind, canon, sg};
+      ra.wg_start[ns + 1] = ra.wg_start[ns] + cdiv(count / 4, 256 / sg);
       ++ns;
     };
-    ra.start4[0] = 0;
+    ra.wg_start[0] = 0;
     add(h->s_w1, h->sp1.S, OC1 * K1, RK_ID, (long long)h->cn.w1);
     add(h->s_b1, h->sp1.S, OC1, RK_ID, (long long)h->cn.b1);
     add(h->s_w2, h->sp2.S, OC2 * K2, RK_CONV2, (long long)h->cn.w2);
@@ -481,6 +484,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     add(h->s_bfc, h->spfc.S, HID, RK_ID, (long long)h->cn.bfc);
     add(h->s_h, h->sph.S, HEADS * HID, RK_HEADS_W, 0);
     add(h->s_bh, h->sph.S, HEADS, RK_HEADS_B, 0);
+    h->n_red_wg = ra.wg_start[ns];
     ra.nseg = ns;
     ra.cn = h->cn;
     ra.sumsq_part = h->sumsq_part;

@@ -336,14 +336,11 @@ DEV void write_shadow(const ShadowPtrs& sp, const Canon& cn, const Shadow& sh, s
     const int k = (int)(i - cn.w2), oc = k / K2, rem = k % K2, ci = rem >> 4, kh = (rem >> 2) & 3,
               kw = rem & 3;
     w[sh.w2 + oc * K2 + (kh * 4 + kw) * OC1 + ci] = pt;
-    const int cls = (kh & 1) * 2 + (kw & 1), t = (kh >> 1) * 2 + (kw >> 1);
-    w[sh.w2t + ((size_t)(cls * OC1 + ci) * 4 + t) * OC2 + oc] = pt;
   } else if (i < cn.w3) {
     vv[Vecs::b2 + (i - cn.b2)] = p;
   } else if (i < cn.b3) {
     const int k = (int)(i - cn.w3), oc = k / K3, rem = k % K3, ci = rem / 9, tap = rem % 9;
     w[sh.w3 + oc * K3 + tap * OC2 + ci] = pt;
-    w[sh.w3t + ci * K3 + tap * OC3 + oc] = pt;
   } else if (i < cn.lng) {
     vv[Vecs::b3 + (i - cn.b3)] = p;
   } else if (i < cn.lnb) {
@@ -356,7 +353,6 @@ DEV void write_shadow(const ShadowPtrs& sp, const Canon& cn, const Shadow& sh, s
     const int k = (int)(i - cn.wfc), o = k >> 10, j = k & 1023;
     const int jj = (j & 15) * OC3 + (j >> 4);
     w[sh.wfc + (size_t)o * FLAT + jj] = pt;
-    w[sh.wfct + (size_t)jj * HID + o] = pt;
   } else if (i < cn.wa) {
     vv[Vecs::bfc + (i - cn.bfc)] = p;
   } else if (i < cn.ba) {
@@ -394,10 +390,11 @@ struct RedSeg {
   const float* slab;  // [S][count]
   int S, count, kind;
   long long canon;    // canonical offset (for RK_LN: lng offset; lnb follows)
+  int sg;             // split groups per workgroup (power of two, <= 16)
 };
 struct RedArgs {
   RedSeg seg[MAX_RED_SEGS];
-  int start4[MAX_RED_SEGS + 1];  // prefix sums of count/4
+  int wg_start[MAX_RED_SEGS + 1];  // first workgroup of each segment
   int nseg;
   float* grads;
   Canon cn;
@@ -443,29 +440,42 @@ DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
   }
 }
 
+// Each segment is processed by workgroups of 256 threads = (256/SG) float4 columns x SG
+// split groups; split group g sums splits g, g+SG, ... and the SG partials are combined in
+// LDS in a fixed order (deterministic for a given SG).  wg_start[] holds each segment's
+// first workgroup.
 __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a) {
+  __shared__ f32x4 part[256];
   __shared__ float red[4];
-  const int g4 = blockIdx.x * 256 + threadIdx.x;
-  float sq = 0.f;
-  if (g4 < a.start4[a.nseg]) {
-    int s = 0;
-    while (g4 >= a.start4[s + 1]) ++s;
-    const RedSeg& sg = a.seg[s];
-    const int k = (g4 - a.start4[s]) * 4;
-    const float* p = sg.slab + k;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    int q = 0;
-    for (; q + 4 <= sg.S; q += 4) {
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 0) * sg.count);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 1) * sg.count);
-      const f32x4 v2 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 2) * sg.count);
-      const f32x4 v3 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 3) * sg.count);
+  int s = 0;
+  while ((int)blockIdx.x >= a.wg_start[s + 1]) ++s;
+  const RedSeg& sg = a.seg[s];
+  const int SG = sg.sg, cols = 256 / SG;
+  const int col = threadIdx.x % cols, grp = threadIdx.x / cols;
+  const int v4 = (blockIdx.x - a.wg_start[s]) * cols + col;  // float4 index in the segment
+  const bool in = v4 * 4 < sg.count;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (in) {
+    const float* p = sg.slab + (size_t)v4 * 4;
+    int q = grp;
+    for (; q + 3 * SG < sg.S; q += 4 * SG) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + (size_t)q * sg.count);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + SG) * sg.count);
+      const f32x4 v2 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 2 * SG) * sg.count);
+      const f32x4 v3 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 3 * SG) * sg.count);
       acc += v0;
       acc += v1;
       acc += v2;
       acc += v3;
     }
-    for (; q < sg.S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (size_t)q * sg.count);
+    for (; q < sg.S; q += SG) acc += *reinterpret_cast<const f32x4*>(p + (size_t)q * sg.count);
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  float sq = 0.f;
+  if (grp == 0 && in) {
+    for (int g2 = 1; g2 < SG; ++g2) acc += part[g2 * cols + col];
+    const int k = v4 * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const long long c = canon_index(a, sg, k + i);

@@ -7,12 +7,10 @@
 //
 //   w1  [32][192]        k = ci*64 + kh*8 + kw                      (conv1, = canonical)
 //   w2  [64][512]        k = (kh*4+kw)*32 + ci                       (conv2, channels-last)
-//   w2t [4][32][256]     class=(py,px); k = (j1*2+j2)*64 + oc, kh=py+2j1, kw=px+2j2 (dgrad)
 //   w3  [64][576]        k = (kh*3+kw)*64 + ci                       (conv3)
-//   w3t [64][576]        row ci, k = (kh*3+kw)*64 + oc               (conv3 dgrad)
 //   wfc [256][1024]      k = p*64 + c   (canonical column j = c*16 + p, NCHW flatten)
-//   wfct[1024][256]      row p*64 + c
 //   wh  [16][256]        rows 0..A-1 actor, row 15 critic, rest 0
+// (the dgrads read w2 / w3 / wfc k-major through LDS: no transposed copies)
 //   wht [256][32]        [j][o'], o' >= 16 zero
 //   f32: b1[32] b2[64] b3[64] lng[1024] lnb[1024] (p*64+c order) bfc[256] bh[16]
 #pragma once
@@ -59,7 +57,7 @@ inline Canon canon(int A) {
 
 // shadow-weight element offsets (elements of the compute type T), 64-element aligned
 struct Shadow {
-  size_t w1, w2, w2t, w3, w3t, wfc, wfct, wh, wht, total;
+  size_t w1, w2, w3, wfc, wh, wht, total;
 };
 constexpr size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 inline Shadow shadow() {
@@ -67,11 +65,8 @@ inline Shadow shadow() {
   size_t o = 0;
   s.w1 = o; o = al64(o + (size_t)OC1 * K1);
   s.w2 = o; o = al64(o + (size_t)OC2 * K2);
-  s.w2t = o; o = al64(o + (size_t)4 * OC1 * 4 * OC2);
   s.w3 = o; o = al64(o + (size_t)OC3 * K3);
-  s.w3t = o; o = al64(o + (size_t)OC2 * K3);
   s.wfc = o; o = al64(o + (size_t)HID * FLAT);
-  s.wfct = o; o = al64(o + (size_t)FLAT * HID);
   s.wh = o; o = al64(o + (size_t)HEADS * HID);
   s.wht = o; o = al64(o + (size_t)HID * HPAD);
   s.total = o;

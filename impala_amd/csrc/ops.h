@@ -12,6 +12,7 @@ using namespace net;
 // input (the x/255 of models/models.py:73 is folded into the epilogue: raw bytes are exact
 // in bf16).  Epilogue: *1/255 + bias, ReLU -> act1[n][oh][ow][oc].
 template <typename T> struct Conv1Fwd {
+  static constexpr bool A_KMAJOR = false;
   static constexpr int K = K1;
   int C;
   const T* w;
@@ -44,6 +45,7 @@ template <typename T> struct Conv1Fwd {
 
 // conv2: rows oc (64), cols (n, oh, ow) in N*36, k = (kh*4+kw)*32 + ci over act1.
 template <typename T> struct Conv2Fwd {
+  static constexpr bool A_KMAJOR = false;
   static constexpr int K = K2;
   int C;
   const T* w;
@@ -71,6 +73,7 @@ template <typename T> struct Conv2Fwd {
 // conv3: rows oc (64), cols (n, oh, ow) in N*16, k = (kh*3+kw)*64 + ci over act2.
 // act3 row n is the flattened feature vector in (p*64 + c) order.
 template <typename T> struct Conv3Fwd {
+  static constexpr bool A_KMAJOR = false;
   static constexpr int K = K3;
   int C;
   const T* w;
@@ -98,6 +101,7 @@ template <typename T> struct Conv3Fwd {
 // projection Linear(1024 -> 256) + exact GELU (models/models.py:67-68).
 // rows o (256), cols frame n, k = p*64 + c over the LayerNorm output y.
 template <typename T> struct FcFwd {
+  static constexpr bool A_KMAJOR = false;
   static constexpr int K = FLAT;
   int C;
   const T* w;
@@ -123,6 +127,7 @@ template <typename T> struct FcFwd {
 
 // actor ‖ critic heads fused into one 16-row GEMM (models/models.py:69-70, 76).
 template <typename T> struct HeadsFwd {
+  static constexpr bool A_KMAJOR = false;
   static constexpr int K = HID;
   int C;
   const T* w;
@@ -144,6 +149,7 @@ template <typename T> struct HeadsFwd {
 // ------------------------------- backward (dgrad) ---------------------------------------
 // dh = dH . Wh  then GELU backward:  dz[n][j] = dh[n][j] * gelu'(z[n][j]).  K = 32 (padded).
 template <typename T> struct HeadsDgrad {
+  static constexpr bool A_KMAJOR = false;
   static constexpr int K = HPAD;
   int C;
   const T* wt;  // [256][32]
@@ -164,15 +170,18 @@ template <typename T> struct HeadsDgrad {
 };
 
 // dy = dz . Wfc  (rows j in p*64+c order, cols frame), fp32 out for the LayerNorm backward.
+// A[j][o] = wfc[o][j]: read k-major from the forward weight (no transposed copy).
 template <typename T> struct FcDgrad {
+  static constexpr bool A_KMAJOR = true;
   static constexpr int K = HID;
   int C;
-  const T* wt;  // [1024][256]
+  const T* w;   // wfc [256][1024]
   const T* dz;
   float* dy;
   struct ColCtx { const T* p; };
   DEV ColCtx col_ctx(int c) const { return ColCtx{dz + (size_t)c * HID}; }
-  DEV const T* a_row(int r, int) const { return wt + r * K; }
+  DEV const T* a_row(int, int) const { return nullptr; }
+  DEV const T* a_kptr(int k, int r, int) const { return w + (size_t)k * FLAT + r; }
   DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const { return Frag<T>::load(cc.p + k); }
   DEV void store(int r, int c, float v[4]) const { store4(dy + (size_t)c * FLAT + r, v); }
 };
@@ -181,9 +190,10 @@ template <typename T> struct FcDgrad {
 // k = (kh*3+kw)*64 + oc; B = dact3[n][iy-kh][ix-kw][oc] (0 outside the 4x4 output).
 // Epilogue applies conv2's ReLU mask (act2 > 0).
 template <typename T> struct Conv3Dgrad {
+  static constexpr bool A_KMAJOR = true;
   static constexpr int K = K3;
   int C;
-  const T* wt;    // w3t [64][576]
+  const T* w;     // w3 [64 oc][576 = tap*64 + ci]; A[ci][tap*64 + oc] read k-major
   const T* dy;    // dact3 [n][16][64]
   const T* act;   // act2 (mask)
   T* dx;          // dact2
@@ -192,7 +202,11 @@ template <typename T> struct Conv3Dgrad {
     const int n = c / P2, p = c - n * P2, iy = p / H2, ix = p - iy * H2;
     return ColCtx{dy + (size_t)n * P3 * OC3, iy, ix};
   }
-  DEV const T* a_row(int r, int) const { return wt + r * K; }
+  DEV const T* a_row(int, int) const { return nullptr; }
+  DEV const T* a_kptr(int k, int r, int) const {
+    const int tap = k >> 6, oc = k & 63;
+    return w + (size_t)oc * K3 + tap * OC2 + r;
+  }
   DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const {
     const int tap = k >> 6, oc = k & 63, kh = tap / 3, kw = tap - kh * 3;
     const int oy = cc.iy - kh, ox = cc.ix - kw;
@@ -215,11 +229,12 @@ template <typename T> struct Conv3Dgrad {
 // kh = py + 2*j1, kw = px + 2*j2, oh = iy' - j1.
 // Epilogue applies conv1's ReLU mask (act1 > 0); ih/iw == 15 are outside the 15x15 map.
 template <typename T> struct Conv2Dgrad {
+  static constexpr bool A_KMAJOR = true;
   static constexpr int K = 4 * OC2;
   int C;        // 4 * NC
   int NC;       // columns per class (multiple of the tile width)
   int NQ;       // valid columns per class = N * 64
-  const T* wt;  // w2t [4][32][256]
+  const T* w;   // w2 [64 oc][512 = (kh*4+kw)*32 + ci]; A[ci][t*64 + oc] read k-major
   const T* dy;  // dact2 [n][36][64]
   const T* act; // act1 (mask)
   T* dx;        // dact1
@@ -228,7 +243,12 @@ template <typename T> struct Conv2Dgrad {
     const int cl = c / NC, q = min(c - cl * NC, NQ - 1), n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
     return ColCtx{dy + (size_t)n * P2 * OC2, iy, ix};
   }
-  DEV const T* a_row(int r, int cw) const { return wt + ((size_t)(cw / NC) * OC1 + r) * K; }
+  DEV const T* a_row(int, int) const { return nullptr; }
+  DEV const T* a_kptr(int k, int r, int cw) const {
+    const int cl = cw / NC, t = k >> 6, oc = k & 63;
+    const int kh = (cl >> 1) + 2 * (t >> 1), kw = (cl & 1) + 2 * (t & 1);
+    return w + (size_t)oc * K2 + (kh * KS2 + kw) * OC1 + r;
+  }
   DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const {
     const int t = k >> 6, oc = k & 63, j1 = t >> 1, j2 = t & 1;
     const int oy = cc.iy - j1, ox = cc.ix - j2;
