@@ -78,18 +78,20 @@ DEV Frag<float>::vec lds_frag_k(const float* tile, int ld, int lane) {
   return f32x4{a0[0], a0[ld], a0[2 * ld], a0[3 * ld]};
 }
 
-// LDS-staged tile GEMM for the same operand definitions as gemm_rc:
+// LDS-staged, persistent tile GEMM for the same operand definitions as gemm_rc:
 //   D[r][c] = sum_k A[r][k] * B(c, k),  WG tile BR x BC, K chunk BK.
-// Each K chunk of A (weights, row-major) and B (im2col / activation gather, 16-byte runs along
-// k) is loaded into registers one chunk ahead, stored k-contiguous into one of two LDS
-// buffers with 16-byte writes (rows padded by 16 B), and every wave reads its fragments with
-// ds_read_b128 -- operand reuse across the WG's waves comes from LDS instead of L1.
-// WR x WC waves, each owning (BR/WR) x (BC/WC) of the tile.  K % BK == 0, BR % (16*WR) == 0.
+// A persistent grid walks the (row-tile, col-tile) list; every K chunk of A (weights) and B
+// (im2col / activation gather, 16-byte runs along k) is loaded into registers one chunk
+// ahead -- across tile boundaries too, so a workgroup never waits on a cold prologue --
+// stored k-contiguous into one of two LDS buffers with 16-byte writes (rows padded by 16 B),
+// and every wave reads its fragments with ds_read_b128: operand reuse across the WG's waves
+// comes from LDS instead of L1.  WR x WC waves, each owning (BR/WR) x (BC/WC) of the tile.
 // Op::A_KMAJOR: A is stored transposed (a_kptr(k, r, c0) -> 16-byte run along r; e.g. the
 // forward weight consumed by a dgrad); its chunk is staged [k][r] and the A fragments are
 // read with the LDS transpose read, so no transposed weight copy is kept in HBM.
+// Requires K % BK == 0, R % BR == 0 and no A dependence on columns inside one BC tile.
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
-__global__ __launch_bounds__(256) void gemm_tile(const Op op) {
+__global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   constexpr bool AK = Op::A_KMAJOR;
   using F = Frag<T>;
   typedef typename F::vec V;
@@ -102,31 +104,39 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op) {
   constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
   constexpr int LDA = AK ? BR + VEC : LD; // A tile row length (elements)
   constexpr int ASZ = AK ? BK * LDA : BR * LD;
+  constexpr int NK = Op::K / BK;
   static_assert(WR * WC == 4 && TRW >= 1 && TCW >= 1, "tile");
   static_assert(BR * KV % 256 == 0 && BC * KV % 256 == 0, "staging");
   static_assert(Op::K % BK == 0 && BK % F::KSTEP == 0, "K chunking");
   __shared__ __attribute__((aligned(16))) T smem[2 * (ASZ + BC * LD)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
-  const int r0 = blockIdx.y * BR, c0 = blockIdx.x * BC;
   const int kv = tid % KV, rl = tid / KV;
-  // per-thread staging contexts (fixed rows / columns for the whole K loop)
+  const int n_tiles = n_rtiles * ((op.C + BC - 1) / BC);
+  const int ft = blockIdx.x;  // first tile of this workgroup
+  if (ft >= n_tiles) return;
+  // per-thread staging contexts of the fetch tile
   const T* arow[NA];
-  const int cw = min(c0, op.C - 1);
-  if constexpr (!AK) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) arow[i] = op.a_row(r0 + rl + i * RPP, cw);
-  }
   typename Op::ColCtx bctx[NB];
+  int fr0 = 0, fc0 = 0, fcw = 0;
+  auto set_ctx = [&](int t) {
+    fr0 = (t % n_rtiles) * BR;
+    fc0 = (t / n_rtiles) * BC;
+    fcw = min(fc0, op.C - 1);
+    if constexpr (!AK) {
 #pragma unroll
-  for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(c0 + rl + i * RPP, op.C - 1));
+      for (int i = 0; i < NA; ++i) arow[i] = op.a_row(fr0 + rl + i * RPP, fcw);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(fc0 + rl + i * RPP, op.C - 1));
+  };
   V ra[NA], rb[NB];
   auto fetch = [&](int k0) {
     if constexpr (AK) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int e = tid + i * 256, kr = e / RV, rv = e % RV;
-        ra[i] = F::load(op.a_kptr(k0 + kr, r0 + rv * VEC, cw));
+        ra[i] = F::load(op.a_kptr(k0 + kr, fr0 + rv * VEC, fcw));
       }
     } else {
 #pragma unroll
@@ -151,48 +161,59 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + (rl + i * RPP) * LD + kv * VEC) = rb[i];
   };
-  f32x4 acc[TRW][TCW];
-#pragma unroll
-  for (int i = 0; i < TRW; ++i)
-#pragma unroll
-    for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kl = F::KPL * (lane >> 4);
+  set_ctx(ft);
   fetch(0);
-  constexpr int NK = Op::K / BK;
-  for (int kc = 0; kc < NK; ++kc) {
-    const int buf = kc & 1;
-    stash(buf);
-    __syncthreads();
-    if (kc + 1 < NK) fetch((kc + 1) * BK);
-    const T* As = smem + buf * (ASZ + BC * LD);
-    const T* Bs = As + ASZ;
+  for (int t = ft; t < n_tiles; t += gridDim.x) {
+    const int cr0 = fr0, cc0 = fc0;  // coordinates of tile t (the fetch cursor is on it)
+    f32x4 acc[TRW][TCW];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += F::KSTEP) {
-      V a[TRW], b[TCW];
+    for (int i = 0; i < TRW; ++i)
 #pragma unroll
-      for (int i = 0; i < TRW; ++i) {
-        if constexpr (AK)
-          a[i] = lds_frag_k(As + kk * LDA + (wr * TRW + i) * 16, LDA, lane);
-        else
-          a[i] = *reinterpret_cast<const V*>(As + ((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl);
+      for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < NK; ++kc) {
+      const int buf = kc & 1;  // NK is even or the next tile restarts at buffer 0 after a sync
+      stash(buf);
+      __syncthreads();
+      if (kc + 1 < NK) {
+        fetch((kc + 1) * BK);
+      } else if (t + (int)gridDim.x < n_tiles) {
+        set_ctx(t + gridDim.x);  // prefetch the next tile's first chunk under this compute
+        fetch(0);
       }
+      const T* As = smem + buf * (ASZ + BC * LD);
+      const T* Bs = As + ASZ;
 #pragma unroll
-      for (int j = 0; j < TCW; ++j)
-        b[j] = *reinterpret_cast<const V*>(Bs + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
+      for (int kk = 0; kk < BK; kk += F::KSTEP) {
+        V a[TRW], b[TCW];
 #pragma unroll
-      for (int i = 0; i < TRW; ++i)
+        for (int i = 0; i < TRW; ++i) {
+          if constexpr (AK)
+            a[i] = lds_frag_k(As + kk * LDA + (wr * TRW + i) * 16, LDA, lane);
+          else
+            a[i] = *reinterpret_cast<const V*>(As + ((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl);
+        }
 #pragma unroll
-        for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < TCW; ++j)
+          b[j] = *reinterpret_cast<const V*>(Bs + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
+#pragma unroll
+        for (int i = 0; i < TRW; ++i)
+#pragma unroll
+          for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+      }
     }
-  }
+    if constexpr (NK % 2 == 1) __syncthreads();  // next tile reuses buffer 0 first
 #pragma unroll
-  for (int j = 0; j < TCW; ++j) {
-    const int c = c0 + (wc * TCW + j) * 16 + (lane & 15);
-    if (c >= op.C) continue;
+    for (int j = 0; j < TCW; ++j) {
+      const int c = cc0 + (wc * TCW + j) * 16 + (lane & 15);
+      if (c < op.C) {
 #pragma unroll
-    for (int i = 0; i < TRW; ++i) {
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      op.store(r0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
+        for (int i = 0; i < TRW; ++i) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
+        }
+      }
     }
   }
 }
@@ -201,29 +222,35 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op) {
 // blockIdx.z.  X is a row-major [M][x_ld] matrix (the channels-last output gradient); Y is a
 // gather (im2col of the layer input) returning 16-byte runs along c.  Each BM-row chunk of both
 // is staged row-major into LDS with 16-byte stores and the MFMA fragments are read along m
-// with the hardware transpose read (bf16).  A workgroup holds G independent 4-wave groups
-// working on interleaved chunks (G x the loads in flight per CU without more partial slabs);
-// their accumulators are summed in a fixed order at the end.  Output: fp32 partial slab
-// [split][R][C] (+ per-split bias sums).
+// with the hardware transpose read (bf16).  The next chunk is loaded into registers while the
+// current one is multiplied (double-buffered LDS, one barrier per chunk), and a workgroup holds
+// G independent 4-wave groups on interleaved chunks (more loads in flight per CU without more
+// partial slabs); the groups' accumulators are summed in a fixed order at the end.
+// Output: fp32 partial slab [split][R][C] (+ per-split bias sums).
 template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op>
 __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restrict__ slab,
                                                    float* __restrict__ slab_bias,
                                                    int m_per_split) {
   using F = Frag<T>;
+  typedef typename F::vec V;  // 16 bytes of T
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int LDX = BR + VEC, LDY = BC + VEC;
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NACC = TRW * TCW * 4;
-  constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per group
+  constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per buffer
+  constexpr int NXV = BM * (BR / VEC), NYV = BM * (BC / VEC);
+  constexpr int NX = (NXV + 255) / 256;
+  // Y staging: thread t owns m-row (t % BM) of the chunk and column vectors t/BM + i*(256/BM),
+  // so the im2col row context (n, oy, ox) is derived once per chunk, not per vector.
+  constexpr int YCS = 256 / BM, NY = (BC / VEC + YCS - 1) / YCS;
+  static_assert(256 % BM == 0, "Y staging");
   static_assert(WR * WC == 4, "4 waves per group");
   static_assert(TRW >= 1 && TCW >= 1 && BR % 16 == 0 && BC % 16 == 0, "tile");
   static_assert(BM % F::KSTEP == 0, "chunk");
-  static_assert((size_t)STAGE * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
+  static_assert((size_t)STAGE * 2 * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
                 "LDS reuse for the group reduction");
-  __shared__ __attribute__((aligned(16))) T smem[STAGE * G];
+  __shared__ __attribute__((aligned(16))) T smem[STAGE * 2 * G];
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-  T* Xs = smem + grp * STAGE;
-  T* Ys = Xs + BM * LDX;
   const int c0 = blockIdx.x * BC, r0 = blockIdx.y * BR, split = blockIdx.z;
   const int m_beg = split * m_per_split;
   const int m_end = min(op.M, m_beg + m_per_split);
@@ -235,34 +262,60 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
 #pragma unroll
     for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bias_acc = 0.f;
-  typedef typename F::vec V;  // 16 bytes of T
+  V rx[NX], ry[NY];
+  auto fetch = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int e = tid + i * 256, mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
+      rx[i] = (e < NXV && m0 + mm < m_end)
+                  ? *reinterpret_cast<const V*>(op.x + (size_t)(m0 + mm) * op.x_ld + r0 + rr)
+                  : F::zero();
+    }
+    {
+      const int mm = tid % BM, cv0 = tid / BM;
+      const bool mok = m0 + mm < m_end;
+      const auto yc = op.y_row(mok ? m0 + mm : m_beg);
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        const int cv = cv0 + i * YCS, cc = cv * VEC;
+        ry[i] = (cv < BC / VEC && mok && c0 + cc < op.C) ? op.load_y(yc, c0 + cc) : F::zero();
+      }
+    }
+  };
+  auto stash = [&](T* Xs) {
+    T* Ys = Xs + BM * LDX;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int e = tid + i * 256, mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
+      if (e < NXV) *reinterpret_cast<V*>(Xs + mm * LDX + rr) = rx[i];
+    }
+    {
+      const int mm = tid % BM, cv0 = tid / BM;
+#pragma unroll
+      for (int i = 0; i < NY; ++i) {
+        const int cv = cv0 + i * YCS;
+        if (cv < BC / VEC) *reinterpret_cast<V*>(Ys + mm * LDY + cv * VEC) = ry[i];
+      }
+    }
+  };
   const int n_it = (m_end - m_beg + BM * G - 1) / (BM * G);
+  if (n_it > 0) fetch(m_beg + grp * BM);
   for (int it = 0; it < n_it; ++it) {
     const int m0 = m_beg + (it * G + grp) * BM;
     const bool active = m0 < m_end;
-    if (active) {
-      for (int e = tid; e < BM * (BR / VEC); e += 256) {
-        const int mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
-        V v;
-        if (m0 + mm < m_end)
-          v = *reinterpret_cast<const V*>(op.x + (size_t)(m0 + mm) * op.x_ld + r0 + rr);
-        else
-          v = F::zero();
-        *reinterpret_cast<V*>(Xs + mm * LDX + rr) = v;
-      }
-      for (int e = tid; e < BM * (BC / VEC); e += 256) {
-        const int mm = e / (BC / VEC), cc = (e % (BC / VEC)) * VEC;
-        V v;
-        if (m0 + mm < m_end && c0 + cc < op.C) v = op.load_y(m0 + mm, c0 + cc);
-        else v = F::zero();
-        *reinterpret_cast<V*>(Ys + mm * LDY + cc) = v;
-      }
-    }
+    T* Xs = smem + (grp * 2 + (it & 1)) * STAGE;
+    const T* Ys = Xs + BM * LDX;
+    if (active) stash(Xs);
     __syncthreads();
+    if (it + 1 < n_it) fetch(m0 + G * BM);  // in flight under this chunk's MFMAs
     if (active) {
-      if (do_bias && tid < BR) {
-#pragma unroll 8
-        for (int mm = 0; mm < BM; ++mm) bias_acc += (float)Xs[mm * LDX + tid];
+      if (do_bias) {  // (256/BR) row groups x BR channels; summed across groups at the end
+        constexpr int RG = 256 / BR;
+        const int rch = tid % BR, rg = tid / BR;
+        float s0 = 0.f;
+#pragma unroll
+        for (int mm = rg; mm < BM; mm += RG) s0 += (float)Xs[mm * LDX + rch];
+        bias_acc += s0;
       }
 #pragma unroll
       for (int kk = 0; kk < BM; kk += F::KSTEP) {
@@ -279,8 +332,8 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
           for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   // fixed-order reduction of the G groups' accumulators through (reused) LDS
   if constexpr (G > 1) {
     float* red = reinterpret_cast<float*>(smem);
@@ -306,8 +359,20 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
       }
       __syncthreads();
     }
-    if (grp != 0) return;
   }
+  if (do_bias) {  // combine the (256/BR) row groups of group 0's bias sums, fixed order
+    constexpr int RG = 256 / BR;
+    float* redb = reinterpret_cast<float*>(smem);
+    if (grp == 0) redb[tid] = bias_acc;
+    __syncthreads();
+    if (grp == 0 && tid < BR) {
+      float bsum = 0.f;
+#pragma unroll
+      for (int g = 0; g < RG; ++g) bsum += redb[g * BR + tid];
+      slab_bias[(size_t)split * op.R + r0 + tid] = bsum;
+    }
+  }
+  if (grp != 0) return;
   const float sc = op.out_scale;
 #pragma unroll
   for (int j = 0; j < TCW; ++j) {
@@ -321,5 +386,4 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
         slab[((size_t)split * op.R + r + q) * op.C + c] = acc[i][j][q] * sc;
     }
   }
-  if (do_bias && tid < BR) slab_bias[(size_t)split * op.R + r0 + tid] = bias_acc;
 }

@@ -9,7 +9,9 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <string>
 
@@ -107,12 +109,25 @@ struct impala_learner {
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   RedArgs red{};
+  // side stream for the weight-gradient branches (fork/join with events, graph-capturable)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_join = nullptr;
+  bool use_side = true;
   // live launch timer: hipEvent pairs around every launch of one kernel id
+  int n_cu = 256;
+  int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
   hipEvent_t* timer_ev = nullptr;
 };
 
 namespace {
+// persistent grid for gemm_tile: a few workgroups per CU, never more than the tile count
+inline int persist_grid(const impala_learner* h, long tiles) {
+  const long cap = (long)h->n_cu * 3;
+  return (int)(tiles < cap ? tiles : cap);
+}
+
 inline void timer_begin(impala_learner* h, int kid, hipStream_t st) {
   if (h->timer_kernel == kid && h->timer_n < h->timer_cap)
     (void)hipEventRecord(h->timer_ev[2 * h->timer_n], st);
@@ -134,24 +149,22 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
-  {
-    Conv1Fwd<T> op{n * P1, sw + sh.w1, vv + Vecs::b1, obs, (T*)h->act1};
-    timer_begin(h, K_CONV1_FWD, st);
-    gemm_tile<T, 32, 128, TBK, 1, 4><<<dim3(cdiv((long)n * P1, 128), 1), 256, 0, st>>>(op);
-    timer_end(h, K_CONV1_FWD, st);
-    CK_LAUNCH("conv1_fwd");
-  }
+  timer_begin(h, K_CONV1_FWD, st);
+  conv1_fwd_s2d<T><<<min(n, h->n_cu * 2), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
+                                                         (T*)h->act1, n);
+  timer_end(h, K_CONV1_FWD, st);
+  CK_LAUNCH("conv1_fwd");
   {
     Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
     timer_begin(h, K_CONV2_FWD, st);
-    gemm_tile<T, 64, 128, TBK, 1, 4><<<dim3(cdiv((long)n * P2, 128), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 128, TBK, 1, 4><<<persist_grid(h, (long)(cdiv((long)n * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV2_FWD, st);
     CK_LAUNCH("conv2_fwd");
   }
   {
     Conv3Fwd<T> op{n * P3, sw + sh.w3, vv + Vecs::b3, (const T*)h->act2, (T*)h->act3};
     timer_begin(h, K_CONV3_FWD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv((long)n * P3, 64), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_FWD, st);
     CK_LAUNCH("conv3_fwd");
   }
@@ -163,7 +176,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
     timer_begin(h, K_FC_FWD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv(n, 64), HID / 64), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv(n, 64)) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
     timer_end(h, K_FC_FWD, st);
     CK_LAUNCH("fc_fwd");
   }
@@ -201,6 +214,26 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     timer_end(h, K_LOSS, st);
     CK_LAUNCH("loss_head");
   }
+  // ---- dgrad chain on `st`; each weight-gradient branch forks onto the side stream as soon
+  // as its inputs exist and joins before the slab reduction ----
+  constexpr int WBM = sizeof(T) == 4 ? 32 : 64;  // m-chunk of gemm_wg (LDS budget of f32)
+  hipStream_t ss = h->use_side ? h->side : st;
+  auto fork = [&](int i) -> int {
+    if (!h->use_side) return 0;
+    CK(hipEventRecord(h->ev_fork[i], st));
+    CK(hipStreamWaitEvent(ss, h->ev_fork[i], 0));
+    return 0;
+  };
+  if (int r = fork(0)) return r;  // dH, h ready
+  {
+    HeadsWgrad<T> op{};
+    op.M = N; op.x = (const T*)h->dH; op.h = (const T*)h->h;
+    timer_begin(h, K_HEADS_WGRAD, ss);
+    gemm_wg<T, 16, 256, 1, 4, WBM, 1><<<dim3(1, 1, h->sph.S), 256, 0, ss>>>(op, h->s_h, h->s_bh,
+                                                                         h->sph.mps);
+    timer_end(h, K_HEADS_WGRAD, ss);
+    CK_LAUNCH("heads_wgrad");
+  }
   {
     HeadsDgrad<T> op{N, sw + sh.wht, (const T*)h->dH, h->z, (T*)h->dz};
     timer_begin(h, K_HEADS_DGRAD, st);
@@ -208,10 +241,20 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     timer_end(h, K_HEADS_DGRAD, st);
     CK_LAUNCH("heads_dgrad");
   }
+  if (int r = fork(1)) return r;  // dz ready
+  {
+    FcWgrad<T> op{};
+    op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
+    timer_begin(h, K_FC_WGRAD, ss);
+    gemm_wg<T, 64, 256, 1, 4, WBM, 1><<<dim3(FLAT / 256, HID / 64, h->spfc.S), 256, 0, ss>>>(
+        op, h->s_fc, h->s_bfc, h->spfc.mps);
+    timer_end(h, K_FC_WGRAD, ss);
+    CK_LAUNCH("fc_wgrad");
+  }
   {
     FcDgrad<T> op{N, sw + sh.wfc, (const T*)h->dz, h->dy};
     timer_begin(h, K_FC_DGRAD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<dim3(cdiv(N, 64), FLAT / 64), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv(N, 64)) * (FLAT / 64)), 256, 0, st>>>(op, FLAT / 64);
     timer_end(h, K_FC_DGRAD, st);
     CK_LAUNCH("fc_dgrad");
   }
@@ -221,68 +264,50 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
                                                 h->ln_fpw);
   timer_end(h, K_LN_BWD, st);
   CK_LAUNCH("ln_bwd");
+  if (int r = fork(2)) return r;  // dact3 ready
+  {
+    Conv3Wgrad<T> op{};
+    op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
+    timer_begin(h, K_CONV3_WGRAD, ss);
+    gemm_wg<T, 64, 192, 1, 4, WBM, 2><<<dim3(K3 / 192, 1, h->sp3.S), 512, 0, ss>>>(
+        op, h->s_w3, h->s_b3, h->sp3.mps);
+    timer_end(h, K_CONV3_WGRAD, ss);
+    CK_LAUNCH("conv3_wgrad");
+  }
   {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
     timer_begin(h, K_CONV3_DGRAD, st);
-    gemm_tile<T, 64, 128, TBK, 1, 4><<<dim3(cdiv((long)N * P2, 128), 1), 256, 0, st>>>(op);
+    gemm_tile<T, 64, 128, TBK, 1, 4><<<persist_grid(h, (long)(cdiv((long)N * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_DGRAD, st);
     CK_LAUNCH("conv3_dgrad");
+  }
+  if (int r = fork(3)) return r;  // dact2 ready
+  {
+    Conv2Wgrad<T> op{};
+    op.M = N * P2; op.x = (const T*)h->dact2; op.in = (const T*)h->act1;
+    timer_begin(h, K_CONV2_WGRAD, ss);
+    gemm_wg<T, 64, 128, 1, 4, WBM, 2><<<dim3(K2 / 128, 1, h->sp2.S), 512, 0, ss>>>(
+        op, h->s_w2, h->s_b2, h->sp2.mps);
+    timer_end(h, K_CONV2_WGRAD, ss);
+    CK_LAUNCH("conv2_wgrad");
   }
   {
     const int NC = (N * 64 + 127) / 128 * 128;  // class stride, multiple of the tile width
     Conv2Dgrad<T> op{4 * NC, NC, N * 64, sw + sh.w2, (const T*)h->dact2, (const T*)h->act1,
                      (T*)h->dact1};
     timer_begin(h, K_CONV2_DGRAD, st);
-    gemm_tile<T, 32, 128, TBK, 1, 4><<<dim3(4 * NC / 128, 1), 256, 0, st>>>(op);
+    gemm_tile<T, 32, 128, TBK, 1, 4><<<persist_grid(h, (long)(4 * NC / 128) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV2_DGRAD, st);
     CK_LAUNCH("conv2_dgrad");
   }
-  // ---- weight gradients (split-M partial slabs) ----
-  constexpr int WBM = sizeof(T) == 4 ? 32 : 64;  // m-chunk (LDS budget of the f32 mode)
-  {
-    HeadsWgrad<T> op{};
-    op.M = N; op.x = (const T*)h->dH; op.h = (const T*)h->h;
-    timer_begin(h, K_HEADS_WGRAD, st);
-    gemm_wg<T, 16, 256, 1, 4, WBM, 1><<<dim3(1, 1, h->sph.S), 256, 0, st>>>(op, h->s_h, h->s_bh,
-                                                                        h->sph.mps);
-    timer_end(h, K_HEADS_WGRAD, st);
-    CK_LAUNCH("heads_wgrad");
-  }
-  {
-    FcWgrad<T> op{};
-    op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
-    timer_begin(h, K_FC_WGRAD, st);
-    gemm_wg<T, 64, 256, 1, 4, WBM, 2><<<dim3(FLAT / 256, HID / 64, h->spfc.S), 512, 0, st>>>(
-        op, h->s_fc, h->s_bfc, h->spfc.mps);
-    timer_end(h, K_FC_WGRAD, st);
-    CK_LAUNCH("fc_wgrad");
-  }
-  {
-    Conv3Wgrad<T> op{};
-    op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
-    timer_begin(h, K_CONV3_WGRAD, st);
-    gemm_wg<T, 64, 192, 1, 4, WBM, 4><<<dim3(K3 / 192, 1, h->sp3.S), 1024, 0, st>>>(
-        op, h->s_w3, h->s_b3, h->sp3.mps);
-    timer_end(h, K_CONV3_WGRAD, st);
-    CK_LAUNCH("conv3_wgrad");
-  }
-  {
-    Conv2Wgrad<T> op{};
-    op.M = N * P2; op.x = (const T*)h->dact2; op.in = (const T*)h->act1;
-    timer_begin(h, K_CONV2_WGRAD, st);
-    gemm_wg<T, 64, 128, 1, 4, WBM, 4><<<dim3(K2 / 128, 1, h->sp2.S), 1024, 0, st>>>(
-        op, h->s_w2, h->s_b2, h->sp2.mps);
-    timer_end(h, K_CONV2_WGRAD, st);
-    CK_LAUNCH("conv2_wgrad");
-  }
-  {
-    Conv1Wgrad<T> op{};
-    op.M = N * P1; op.x = (const T*)h->dact1; op.img = b->obs;
-    timer_begin(h, K_CONV1_WGRAD, st);
-    gemm_wg<T, 32, 192, 1, 4, WBM, 4><<<dim3(1, 1, h->sp1.S), 1024, 0, st>>>(op, h->s_w1, h->s_b1,
-                                                                        h->sp1.mps);
-    timer_end(h, K_CONV1_WGRAD, st);
-    CK_LAUNCH("conv1_wgrad");
+  timer_begin(h, K_CONV1_WGRAD, st);
+  conv1_wgrad_s2d<T><<<h->c1_wg, 256, 0, st>>>(b->obs, (const T*)h->dact1, h->s_w1, h->s_b1, N,
+                                               h->c1_fpw);
+  timer_end(h, K_CONV1_WGRAD, st);
+  CK_LAUNCH("conv1_wgrad");
+  if (h->use_side) {  // join
+    CK(hipEventRecord(h->ev_join, ss));
+    CK(hipStreamWaitEvent(st, h->ev_join, 0));
   }
   // ---- slab reduction -> canonical grads, sum of squares, loss metrics, step += 1 ----
   timer_begin(h, K_REDUCE, st);
@@ -304,7 +329,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
   aa.cn = h->cn; aa.sh = h->sh;
   timer_begin(h, K_ADAM, st);
-  adam_kernel<T><<<h->n_adam_wg, 256, 0, st>>>(aa);
+  adam_kernel<T><<<cdiv((long)(h->cn.total + 3) / 4, 256), 256, 0, st>>>(aa);
   timer_end(h, K_ADAM, st);
   CK_LAUNCH("adam");
   return 0;
@@ -381,6 +406,12 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->A = cfg->num_actions;
   h->bf16 = cfg->dtype == IMPALA_DTYPE_BF16;
   h->N = cfg->batch_size * cfg->rollout_length;
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cu > 0)
+      h->n_cu = cu;
+  }
   h->cn = canon(h->A);
   h->sh = shadow();
   const int N = h->N;
@@ -396,7 +427,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), 96);
   h->sp3 = plan_split((long)N * P3, K3 / 192, 192);
   h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
-  h->sp1 = plan_split((long)N * P1, 1, 256);
+  h->c1_fpw = std::max(1, cdiv(N, h->n_cu));
+  h->c1_wg = cdiv(N, h->c1_fpw);
+  h->sp1.S = h->c1_wg;  // slab splits of conv1 (one per workgroup)
 
   // ---- one workspace allocation, 256-byte aligned carve ----
   size_t off = 0;
@@ -462,6 +495,19 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->s_h = (float*)(w + o_sh); h->s_bh = (float*)(w + o_sbh);
   h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
   h->step = (int64_t*)(w + o_step);
+  const char* serial = std::getenv("IMPALA_SERIAL_STREAM");  // profiling: one stream only
+  if (serial && serial[0] == '1') {
+    h->use_side = false;
+  } else if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) {
+    h->use_side = false;
+    h->side = nullptr;
+  } else {
+    for (int i = 0; i < 4; ++i)
+      if (hipEventCreateWithFlags(&h->ev_fork[i], hipEventDisableTiming) != hipSuccess)
+        h->use_side = false;
+    if (hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
+      h->use_side = false;
+  }
   {
     RedArgs& ra = h->red;
     int ns = 0;
@@ -473,7 +519,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
       ++ns;
     };
     ra.wg_start[0] = 0;
-    add(h->s_w1, h->sp1.S, OC1 * K1, RK_ID, (long long)h->cn.w1);
+    add(h->s_w1, h->sp1.S, OC1 * K1, RK_CONV1, (long long)h->cn.w1);
     add(h->s_b1, h->sp1.S, OC1, RK_ID, (long long)h->cn.b1);
     add(h->s_w2, h->sp2.S, OC2 * K2, RK_CONV2, (long long)h->cn.w2);
     add(h->s_b2, h->sp2.S, OC2, RK_ID, (long long)h->cn.b2);
@@ -506,6 +552,13 @@ int impala_destroy(impala_learner* h) {
   if (h->timer_ev) {
     for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
     delete[] h->timer_ev;
+  }
+  for (int i = 0; i < 4; ++i)
+    if (h->ev_fork[i]) (void)hipEventDestroy(h->ev_fork[i]);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->side) {
+    (void)hipStreamSynchronize(h->side);
+    (void)hipStreamDestroy(h->side);
   }
   if (h->ws) (void)hipFree(h->ws);
   delete h;

@@ -2,6 +2,7 @@
 // forward and backward, gradient-slab reduction, global-norm clip + Adam, weight repacking.
 #pragma once
 #include "common.h"
+#include "conv1.h"
 #include "net.h"
 
 using namespace net;
@@ -329,7 +330,8 @@ DEV void write_shadow(const ShadowPtrs& sp, const Canon& cn, const Shadow& sh, s
   float* vv = sp.vecs;
   const T pt = (T)p;
   if (i < cn.b1) {
-    w[sh.w1 + i] = pt;
+    const int k = (int)i, oc = k / K1, rem = k - oc * K1;
+    w[sh.w1 + oc * K1 + c1_kprime(rem >> 6, (rem >> 3) & 7, rem & 7)] = pt;
   } else if (i < cn.w2) {
     vv[Vecs::b1 + (i - cn.b1)] = p;
   } else if (i < cn.b2) {
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(256) void pack_params_kernel(const float* __restric
 // computed on the write side.  Also: per-block sum of squares (clip norm), loss-metric
 // finalisation and the Adam step counter increment (block 0).
 // =========================================================================================
-enum RedKind { RK_ID = 0, RK_CONV2, RK_CONV3, RK_LN, RK_FC, RK_HEADS_W, RK_HEADS_B };
+enum RedKind { RK_ID = 0, RK_CONV2, RK_CONV3, RK_LN, RK_FC, RK_HEADS_W, RK_HEADS_B, RK_CONV1 };
 constexpr int MAX_RED_SEGS = 12;
 struct RedSeg {
   const float* slab;  // [S][count]
@@ -408,6 +410,10 @@ struct RedArgs {
 
 DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
   switch (sg.kind) {
+    case RK_CONV1: {  // k = oc*192 + k' (s2d order)  ->  oc*192 + ci*64 + kh*8 + kw
+      const int oc = k / K1;
+      return sg.canon + oc * K1 + c1_canon_k(k - oc * K1);
+    }
     case RK_CONV2: {  // k = oc*512 + tap*32 + ci  ->  oc*512 + ci*16 + tap
       const int oc = k >> 9, rem = k & 511, tap = rem >> 5, ci = rem & 31;
       return sg.canon + oc * K2 + ci * 16 + tap;
@@ -528,37 +534,65 @@ struct AdamArgs {
 template <typename T>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   __shared__ float red[4];
+  __shared__ float sc[3];  // step_size, sqrt(bias_correction2), coef
   float s = 0.f;
   for (int p = threadIdx.x; p < a.n_part; p += 256) s += a.sumsq_part[p];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  const float tot = red[0] + red[1] + red[2] + red[3];
-  const float norm = sqrtf(tot) * a.inv_world;
-  const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.f);
-  const double stepd = (double)*a.step;
-  const double bc1 = 1.0 - pow(a.b1, stepd), bc2 = 1.0 - pow(a.b2, stepd);
-  const float step_size = (float)(a.lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
+  if (threadIdx.x == 0) {
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    const float norm = sqrtf(tot) * a.inv_world;
+    const double stepd = (double)*a.step;
+    const double bc1 = 1.0 - pow(a.b1, stepd), bc2 = 1.0 - pow(a.b2, stepd);
+    sc[0] = (float)(a.lr / bc1);
+    sc[1] = (float)sqrt(bc2);
+    sc[2] = fminf(a.max_norm / (norm + 1e-6f), 1.f);
+    if (blockIdx.x == 0) {
+      a.metrics[6] = norm;
+      a.metrics[7] = (float)stepd;
+    }
+  }
+  __syncthreads();
+  const float step_size = sc[0], bc2s = sc[1], gscale = a.inv_world * sc[2];
   const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < a.cn.total;
-       i += (size_t)gridDim.x * 256) {
-    const float g = a.grads[i] * a.inv_world * coef;
-    a.grads[i] = g;
-    float m = a.m[i], v = a.v[i];
-    m = m + w1 * (g - m);
-    v = v * b2f + w2 * g * g;
-    const float denom = sqrtf(v) / bc2s + a.eps;
-    const float p = a.params[i] - step_size * (m / denom);
-    a.m[i] = m;
-    a.v[i] = v;
-    a.params[i] = p;
-    write_shadow<T>(a.sp, a.cn, a.sh, i, p);
+  const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= a.cn.total) return;
+  const int n = (int)min((size_t)4, a.cn.total - i0);
+  float g[4], m[4], v[4], p[4];
+  if (n == 4) {
+    const f32x4 G = *reinterpret_cast<const f32x4*>(a.grads + i0);
+    const f32x4 M = *reinterpret_cast<const f32x4*>(a.m + i0);
+    const f32x4 Vv = *reinterpret_cast<const f32x4*>(a.v + i0);
+    const f32x4 P = *reinterpret_cast<const f32x4*>(a.params + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { g[k] = G[k]; m[k] = M[k]; v[k] = Vv[k]; p[k] = P[k]; }
+  } else {
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = k < n;
+      g[k] = ok ? a.grads[i0 + k] : 0.f; m[k] = ok ? a.m[i0 + k] : 0.f;
+      v[k] = ok ? a.v[i0 + k] : 0.f;     p[k] = ok ? a.params[i0 + k] : 0.f;
+    }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    a.metrics[6] = norm;
-    a.metrics[7] = (float)stepd;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    g[k] = g[k] * gscale;
+    m[k] = m[k] + w1 * (g[k] - m[k]);
+    v[k] = v[k] * b2f + w2 * g[k] * g[k];
+    const float denom = sqrtf(v[k]) / bc2s + a.eps;
+    p[k] = p[k] - step_size * (m[k] / denom);
   }
+  if (n == 4) {
+    *reinterpret_cast<f32x4*>(a.grads + i0) = f32x4{g[0], g[1], g[2], g[3]};
+    *reinterpret_cast<f32x4*>(a.m + i0) = f32x4{m[0], m[1], m[2], m[3]};
+    *reinterpret_cast<f32x4*>(a.v + i0) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(a.params + i0) = f32x4{p[0], p[1], p[2], p[3]};
+  } else {
+    for (int k = 0; k < n; ++k) {
+      a.grads[i0 + k] = g[k]; a.m[i0 + k] = m[k]; a.v[i0 + k] = v[k]; a.params[i0 + k] = p[k];
+    }
+  }
+  for (int k = 0; k < n; ++k) write_shadow<T>(a.sp, a.cn, a.sh, i0 + k, p[k]);
 }
 
 // heads output [n][16] -> logits [n][A], values [n]

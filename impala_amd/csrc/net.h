@@ -5,7 +5,7 @@
 // (SURVEY.md §8(a) a6).  The kernels never read them: the Adam kernel (and pack_params at
 // bind time) re-emits every weight in the layout and dtype each GEMM consumes:
 //
-//   w1  [32][192]        k = ci*64 + kh*8 + kw                      (conv1, = canonical)
+//   w1  [32][192]        k' = tap*48 + ci*16 + (kh%4)*4 + kw%4, tap = (kh/4)*2 + kw/4 (s2d)
 //   w2  [64][512]        k = (kh*4+kw)*32 + ci                       (conv2, channels-last)
 //   w3  [64][576]        k = (kh*3+kw)*64 + ci                       (conv3)
 //   wfc [256][1024]      k = p*64 + c   (canonical column j = c*16 + p, NCHW flatten)

@@ -280,8 +280,9 @@ template <typename T> struct HeadsWgrad {  // dWh[o'][j] = sum_n dH[n][o'] h[n][
   const T* x;  // dH [n][32]
   int x_ld = HPAD;
   const T* h;
-  DEV typename Frag<T>::vec load_y(int m, int c) const {
-    return *reinterpret_cast<const typename Frag<T>::vec*>(h + (size_t)m * HID + c);
+  DEV const T* y_row(int m) const { return h + (size_t)m * HID; }
+  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
+    return *reinterpret_cast<const typename Frag<T>::vec*>(row + c);
   }
 };
 template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
@@ -291,8 +292,9 @@ template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
   const T* x;  // dz
   int x_ld = HID;
   const T* y;
-  DEV typename Frag<T>::vec load_y(int m, int c) const {
-    return *reinterpret_cast<const typename Frag<T>::vec*>(y + (size_t)m * FLAT + c);
+  DEV const T* y_row(int m) const { return y + (size_t)m * FLAT; }
+  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
+    return *reinterpret_cast<const typename Frag<T>::vec*>(row + c);
   }
 };
 template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3+kw)*64 + ci
@@ -302,11 +304,13 @@ template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3
   const T* x;  // dact3
   int x_ld = OC3;
   const T* in;  // act2
-  DEV typename Frag<T>::vec load_y(int m, int c) const {
+  DEV const T* y_row(int m) const {  // top-left input pixel of the 3x3 patch
     const int n = m / P3, p = m - n * P3, oy = p / H3, ox = p - oy * H3;
+    return in + ((size_t)(n * H2 + oy) * H2 + ox) * OC2;
+  }
+  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
     const int tap = c >> 6, ci = c & 63, kh = tap / 3, kw = tap - kh * 3;
-    return *reinterpret_cast<const typename Frag<T>::vec*>(
-        in + ((size_t)(n * H2 + oy + kh) * H2 + ox + kw) * OC2 + ci);
+    return *reinterpret_cast<const typename Frag<T>::vec*>(row + (kh * H2 + kw) * OC2 + ci);
   }
 };
 template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4+kw)*32 + ci
@@ -316,11 +320,13 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
   const T* x;  // dact2
   int x_ld = OC2;
   const T* in;  // act1
-  DEV typename Frag<T>::vec load_y(int m, int c) const {
+  DEV const T* y_row(int m) const {
     const int n = m / P2, p = m - n * P2, oy = p / H2, ox = p - oy * H2;
+    return in + ((size_t)(n * H1 + ST2 * oy) * H1 + ST2 * ox) * OC1;
+  }
+  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
     const int tap = c >> 5, ci = c & 31, kh = tap >> 2, kw = tap & 3;
-    return *reinterpret_cast<const typename Frag<T>::vec*>(
-        in + ((size_t)(n * H1 + ST2 * oy + kh) * H1 + ST2 * ox + kw) * OC1 + ci);
+    return *reinterpret_cast<const typename Frag<T>::vec*>(row + (kh * H1 + kw) * OC1 + ci);
   }
 };
 template <typename T> struct Conv1Wgrad {  // m = (n, oy, ox) in N*225; c = ci*64 + kh*8 + kw
@@ -330,10 +336,13 @@ template <typename T> struct Conv1Wgrad {  // m = (n, oy, ox) in N*225; c = ci*6
   const T* x;  // dact1
   int x_ld = OC1;
   const uint8_t* img;
-  DEV typename Frag<T>::vec load_y(int m, int c) const {
+  DEV const uint8_t* y_row(int m) const {
     const int n = m / P1, p = m - n * P1, oy = p / H1, ox = p - oy * H1;
+    return img + (size_t)n * IMG + (ST1 * oy) * H0 + ST1 * ox;
+  }
+  DEV typename Frag<T>::vec load_y(const uint8_t* row, int c) const {
     const int ci = c >> 6, kh = (c >> 3) & 7, kw = c & 7;
-    const uint8_t* q = img + (size_t)n * IMG + ci * (H0 * H0) + (ST1 * oy + kh) * H0 + ST1 * ox + kw;
+    const uint8_t* q = row + ci * (H0 * H0) + kh * H0 + kw;
     if constexpr (sizeof(T) == 4) {
       return Frag<float>::from_u8(*reinterpret_cast<const uint32_t*>(q));
     } else {
