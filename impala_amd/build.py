@@ -38,6 +38,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
            "-Wall", "-Wno-unused-function", "-o", tmp, os.path.join(SRC_DIR, "impala.hip")]
     if verbose:
         print(" ".join(cmd), flush=True)
+    if os.path.exists(tmp):
+        os.remove(tmp)
     subprocess.run(cmd, check=True)
     os.replace(tmp, OUT)
     return OUT

@@ -143,12 +143,17 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
 // (48 channels = 3 column tiles) for both 16-row oc tiles.  The workgroup handles a
 // contiguous run of frames and writes one fp32 partial slab [32][192] (k' order) + bias sums.
 // ---------------------------------------------------------------------------------------
+template <typename T> constexpr int c1_wgrad_groups() { return sizeof(T) == 2 ? 2 : 1; }
+
 template <typename T>
-__global__ __launch_bounds__(256) void conv1_wgrad_s2d(const uint8_t* __restrict__ x,
+__global__ __launch_bounds__(256 * c1_wgrad_groups<T>()) void conv1_wgrad_s2d(const uint8_t* __restrict__ x,
                                                        const T* __restrict__ dy,  // [N][225][32]
                                                        float* __restrict__ slab,
                                                        float* __restrict__ slab_bias, int N,
                                                        int fpw) {
+  // two 4-wave groups per workgroup work on alternating frames of the workgroup's run (two
+  // frames in flight per CU on top of the one-frame register prefetch); their accumulators are
+  // summed in a fixed order at the end.
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int LDI = c1::L<T>::LDI;
@@ -156,9 +161,12 @@ __global__ __launch_bounds__(256) void conv1_wgrad_s2d(const uint8_t* __restrict
   constexpr int LDX = OC1 + VEC;                      // dY tile row (elements)
   constexpr int DYV = c1::NPIX * OC1 / VEC;           // 16-byte vectors per dY frame
   constexpr int NDY = (DYV + 255) / 256;
-  __shared__ __attribute__((aligned(16))) T img[c1::GRID * c1::GRID * LDI];
-  __shared__ __attribute__((aligned(16))) T dyt[c1::NPAD * LDX];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int IMGSZ = c1::GRID * c1::GRID * LDI, DYSZ = c1::NPAD * LDX;
+  constexpr int G = c1_wgrad_groups<T>();
+  __shared__ __attribute__((aligned(16))) T smem[G * (IMGSZ + DYSZ)];
+  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  T* img = smem + grp * (IMGSZ + DYSZ);
+  T* dyt = img + IMGSZ;
   const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
   // zero the padding rows 225..255 of the dY tile once (never overwritten)
   for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX; e += 256) dyt[c1::NPIX * LDX + e] = (T)0.f;
@@ -179,22 +187,27 @@ __global__ __launch_bounds__(256) void conv1_wgrad_s2d(const uint8_t* __restrict
       ndy[i] = e < DYV ? *reinterpret_cast<const V*>(src + e * VEC) : F::zero();
     }
   };
-  if (f0 < f1) fetch(f0);
-  // per-lane pieces of the B-fragment gather (tap = wave)
+  if (f0 + grp < f1) fetch(f0 + grp);
   const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDI;
-  for (int f = f0; f < f1; ++f) {
+  const int n_it = (f1 - f0 + G - 1) / G;
+  for (int it = 0; it < n_it; ++it) {
+    const int f = f0 + G * it + grp;
+    const bool active = f < f1;
     __syncthreads();
-    c1_stash_frame<T>(img, tid, nv);
+    if (active) {
+      c1_stash_frame<T>(img, tid, nv);
 #pragma unroll
-    for (int i = 0; i < NDY; ++i) {
-      const int e = tid + i * 256;
-      if (e < DYV) {
-        const int row = (e * VEC) / OC1, col = (e * VEC) % OC1;
-        *reinterpret_cast<V*>(dyt + row * LDX + col) = ndy[i];
+      for (int i = 0; i < NDY; ++i) {
+        const int e = tid + i * 256;
+        if (e < DYV) {
+          const int row = (e * VEC) / OC1, col = (e * VEC) % OC1;
+          *reinterpret_cast<V*>(dyt + row * LDX + col) = ndy[i];
+        }
       }
     }
     __syncthreads();
-    if (f + 1 < f1) fetch(f + 1);
+    if (f + G < f1) fetch(f + G);
+    if (!active) continue;
     {  // bias: 8 row groups x 32 channels, partial sums kept per thread across frames
       const int oc = tid & 31, rg = tid >> 5;
       float s0 = 0.f, s1 = 0.f;
@@ -244,6 +257,38 @@ __global__ __launch_bounds__(256) void conv1_wgrad_s2d(const uint8_t* __restrict
         for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
     }
   }
+  // fixed-order combine: group 1 -> LDS -> group 0; bias row groups likewise
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  if (G > 1 && grp == 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[((i * 3 + j) * 4 + q) * 256 + tid] = acc[i][j][q];
+    red[24 * 256 + tid] = bias_acc;
+  }
+  __syncthreads();
+  if (G > 1 && grp == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * 3 + j) * 4 + q) * 256 + tid];
+    bias_acc += red[24 * 256 + tid];
+  }
+  __syncthreads();
+  if (grp == 0) red[tid] = bias_acc;
+  __syncthreads();
+  if (grp != 0) return;
+  if (tid < OC1) {
+    float bsum = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) bsum += red[g * 32 + tid];
+    slab_bias[(size_t)blockIdx.x * OC1 + tid] = bsum;
+  }
   const size_t so = (size_t)blockIdx.x * OC1 * K1;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -254,14 +299,4 @@ __global__ __launch_bounds__(256) void conv1_wgrad_s2d(const uint8_t* __restrict
       for (int q = 0; q < 4; ++q)
         slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);
     }
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(dyt);
-  red[tid] = bias_acc;
-  __syncthreads();
-  if (tid < OC1) {
-    float b = 0.f;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) b += red[g * 32 + tid];
-    slab_bias[(size_t)blockIdx.x * OC1 + tid] = b;
-  }
 }

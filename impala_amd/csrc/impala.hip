@@ -150,7 +150,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
   timer_begin(h, K_CONV1_FWD, st);
-  conv1_fwd_s2d<T><<<min(n, h->n_cu * 2), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
+  conv1_fwd_s2d<T><<<min(n, h->n_cu * 4), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
                                                          (T*)h->act1, n);
   timer_end(h, K_CONV1_FWD, st);
   CK_LAUNCH("conv1_fwd");
@@ -301,7 +301,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     CK_LAUNCH("conv2_dgrad");
   }
   timer_begin(h, K_CONV1_WGRAD, st);
-  conv1_wgrad_s2d<T><<<h->c1_wg, 256, 0, st>>>(b->obs, (const T*)h->dact1, h->s_w1, h->s_b1, N,
+  conv1_wgrad_s2d<T><<<h->c1_wg, 256 * c1_wgrad_groups<T>(), 0, st>>>(b->obs, (const T*)h->dact1, h->s_w1, h->s_b1, N,
                                                h->c1_fpw);
   timer_end(h, K_CONV1_WGRAD, st);
   CK_LAUNCH("conv1_wgrad");

@@ -18,6 +18,10 @@ STEP_KERNELS = None
 
 def short(name):
     n = name.split("(")[0]
+    if "conv1_fwd_s2d" in n:
+        return "Conv1Fwd"
+    if "conv1_wgrad_s2d" in n:
+        return "Conv1Wgrad"
     for tag in ("Conv1Fwd", "Conv2Fwd", "Conv3Fwd", "FcFwd", "HeadsFwd", "HeadsDgrad", "FcDgrad",
                 "Conv3Dgrad", "Conv2Dgrad", "HeadsWgrad", "FcWgrad", "Conv3Wgrad", "Conv2Wgrad",
                 "Conv1Wgrad", "ln_fwd", "ln_bwd", "loss_head", "reduce_grads", "adam", "sumsq",
