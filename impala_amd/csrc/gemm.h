@@ -203,15 +203,33 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
           for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
       }
     }
-    if constexpr (NK % 2 == 1) __syncthreads();  // next tile reuses buffer 0 first
+    if constexpr (Op::TILE_EPI) {
+      // workgroup epilogue: fp32 tile [BC][BR+4] in (reused) LDS, then op.tile_epilogue
+      static_assert((size_t)BC * (BR + 4) * sizeof(float) <= sizeof(smem), "epilogue tile");
+      __syncthreads();  // all waves are done reading the staging buffers
+      float* et = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int j = 0; j < TCW; ++j) {
-      const int c = cc0 + (wc * TCW + j) * 16 + (lane & 15);
-      if (c < op.C) {
+      for (int j = 0; j < TCW; ++j)
 #pragma unroll
         for (int i = 0; i < TRW; ++i) {
-          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
+          const int cl = (wc * TCW + j) * 16 + (lane & 15);
+          const int rl0 = (wr * TRW + i) * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(et + cl * (BR + 4) + rl0) = acc[i][j];
+        }
+      __syncthreads();
+      op.tile_epilogue(et, BR + 4, cr0, cc0, tid);
+      __syncthreads();  // the next tile's stash reuses the LDS
+    } else {
+      if constexpr (NK % 2 == 1) __syncthreads();  // next tile reuses buffer 0 first
+#pragma unroll
+      for (int j = 0; j < TCW; ++j) {
+        const int c = cc0 + (wc * TCW + j) * 16 + (lane & 15);
+        if (c < op.C) {
+#pragma unroll
+          for (int i = 0; i < TRW; ++i) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
+          }
         }
       }
     }

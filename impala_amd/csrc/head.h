@@ -1,0 +1,243 @@
+// Fused learner head: actor/critic heads forward, log-softmax / ratio / V-trace / loss
+// (agents/impala/learning.py:144-170), the heads' input gradient through GELU (dz) and the
+// heads' weight-gradient partial -- one workgroup per group of whole trajectories.
+//
+//   phase 1  stage h[F][256] of the group's F frames in LDS; heads = Wh . h + bh (MFMA)
+//   phase 2  wave 0: one lane per (trajectory, t); V-trace as a wavefront shuffle scan
+//            (seg_rev_scan); d loss / d logits, d loss / d value -> dH[F][32] in LDS
+//   phase 3  dz[f][j] = gelu'(z[f][j]) * sum_o' dH[f][o'] Wh[o'][j]        (MFMA, K = 32)
+//   phase 4  dWh[o'][j] += sum_f dH[f][o'] h[f][j]  (MFMA over frames, LDS transpose reads)
+//            -> fp32 partial slab per workgroup (+ bias sums), reduced by reduce_grads
+//
+// F = (64 / S) * T <= 64 frames (S = segment = next pow2 >= T), i.e. one wavefront of lanes.
+#pragma once
+#include "gemm.h"
+#include "kernels.h"
+#include "net.h"
+
+using namespace net;
+
+DEV float fast_exp(float x) { return exp2f(x * 1.4426950408889634f); }
+DEV float fast_log(float x) { return log2f(x) * 0.69314718055994531f; }
+
+struct HeadArgs {
+  // phase 1 inputs
+  const void* h;      // T [N][256]
+  const float* z;     // [N][256] pre-GELU
+  const void* wh;     // T [16][256]
+  const void* wht;    // T [256][32]
+  const float* bh;    // [16]
+  // batch
+  const int64_t* act; const float* rew; const float* disc; const float* mu;
+  int B, T, A, S, TPW;  // TPW = trajectories per workgroup = 64 / S
+  float lam, crho, cpg, ent_coef;
+  // outputs
+  void* dz;             // T [N][256]
+  float* partials;      // [gridDim.x][8] loss partial sums
+  float* slab_h;        // [gridDim.x][16][256]
+  float* slab_bh;       // [gridDim.x][16]
+  float* heads_out;     // optional [N][16] (logits + value), nullptr = skip
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
+  using F = Frag<T>;
+  typedef typename F::vec V;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int LDH = HID + VEC;     // h tile row (elements)
+  constexpr int LDD = HPAD + VEC;    // dH tile row
+  __shared__ __attribute__((aligned(16))) T hs[64 * LDH];
+  __shared__ __attribute__((aligned(16))) T dHs[64 * LDD];
+  __shared__ float lg_s[64][HEADS + 1];
+  __shared__ __attribute__((aligned(16))) float zs[64 * (HID + 4)];  // z tile (phase 3)
+  __shared__ float bred[4][HEADS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T_ = a.T, S = a.S;
+  const int traj0 = blockIdx.x * a.TPW;
+  const int ntraj = min(a.TPW, a.B - traj0);
+  const int nf = ntraj * T_;                       // valid frames of this workgroup
+  const size_t f0 = (size_t)traj0 * T_;            // first global frame
+  const T* hg = reinterpret_cast<const T*>(a.h);
+  // wave 0's per-(trajectory, t) batch values, loaded first so their latency overlaps phase 1
+  const int A = a.A, L = T_ - 1;
+  const int tl = lane / S, t = lane % S;
+  const bool valid = wave == 0 && tl < ntraj && t < T_;
+  const bool inL = valid && t < L;
+  const int fl = valid ? tl * T_ + t : 0;
+  float mu[MAX_A], r = 0.f, g = 0.f;
+  int act = 0;
+  if (wave == 0) {
+    const size_t n = f0 + fl;
+    const float* mrow = a.mu + n * A;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) mu[j] = mrow[j < A ? j : A - 1];
+    act = (int)a.act[n];
+    r = a.rew[n];
+    g = a.disc[n];
+  }
+  // ---- phase 1: stage h, zero dH, heads forward ----
+  for (int e = tid; e < 64 * (HID / VEC); e += 256) {
+    const int f = e / (HID / VEC), c = (e % (HID / VEC)) * VEC;
+    V v = f < nf ? *reinterpret_cast<const V*>(hg + (f0 + f) * HID + c) : F::zero();
+    *reinterpret_cast<V*>(hs + f * LDH + c) = v;
+  }
+  for (int e = tid; e < 64 * LDD; e += 256) dHs[e] = (T)0.f;
+  __syncthreads();
+  {
+    const int kl = F::KPL * (lane >> 4);
+    const T* wh = reinterpret_cast<const T*>(a.wh);
+    const int f = wave * 16 + (lane & 15);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int k = 0; k < HID; k += F::KSTEP) {
+      const V wa = F::load(wh + (lane & 15) * HID + k + kl);
+      const V hb = *reinterpret_cast<const V*>(hs + f * LDH + k + kl);
+      acc = F::mma(wa, hb, acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = 4 * (lane >> 4) + q;
+      lg_s[f][o] = acc[q] + a.bh[o];
+    }
+  }
+  __syncthreads();
+  if (a.heads_out) {
+    for (int e = tid; e < nf * HEADS; e += 256)
+      a.heads_out[(f0 + e / HEADS) * HEADS + e % HEADS] = lg_s[e / HEADS][e % HEADS];
+  }
+  // ---- phase 2: loss head on wave 0 (one lane per (trajectory, t)); waves 1..3 stage z ----
+  if (wave != 0) {
+    for (int e = tid - 64; e < 64 * (HID / 4); e += 192) {
+      const int f = e / (HID / 4), c = (e % (HID / 4)) * 4;
+      const f32x4 zv = f < nf ? *reinterpret_cast<const f32x4*>(a.z + (f0 + f) * HID + c)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(zs + f * (HID + 4) + c) = zv;
+    }
+  } else {
+    const int f = fl;
+    float lg[MAX_A], p[MAX_A], logp[MAX_A];
+    float H = 0.f, kl = 0.f, logpa = 0.f, rho = 0.f;
+    float v = lg_s[f][VCOL];
+    float m = -INFINITY, mm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      lg[j] = j < A ? lg_s[f][j] : -INFINITY;
+      if (j >= A) mu[j] = -INFINITY;
+      m = fmaxf(m, lg[j]);
+      mm = fmaxf(mm, mu[j]);
+    }
+    float s = 0.f, sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      p[j] = j < A ? fast_exp(lg[j] - m) : 0.f;
+      s += p[j];
+      sm += j < A ? fast_exp(mu[j] - mm) : 0.f;
+    }
+    const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm), inv_s = 1.f / s;
+    float logmua = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      if (j < A) {
+        logp[j] = lg[j] - lse;
+        p[j] *= inv_s;
+        const float lmu = mu[j] - lse_mu;
+        H -= p[j] * logp[j];
+        kl += p[j] * (logp[j] - lmu);
+        if (j == act) { logpa = logp[j]; logmua = lmu; }
+      } else {
+        logp[j] = 0.f;
+      }
+    }
+    rho = fast_exp(logpa - logmua);
+    if (!valid) { H = 0.f; kl = 0.f; rho = 0.f; v = 0.f; r = 0.f; g = 0.f; }
+    const float v_n = __shfl_down(v, 1, 64);
+    const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
+    const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
+    const float e = seg_rev_scan(aa, td, t, L, S);
+    const float tgt = e + v;
+    const float err = tgt - v;
+    const float tgt_n = __shfl_down(tgt, 1, 64);
+    const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
+    const float qq = r + g * boot;
+    const float adv = fminf(a.cpg, rho) * (qq - v);
+    if (valid) {
+      const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T_);
+      const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;
+#pragma unroll
+      for (int j = 0; j < MAX_A; ++j)
+        if (j < A) dHs[f * LDD + j] = (T)(ke * p[j] * (logp[j] + H) - kp * ((j == act ? 1.f : 0.f) - p[j]));
+      dHs[f * LDD + VCOL] = (T)(inL ? -2.f * c_pg * err : 0.f);
+    }
+    float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
+    s0 = wave_sum(s0); s1 = wave_sum(s1);
+    const float s2 = wave_sum(H), s3 = wave_sum(kl), s4 = wave_sum(rho);
+    if (lane == 0) {
+      float* pp = a.partials + blockIdx.x * 8;
+      pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
+    }
+  }
+  __syncthreads();
+  // ---- phase 3: dz = gelu'(z) * (dH . Wh)   rows j (256: wave w -> 4 row tiles), cols f ----
+  {
+    const int kl = F::KPL * (lane >> 4);
+    const T* wht = reinterpret_cast<const T*>(a.wht);
+    T* dz = reinterpret_cast<T*>(a.dz);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j0 = (wave * 4 + i) * 16;
+      V wa[HPAD / F::KSTEP];
+#pragma unroll
+      for (int ks = 0; ks < HPAD / F::KSTEP; ++ks)
+        wa[ks] = F::load(wht + (j0 + (lane & 15)) * HPAD + ks * F::KSTEP + kl);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int f = ct * 16 + (lane & 15);
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < HPAD / F::KSTEP; ++ks)
+          acc = F::mma(wa[ks], *reinterpret_cast<const V*>(dHs + f * LDD + ks * F::KSTEP + kl), acc);
+        if (f < nf) {
+          const int j = j0 + 4 * (lane >> 4);
+          const f32x4 zz = *reinterpret_cast<const f32x4*>(zs + f * (HID + 4) + j);
+          float o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = acc[q] * gelu_grad(zz[q]);
+          store4(dz + (f0 + f) * HID + j, o);
+        }
+      }
+    }
+  }
+  // ---- phase 4: dWh partial = dH^T . h over this group's frames (k = frame) ----
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 64; kk += F::KSTEP) {
+      const V av = lds_frag_k(dHs + kk * LDD, LDD, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const V bv = lds_frag_k(hs + kk * LDH + (wave * 4 + j) * 16, LDH, lane);
+        acc[j] = F::mma(av, bv, acc[j]);
+      }
+    }
+    float* sl = a.slab_h + (size_t)blockIdx.x * HEADS * HID;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = (wave * 4 + j) * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sl[(4 * (lane >> 4) + q) * HID + c] = acc[j][q];
+    }
+    {  // bias = sum over frames of dH: 16 frame groups x 16 heads, fixed-order tree
+      const int o = tid & 15, fg = tid >> 4;
+      float b = 0.f;
+      for (int f = fg; f < nf; f += 16) b += (float)dHs[f * LDD + o];
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if ((lane >> 4) == 0) bred[wave][o] = b;
+      __syncthreads();
+      if (tid < HEADS)
+        a.slab_bh[(size_t)blockIdx.x * HEADS + tid] = bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+    }
+  }
+}

@@ -16,6 +16,7 @@
 #include <string>
 
 #include "../../include/impala_hip.h"
+#include "head.h"
 #include "kernels.h"
 #include "ops.h"
 
@@ -81,7 +82,7 @@ enum KernelId {
   K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
-    "conv1_fwd", "conv2_fwd", "conv3_fwd", "ln_fwd", "fc_fwd", "heads_fwd", "loss_head",
+    "conv1_fwd", "conv2_fwd", "conv3_fwd", "ln_fwd", "fc_fwd", "heads_fwd", "head_step",
     "heads_dgrad", "fc_dgrad", "ln_bwd", "conv3_dgrad", "conv2_dgrad", "heads_wgrad",
     "fc_wgrad", "conv3_wgrad", "conv2_wgrad", "conv1_wgrad", "reduce_grads", "sumsq", "adam"};
 
@@ -143,7 +144,8 @@ inline void timer_end(impala_learner* h, int kid, hipStream_t st) {
 namespace {
 
 template <typename T>
-int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st) {
+int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
+                   bool with_heads) {
   using namespace net;
   constexpr int TBK = sizeof(T) == 4 ? 32 : 64;  // K chunk of the LDS-staged tile GEMM
   const T* sw = reinterpret_cast<const T*>(h->shadow);
@@ -162,25 +164,23 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st)
     CK_LAUNCH("conv2_fwd");
   }
   {
-    Conv3Fwd<T> op{n * P3, sw + sh.w3, vv + Vecs::b3, (const T*)h->act2, (T*)h->act3};
+    Conv3LnFwd<T> op{};
+    op.C = n * P3; op.w = sw + sh.w3; op.b = vv + Vecs::b3; op.x = (const T*)h->act2;
+    op.out = (T*)h->act3; op.gam = vv + Vecs::lng; op.bet = vv + Vecs::lnb; op.y = (T*)h->y;
+    op.stats = h->lnstat;
     timer_begin(h, K_CONV3_FWD, st);
     gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_FWD, st);
     CK_LAUNCH("conv3_fwd");
   }
-  timer_begin(h, K_LN_FWD, st);
-  ln_fwd_kernel<T><<<cdiv(n, 4), 256, 0, st>>>((const T*)h->act3, vv + Vecs::lng, vv + Vecs::lnb,
-                                               (T*)h->y, h->lnstat, n);
-  timer_end(h, K_LN_FWD, st);
-  CK_LAUNCH("ln_fwd");
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
     timer_begin(h, K_FC_FWD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv(n, 64)) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
+    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)cdiv(n, 64) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
     timer_end(h, K_FC_FWD, st);
     CK_LAUNCH("fc_fwd");
   }
-  {
+  if (with_heads) {  // inference; in training the fused head kernel computes the heads
     HeadsFwd<T> op{n, sw + sh.wh, vv + Vecs::bh, (const T*)h->h, h->heads};
     timer_begin(h, K_HEADS_FWD, st);
     gemm_rc<T, 1, 1><<<dim3(cdiv(n, 64), 1), 256, 0, st>>>(op);
@@ -197,23 +197,6 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   const int N = h->N, B = h->cfg.batch_size, Tl = h->cfg.rollout_length;
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
-  // ---- loss head: log-softmax, ratio, V-trace, losses, d/dlogits, d/dvalue ----
-  {
-    LossArgs la{};
-    la.logits = h->heads; la.lg_ld = HEADS;
-    la.values = h->heads + VCOL; la.v_ld = HEADS;
-    la.act = b->actions; la.rew = b->rewards; la.disc = b->discounts;
-    la.mu = b->behaviour_logits;
-    la.B = B; la.T = Tl; la.A = h->A; la.S = h->S_seg;
-    la.lam = h->cfg.vtrace_lambda; la.crho = h->cfg.clip_rho_threshold;
-    la.cpg = h->cfg.clip_pg_rho_threshold; la.ent_coef = h->cfg.entropy_coeff;
-    la.partials = h->loss_part;
-    T* dH = (T*)h->dH;
-    timer_begin(h, K_LOSS, st);
-    loss_head_kernel<T><<<h->n_loss_wg, 256, 0, st>>>(la, dH, HPAD, dH + VCOL, HPAD, VCOL);
-    timer_end(h, K_LOSS, st);
-    CK_LAUNCH("loss_head");
-  }
   // ---- dgrad chain on `st`; each weight-gradient branch forks onto the side stream as soon
   // as its inputs exist and joins before the slab reduction ----
   constexpr int WBM = sizeof(T) == 4 ? 32 : 64;  // m-chunk of gemm_wg (LDS budget of f32)
@@ -224,22 +207,21 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     CK(hipStreamWaitEvent(ss, h->ev_fork[i], 0));
     return 0;
   };
-  if (int r = fork(0)) return r;  // dH, h ready
+  // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
   {
-    HeadsWgrad<T> op{};
-    op.M = N; op.x = (const T*)h->dH; op.h = (const T*)h->h;
-    timer_begin(h, K_HEADS_WGRAD, ss);
-    gemm_wg<T, 16, 256, 1, 4, WBM, 1><<<dim3(1, 1, h->sph.S), 256, 0, ss>>>(op, h->s_h, h->s_bh,
-                                                                         h->sph.mps);
-    timer_end(h, K_HEADS_WGRAD, ss);
-    CK_LAUNCH("heads_wgrad");
-  }
-  {
-    HeadsDgrad<T> op{N, sw + sh.wht, (const T*)h->dH, h->z, (T*)h->dz};
-    timer_begin(h, K_HEADS_DGRAD, st);
-    gemm_rc<T, 4, 1><<<dim3(cdiv(N, 64), HID / 64), 256, 0, st>>>(op);
-    timer_end(h, K_HEADS_DGRAD, st);
-    CK_LAUNCH("heads_dgrad");
+    HeadArgs ha{};
+    ha.h = h->h; ha.z = h->z; ha.wh = sw + sh.wh; ha.wht = sw + sh.wht;
+    ha.bh = h->vecs + Vecs::bh;
+    ha.act = b->actions; ha.rew = b->rewards; ha.disc = b->discounts; ha.mu = b->behaviour_logits;
+    ha.B = B; ha.T = Tl; ha.A = h->A; ha.S = h->S_seg; ha.TPW = 64 / h->S_seg;
+    ha.lam = h->cfg.vtrace_lambda; ha.crho = h->cfg.clip_rho_threshold;
+    ha.cpg = h->cfg.clip_pg_rho_threshold; ha.ent_coef = h->cfg.entropy_coeff;
+    ha.dz = h->dz; ha.partials = h->loss_part; ha.slab_h = h->s_h; ha.slab_bh = h->s_bh;
+    ha.heads_out = h->heads;
+    timer_begin(h, K_LOSS, st);
+    head_step_kernel<T><<<h->n_loss_wg, 256, 0, st>>>(ha);
+    timer_end(h, K_LOSS, st);
+    CK_LAUNCH("head_step");
   }
   if (int r = fork(1)) return r;  // dz ready
   {
@@ -417,13 +399,13 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const int N = h->N;
   const size_t es = h->bf16 ? 2 : 4;
   h->S_seg = next_pow2(cfg->rollout_length);
-  h->n_loss_wg = cdiv(cfg->batch_size, 4 * (64 / h->S_seg));
+  h->n_loss_wg = cdiv(cfg->batch_size, 64 / h->S_seg);  // fused head: 64/S trajectories per WG
   h->n_ln_wg = cdiv(N, 4 * h->ln_fpw);
 
   // upper bound on the reduce workgroups (each segment: count/4 float4 columns, >= 16 per WG)
   h->n_red_wg = 11 + (OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT + HID * FLAT +
                       HID + HEADS * HID + HEADS) / 4 / 16;
-  h->sph = plan_split(N, 1, 16);
+  h->sph.S = h->n_loss_wg;  // heads weight-gradient partials: one slab per head workgroup
   h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), 96);
   h->sp3 = plan_split((long)N * P3, K3 / 192, 192);
   h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
@@ -602,7 +584,8 @@ int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, 
   if (((uintptr_t)obs & 15) != 0) return fail(IMPALA_E_INVALID, "obs must be 16-byte aligned");
   CK(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  int r = h->bf16 ? launch_forward<__bf16>(h, obs, n, st) : launch_forward<float>(h, obs, n, st);
+  int r = h->bf16 ? launch_forward<__bf16>(h, obs, n, st, true)
+                  : launch_forward<float>(h, obs, n, st, true);
   if (r) return r;
   split_heads_kernel<<<cdiv((long)n * net::HEADS, 256), 256, 0, st>>>(h->heads, n, h->A, logits,
                                                                        values);
@@ -615,8 +598,8 @@ int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream)
   if (int r = check_batch(b)) return r;
   CK(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st)
-                  : launch_forward<float>(h, b->obs, h->N, st);
+  int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st, false)
+                  : launch_forward<float>(h, b->obs, h->N, st, false);
   if (r) return r;
   return h->bf16 ? launch_backward<__bf16>(h, b, st) : launch_backward<float>(h, b, st);
 }

@@ -97,27 +97,40 @@ __global__ __launch_bounds__(256) void loss_head_kernel(const LossArgs a, TO* __
   float H = 0.f, kl = 0.f, logpa = 0.f, rho = 0.f, v = 0.f, r = 0.f, g = 0.f;
   int act = 0;
   if (valid) {
-    float m = -INFINITY;
+    // all loads are issued unconditionally (clamped index) and masked afterwards: a
+    // "load or constant" select per element would make the compiler wait on each load
+    float m = -INFINITY, mu[MAX_A];
+    const float* lrow = a.logits + n * a.lg_ld;
+    const float* mrow = a.mu + n * A;
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) {
-      lg[j] = j < A ? a.logits[n * a.lg_ld + j] : -INFINITY;
+      const int jj = j < A ? j : A - 1;
+      lg[j] = lrow[jj];
+      mu[j] = mrow[jj];
+    }
+    act = (int)a.act[n];
+    v = a.values[n * a.v_ld];
+    r = a.rew[n];
+    g = a.disc[n];
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      if (j >= A) lg[j] = -INFINITY;
       m = fmaxf(m, lg[j]);
     }
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) s += j < A ? expf(lg[j] - m) : 0.f;
     const float lse = m + logf(s);
-    float mm = -INFINITY, mu[MAX_A];
+    float mm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) {
-      mu[j] = j < A ? a.mu[n * A + j] : -INFINITY;
+      if (j >= A) mu[j] = -INFINITY;
       mm = fmaxf(mm, mu[j]);
     }
     float sm = 0.f;
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) sm += j < A ? expf(mu[j] - mm) : 0.f;
     const float lse_mu = mm + logf(sm);
-    act = (int)a.act[n];
     float logmua = 0.f;
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) {
@@ -133,9 +146,6 @@ __global__ __launch_bounds__(256) void loss_head_kernel(const LossArgs a, TO* __
       }
     }
     rho = expf(logpa - logmua);
-    v = a.values[n * a.v_ld];
-    r = a.rew[n];
-    g = a.disc[n];
   }
   // ---- V-trace over the first T-1 steps of each trajectory segment ----
   const float v_n = __shfl_down(v, 1, 64);  // values[:, 1:]

@@ -13,6 +13,7 @@ using namespace net;
 // in bf16).  Epilogue: *1/255 + bias, ReLU -> act1[n][oh][ow][oc].
 template <typename T> struct Conv1Fwd {
   static constexpr bool A_KMAJOR = false;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = K1;
   int C;
   const T* w;
@@ -46,6 +47,7 @@ template <typename T> struct Conv1Fwd {
 // conv2: rows oc (64), cols (n, oh, ow) in N*36, k = (kh*4+kw)*32 + ci over act1.
 template <typename T> struct Conv2Fwd {
   static constexpr bool A_KMAJOR = false;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = K2;
   int C;
   const T* w;
@@ -74,6 +76,7 @@ template <typename T> struct Conv2Fwd {
 // act3 row n is the flattened feature vector in (p*64 + c) order.
 template <typename T> struct Conv3Fwd {
   static constexpr bool A_KMAJOR = false;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = K3;
   int C;
   const T* w;
@@ -102,6 +105,7 @@ template <typename T> struct Conv3Fwd {
 // rows o (256), cols frame n, k = p*64 + c over the LayerNorm output y.
 template <typename T> struct FcFwd {
   static constexpr bool A_KMAJOR = false;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = FLAT;
   int C;
   const T* w;
@@ -128,6 +132,7 @@ template <typename T> struct FcFwd {
 // actor ‖ critic heads fused into one 16-row GEMM (models/models.py:69-70, 76).
 template <typename T> struct HeadsFwd {
   static constexpr bool A_KMAJOR = false;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = HID;
   int C;
   const T* w;
@@ -146,10 +151,108 @@ template <typename T> struct HeadsFwd {
   }
 };
 
+// conv3 + ReLU + LayerNorm(1024) fused (models/common.py:117-119, models/models.py:66):
+// a 64(oc) x 64(pixel) tile holds 4 whole frames; wave w normalises frame w of the tile.
+// Writes act3 (post-ReLU, kept for the mask and the LN backward), y = LN(act3), mean/rstd.
+template <typename T> struct Conv3LnFwd : Conv3Fwd<T> {
+  static constexpr bool TILE_EPI = true;
+  const float* gam;  // permuted to p*64 + c
+  const float* bet;
+  T* y;
+  float* stats;
+  DEV void tile_epilogue(const float* et, int ldt, int, int cc0, int tid) const {
+    const int lane = tid & 63, wave = tid >> 6;
+    const int frame = cc0 / P3 + wave;
+    if ((frame + 1) * P3 > this->C) return;
+    // lane owns features j = 16*lane .. 16*lane+15  (pixel p = lane/4, channels 16*(lane%4)..)
+    const int p = lane >> 2, c0 = (lane & 3) * 16;
+    const float* src = et + (wave * P3 + p) * ldt + c0;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = fmaxf(src[i] + this->b[c0 + i], 0.f);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sum += v[i];
+    const float mean = wave_sum(sum) * (1.f / FLAT);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) q += (v[i] - mean) * (v[i] - mean);
+    const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / FLAT) + LN_EPS);
+    const size_t o = (size_t)frame * FLAT + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      float yy[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        yy[k] = (v[i + k] - mean) * rstd * gam[lane * 16 + i + k] + bet[lane * 16 + i + k];
+      store4(this->out + o + i, v + i);
+      store4(y + o + i, yy);
+    }
+    if (lane == 0) {
+      stats[2 * frame] = mean;
+      stats[2 * frame + 1] = rstd;
+    }
+  }
+};
+
+// projection Linear + GELU + actor/critic heads fused: a 256(o) x 32(frame) tile holds whole
+// h rows; the heads (16 x 256) are applied from LDS in the epilogue (wave 0..1: 16 frames each).
+template <typename T> struct FcHeadsFwd : FcFwd<T> {
+  static constexpr bool TILE_EPI = true;
+  const T* wh;       // [16][256]
+  const float* bh;   // [16]
+  float* heads;      // [n][16]
+  DEV void tile_epilogue(const float* et, int ldt, int, int cc0, int tid) const {
+    // 1) z = acc + b, h = gelu(z): write z, h to HBM, h (fp32) back into the LDS tile
+    float* etw = const_cast<float*>(et);
+    for (int e = tid; e < 32 * (HID / 4); e += 256) {
+      const int f = e / (HID / 4), r = (e % (HID / 4)) * 4;
+      const int c = cc0 + f;
+      float zz[4], hh[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        zz[k] = et[f * ldt + r + k] + this->b[r + k];
+        hh[k] = gelu_f(zz[k]);
+      }
+      if (c < this->C) {
+        store4(this->z + (size_t)c * HID + r, zz);
+        store4(this->h + (size_t)c * HID + r, hh);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) etw[f * ldt + r + k] = (float)(T)hh[k];  // as stored (T)
+    }
+    __syncthreads();
+    // 2) heads: out[f][o'] = sum_j wh[o'][j] h[f][j] + bh[o'], one 16x16 tile per wave 0..1
+    const int lane = tid & 63, wave = tid >> 6;
+    if (wave < 2) {
+      using F = Frag<T>;
+      const int kl = F::KPL * (lane >> 4);
+      const int f = wave * 16 + (lane & 15);
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int k = 0; k < HID; k += F::KSTEP) {
+        const typename F::vec a = F::load(wh + (lane & 15) * HID + k + kl);
+        typename F::vec bv;
+#pragma unroll
+        for (int q = 0; q < F::KPL; ++q) bv[q] = (T)et[f * ldt + k + kl + q];
+        acc = F::mma(a, bv, acc);
+      }
+      const int c = cc0 + f;
+      if (c < this->C) {
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = acc[q] + bh[4 * (lane >> 4) + q];
+        store4(heads + (size_t)c * HEADS + 4 * (lane >> 4), o);
+      }
+    }
+  }
+};
+
 // ------------------------------- backward (dgrad) ---------------------------------------
 // dh = dH . Wh  then GELU backward:  dz[n][j] = dh[n][j] * gelu'(z[n][j]).  K = 32 (padded).
 template <typename T> struct HeadsDgrad {
   static constexpr bool A_KMAJOR = false;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = HPAD;
   int C;
   const T* wt;  // [256][32]
@@ -173,6 +276,7 @@ template <typename T> struct HeadsDgrad {
 // A[j][o] = wfc[o][j]: read k-major from the forward weight (no transposed copy).
 template <typename T> struct FcDgrad {
   static constexpr bool A_KMAJOR = true;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = HID;
   int C;
   const T* w;   // wfc [256][1024]
@@ -191,6 +295,7 @@ template <typename T> struct FcDgrad {
 // Epilogue applies conv2's ReLU mask (act2 > 0).
 template <typename T> struct Conv3Dgrad {
   static constexpr bool A_KMAJOR = true;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = K3;
   int C;
   const T* w;     // w3 [64 oc][576 = tap*64 + ci]; A[ci][tap*64 + oc] read k-major
@@ -230,6 +335,7 @@ template <typename T> struct Conv3Dgrad {
 // Epilogue applies conv1's ReLU mask (act1 > 0); ih/iw == 15 are outside the 15x15 map.
 template <typename T> struct Conv2Dgrad {
   static constexpr bool A_KMAJOR = true;
+  static constexpr bool TILE_EPI = false;
   static constexpr int K = 4 * OC2;
   int C;        // 4 * NC
   int NC;       // columns per class (multiple of the tile width)
