@@ -39,6 +39,11 @@ struct HeadArgs {
   float* heads_out;     // optional [N][16] (logits + value), nullptr = skip
 };
 
+constexpr int HEAD_SPLIT = 4;              // workgroups per trajectory group (hidden-column slices)
+constexpr int HEAD_JC = HID / HEAD_SPLIT;  // 64 hidden columns per workgroup in phases 3/4
+
+// grid (groups, HEAD_SPLIT): all HEAD_SPLIT workgroups of a group redo phases 1-2 (cheap: h is an
+// L2 hit and the loss is one wavefront), then each takes a 64-column slice of dz / dWh.
 template <typename T>
 __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   using F = Frag<T>;
@@ -49,7 +54,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   __shared__ __attribute__((aligned(16))) T hs[64 * LDH];
   __shared__ __attribute__((aligned(16))) T dHs[64 * LDD];
   __shared__ float lg_s[64][HEADS + 1];
-  __shared__ __attribute__((aligned(16))) float zs[64 * (HID + 4)];  // z tile (phase 3)
+  __shared__ __attribute__((aligned(16))) float zs[64 * (HEAD_JC + 4)];  // z slice (phase 3)
   __shared__ float bred[4][HEADS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T_ = a.T, S = a.S;
@@ -58,6 +63,8 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   const int nf = ntraj * T_;                       // valid frames of this workgroup
   const size_t f0 = (size_t)traj0 * T_;            // first global frame
   const T* hg = reinterpret_cast<const T*>(a.h);
+  const int jw = blockIdx.y * HEAD_JC;            // this workgroup's hidden-column slice
+  const bool lead = blockIdx.y == 0;              // writes the per-group outputs
   // wave 0's per-(trajectory, t) batch values, loaded first so their latency overlaps phase 1
   const int A = a.A, L = T_ - 1;
   const int tl = lane / S, t = lane % S;
@@ -101,17 +108,17 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     }
   }
   __syncthreads();
-  if (a.heads_out) {
+  if (a.heads_out && lead) {
     for (int e = tid; e < nf * HEADS; e += 256)
       a.heads_out[(f0 + e / HEADS) * HEADS + e % HEADS] = lg_s[e / HEADS][e % HEADS];
   }
   // ---- phase 2: loss head on wave 0 (one lane per (trajectory, t)); waves 1..3 stage z ----
   if (wave != 0) {
-    for (int e = tid - 64; e < 64 * (HID / 4); e += 192) {
-      const int f = e / (HID / 4), c = (e % (HID / 4)) * 4;
-      const f32x4 zv = f < nf ? *reinterpret_cast<const f32x4*>(a.z + (f0 + f) * HID + c)
+    for (int e = tid - 64; e < 64 * (HEAD_JC / 4); e += 192) {
+      const int f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
+      const f32x4 zv = f < nf ? *reinterpret_cast<const f32x4*>(a.z + (f0 + f) * HID + jw + c)
                               : f32x4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(zs + f * (HID + 4) + c) = zv;
+      *reinterpret_cast<f32x4*>(zs + f * (HEAD_JC + 4) + c) = zv;
     }
   } else {
     const int f = fl;
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
     s0 = wave_sum(s0); s1 = wave_sum(s1);
     const float s2 = wave_sum(H), s3 = wave_sum(kl), s4 = wave_sum(rho);
-    if (lane == 0) {
+    if (lane == 0 && lead) {
       float* pp = a.partials + blockIdx.x * 8;
       pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
     }
@@ -182,9 +189,8 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     const int kl = F::KPL * (lane >> 4);
     const T* wht = reinterpret_cast<const T*>(a.wht);
     T* dz = reinterpret_cast<T*>(a.dz);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j0 = (wave * 4 + i) * 16;
+    {
+      const int j0 = jw + wave * 16;
       V wa[HPAD / F::KSTEP];
 #pragma unroll
       for (int ks = 0; ks < HPAD / F::KSTEP; ++ks)
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
           acc = F::mma(wa[ks], *reinterpret_cast<const V*>(dHs + f * LDD + ks * F::KSTEP + kl), acc);
         if (f < nf) {
           const int j = j0 + 4 * (lane >> 4);
-          const f32x4 zz = *reinterpret_cast<const f32x4*>(zs + f * (HID + 4) + j);
+          const f32x4 zz = *reinterpret_cast<const f32x4*>(zs + f * (HEAD_JC + 4) + j - jw);
           float o[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) o[q] = acc[q] * gelu_grad(zz[q]);
@@ -209,25 +215,15 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   }
   // ---- phase 4: dWh partial = dH^T . h over this group's frames (k = frame) ----
   {
-    f32x4 acc[4];
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c0 = jw + wave * 16;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < 64; kk += F::KSTEP) {
-      const V av = lds_frag_k(dHs + kk * LDD, LDD, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const V bv = lds_frag_k(hs + kk * LDH + (wave * 4 + j) * 16, LDH, lane);
-        acc[j] = F::mma(av, bv, acc[j]);
-      }
-    }
+    for (int kk = 0; kk < 64; kk += F::KSTEP)
+      acc = F::mma(lds_frag_k(dHs + kk * LDD, LDD, lane), lds_frag_k(hs + kk * LDH + c0, LDH, lane), acc);
     float* sl = a.slab_h + (size_t)blockIdx.x * HEADS * HID;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = (wave * 4 + j) * 16 + (lane & 15);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sl[(4 * (lane >> 4) + q) * HID + c] = acc[j][q];
-    }
+    for (int q = 0; q < 4; ++q) sl[(4 * (lane >> 4) + q) * HID + c0 + (lane & 15)] = acc[q];
+    if (lead) {
     {  // bias = sum over frames of dH: 16 frame groups x 16 heads, fixed-order tree
       const int o = tid & 15, fg = tid >> 4;
       float b = 0.f;
@@ -238,6 +234,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
       __syncthreads();
       if (tid < HEADS)
         a.slab_bh[(size_t)blockIdx.x * HEADS + tid] = bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+    }
     }
   }
 }

@@ -219,7 +219,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     ha.dz = h->dz; ha.partials = h->loss_part; ha.slab_h = h->s_h; ha.slab_bh = h->s_bh;
     ha.heads_out = h->heads;
     timer_begin(h, K_LOSS, st);
-    head_step_kernel<T><<<h->n_loss_wg, 256, 0, st>>>(ha);
+    head_step_kernel<T><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
     timer_end(h, K_LOSS, st);
     CK_LAUNCH("head_step");
   }

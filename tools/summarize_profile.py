@@ -22,6 +22,12 @@ def short(name):
         return "Conv1Fwd"
     if "conv1_wgrad_s2d" in n:
         return "Conv1Wgrad"
+    if "head_step" in n:
+        return "head_step"
+    if "gemm_tile" in n or "gemm_wg" in n or "gemm_rc" in n:
+        for tag in ("Conv3LnFwd", "FcHeadsFwd"):
+            if tag in n:
+                return tag
     for tag in ("Conv1Fwd", "Conv2Fwd", "Conv3Fwd", "FcFwd", "HeadsFwd", "HeadsDgrad", "FcDgrad",
                 "Conv3Dgrad", "Conv2Dgrad", "HeadsWgrad", "FcWgrad", "Conv3Wgrad", "Conv2Wgrad",
                 "Conv1Wgrad", "ln_fwd", "ln_bwd", "loss_head", "reduce_grads", "adam", "sumsq",
