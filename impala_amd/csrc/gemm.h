@@ -100,7 +100,6 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   constexpr int LD = BK + VEC;            // padded row (elements)
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NA = BR * KV / 256, NB = BC * KV / 256;
-  constexpr int RPP = 256 / KV;           // tile rows covered per staging pass
   constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
   constexpr int LDA = AK ? BR + VEC : LD; // A tile row length (elements)
   constexpr int ASZ = AK ? BK * LDA : BR * LD;
@@ -111,7 +110,9 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   __shared__ __attribute__((aligned(16))) T smem[2 * (ASZ + BC * LD)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
-  const int kv = tid % KV, rl = tid / KV;
+  // staging element e = tid + i*256 of a chunk -> (tile row e / KV, 16-byte vector e % KV)
+  auto srow = [&](int i) { return (tid + i * 256) / KV; };
+  auto skv = [&](int i) { return (tid + i * 256) % KV; };
   const int n_tiles = n_rtiles * ((op.C + BC - 1) / BC);
   const int ft = blockIdx.x;  // first tile of this workgroup
   if (ft >= n_tiles) return;
@@ -125,10 +126,10 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
     fcw = min(fc0, op.C - 1);
     if constexpr (!AK) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) arow[i] = op.a_row(fr0 + rl + i * RPP, fcw);
+      for (int i = 0; i < NA; ++i) arow[i] = op.a_row(fr0 + srow(i), fcw);
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(fc0 + rl + i * RPP, op.C - 1));
+    for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(fc0 + srow(i), op.C - 1));
   };
   V ra[NA], rb[NB];
   auto fetch = [&](int k0) {
@@ -140,10 +141,10 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) ra[i] = F::load(arow[i] + k0 + kv * VEC);
+      for (int i = 0; i < NA; ++i) ra[i] = F::load(arow[i] + k0 + skv(i) * VEC);
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = op.load_b(bctx[i], k0 + kv * VEC);
+    for (int i = 0; i < NB; ++i) rb[i] = op.load_b(bctx[i], k0 + skv(i) * VEC);
   };
   auto stash = [&](int buf) {
     T* As = smem + buf * (ASZ + BC * LD);
@@ -156,10 +157,10 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + (rl + i * RPP) * LD + kv * VEC) = ra[i];
+      for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + srow(i) * LD + skv(i) * VEC) = ra[i];
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + (rl + i * RPP) * LD + kv * VEC) = rb[i];
+    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + srow(i) * LD + skv(i) * VEC) = rb[i];
   };
   const int kl = F::KPL * (lane >> 4);
   set_ctx(ft);

@@ -147,7 +147,9 @@ template <typename T>
 int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
                    bool with_heads) {
   using namespace net;
-  constexpr int TBK = sizeof(T) == 4 ? 32 : 64;  // K chunk of the LDS-staged tile GEMM
+  // K chunk of the LDS-staged tile GEMM: long chunks (few, each a full memory round trip) for
+  // bf16; fp32 (parity mode) keeps 32 for its LDS budget
+#define BK(kb) (sizeof(T) == 4 ? 32 : (kb))
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
@@ -159,7 +161,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   {
     Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
     timer_begin(h, K_CONV2_FWD, st);
-    gemm_tile<T, 64, 128, TBK, 1, 4><<<persist_grid(h, (long)(cdiv((long)n * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
+    gemm_tile<T, 64, 128, BK(64), 1, 4><<<persist_grid(h, (long)(cdiv((long)n * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV2_FWD, st);
     CK_LAUNCH("conv2_fwd");
   }
@@ -169,14 +171,14 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     op.out = (T*)h->act3; op.gam = vv + Vecs::lng; op.bet = vv + Vecs::lnb; op.y = (T*)h->y;
     op.stats = h->lnstat;
     timer_begin(h, K_CONV3_FWD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
+    gemm_tile<T, 64, 64, BK(64), 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_FWD, st);
     CK_LAUNCH("conv3_fwd");
   }
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
     timer_begin(h, K_FC_FWD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)cdiv(n, 64) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
+    gemm_tile<T, 64, 64, BK(256), 2, 2><<<persist_grid(h, (long)cdiv(n, 64) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
     timer_end(h, K_FC_FWD, st);
     CK_LAUNCH("fc_fwd");
   }
@@ -193,7 +195,6 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
 template <typename T>
 int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   using namespace net;
-  constexpr int TBK = sizeof(T) == 4 ? 32 : 64;
   const int N = h->N, B = h->cfg.batch_size, Tl = h->cfg.rollout_length;
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
@@ -236,7 +237,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   {
     FcDgrad<T> op{N, sw + sh.wfc, (const T*)h->dz, h->dy};
     timer_begin(h, K_FC_DGRAD, st);
-    gemm_tile<T, 64, 64, TBK, 2, 2><<<persist_grid(h, (long)(cdiv(N, 64)) * (FLAT / 64)), 256, 0, st>>>(op, FLAT / 64);
+    gemm_tile<T, 64, 64, BK(128), 2, 2><<<persist_grid(h, (long)(cdiv(N, 64)) * (FLAT / 64)), 256, 0, st>>>(op, FLAT / 64);
     timer_end(h, K_FC_DGRAD, st);
     CK_LAUNCH("fc_dgrad");
   }
@@ -259,7 +260,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
     timer_begin(h, K_CONV3_DGRAD, st);
-    gemm_tile<T, 64, 128, TBK, 1, 4><<<persist_grid(h, (long)(cdiv((long)N * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
+    gemm_tile<T, 64, 128, BK(64), 1, 4><<<persist_grid(h, (long)(cdiv((long)N * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_DGRAD, st);
     CK_LAUNCH("conv3_dgrad");
   }
@@ -278,7 +279,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     Conv2Dgrad<T> op{4 * NC, NC, N * 64, sw + sh.w2, (const T*)h->dact2, (const T*)h->act1,
                      (T*)h->dact1};
     timer_begin(h, K_CONV2_DGRAD, st);
-    gemm_tile<T, 32, 128, TBK, 1, 4><<<persist_grid(h, (long)(4 * NC / 128) * (1)), 256, 0, st>>>(op, 1);
+    gemm_tile<T, 32, 128, BK(64), 1, 4><<<persist_grid(h, (long)(4 * NC / 128) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV2_DGRAD, st);
     CK_LAUNCH("conv2_dgrad");
   }
