@@ -28,16 +28,33 @@ sys.path.insert(0, HERE)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-# algorithmic FLOPs per frame of each kernel (2*MACs)
-FLOPS_PER_FRAME = {
-    "conv1_fwd": 2 * 225 * 32 * 192, "conv2_fwd": 2 * 36 * 64 * 512, "conv3_fwd": 2 * 16 * 64 * 576,
-    "fc_fwd": 2 * 256 * 1024, "heads_fwd": 2 * 16 * 256,
-    "heads_dgrad": 2 * 16 * 256, "fc_dgrad": 2 * 256 * 1024, "conv3_dgrad": 2 * 16 * 64 * 576,
-    "conv2_dgrad": 2 * 36 * 64 * 512, "heads_wgrad": 2 * 16 * 256, "fc_wgrad": 2 * 256 * 1024,
-    "conv3_wgrad": 2 * 16 * 64 * 576, "conv2_wgrad": 2 * 36 * 64 * 512,
-    "conv1_wgrad": 2 * 225 * 32 * 192,
-}
+# Algorithmic work of each learner-step kernel, per frame of the batch plus a
+# per-launch constant (weights): (FLOPs/frame, HBM bytes/frame, HBM bytes/launch).  Bytes count
+# each operand once (compulsory traffic) at the compute type's width `es` (2 for bf16, 4 for
+# fp32); activations channels-last, fp32 where the kernel keeps fp32 (z, dy, LN stats).
+def kernel_work(es):
+    obs, a1, a2, a3 = 12288, 225 * 32 * es, 36 * 64 * es, 1024 * es
+    m1 = 225 * 4  # conv1 ReLU bit mask
+    return {
+        "conv1_fwd": (2 * 225 * 32 * 192, obs + a1 + m1, 32 * 192 * es),
+        "conv2_fwd": (2 * 36 * 64 * 512, a1 + a2, 64 * 512 * es),
+        "conv3_fwd": (2 * 16 * 64 * 576, a2 + 2 * a3 + 8, 64 * 576 * es + 2 * 1024 * 4),
+        "fc_fwd": (2 * 256 * 1024, a3 + 256 * 4 + 256 * es, 256 * 1024 * es),
+        "head_step": (2 * 3 * 16 * 256, 256 * es + 256 * 4 + 8 + 4 + 4 + 15 * 4 + 256 * es,
+                      2 * 16 * 256 * es),
+        "fc_dgrad": (2 * 256 * 1024, 256 * es + 1024 * 4, 256 * 1024 * es),
+        "ln_bwd": (10 * 1024, 1024 * 4 + 2 * a3 + 8, 2 * 1024 * 4),
+        "conv3_dgrad": (2 * 16 * 64 * 576, a3 + 2 * a2, 64 * 576 * es),
+        "conv2_dgrad_conv1_wgrad": (2 * 36 * 64 * 512 + 2 * 225 * 32 * 192, obs + a2 + m1,
+                                    64 * 512 * es),
+        "fc_wgrad": (2 * 256 * 1024, 256 * es + a3, 0),
+        "conv3_wgrad": (2 * 16 * 64 * 576, a3 + a2, 0),
+        "conv2_wgrad": (2 * 36 * 64 * 512, a2 + a1, 0),
+    }
+
+
 STEP_FLOPS_PER_FRAME = 17_743_872  # fwd 6,836,224 + bwd 10,907,648 (no conv1 dgrad)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA, MI355X_MICROARCH.md
 
 
@@ -78,11 +95,12 @@ def cpu_baseline(B, T, A, seconds):
                       f"{threads} threads, {cpu}) after 2 warm-up; median step {med * 1e3:.1f} ms"}
 
 
-PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3Fwd",
-                 "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "heads_dgrad": "HeadsDgrad",
-                 "fc_dgrad": "FcDgrad", "conv3_dgrad": "Conv3Dgrad", "conv2_dgrad": "Conv2Dgrad",
-                 "heads_wgrad": "HeadsWgrad", "fc_wgrad": "FcWgrad", "conv3_wgrad": "Conv3Wgrad",
-                 "conv2_wgrad": "Conv2Wgrad", "conv1_wgrad": "Conv1Wgrad"}
+PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
+                 "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "head_step": "head_step",
+                 "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
+                 "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "fc_wgrad": "FcWgrad",
+                 "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
+                 "reduce_grads": "reduce_grads", "adam": "adam"}
 
 
 def profiled_traffic(kernel, dtype):
@@ -158,6 +176,7 @@ def main():
         step()
     torch.cuda.synchronize()
     rk = args.roofline_kernel
+    work = kernel_work(2 if args.dtype == "bf16" else 4)
     # dominant kernel: pick the one with the largest measured time in a short probe
     probe = {}
     if rk is None:
@@ -168,7 +187,7 @@ def main():
             ms, n = eng.timer_read()
             if n:
                 probe[kname] = ms / n
-        rk = max((k for k in probe if k in FLOPS_PER_FRAME), key=probe.get)
+        rk = max((k for k in probe if k in work), key=probe.get)
     torch.cuda.synchronize()
 
     eng.timer_start(rk, args.steps)
@@ -195,8 +214,15 @@ def main():
     value = frames / elapsed
     ms_step = elapsed * 1e3 / args.steps
     k_avg_ms = k_ms / max(k_n, 1)
-    achieved = FLOPS_PER_FRAME[rk] * B * T / (k_avg_ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.dtype]
+    # roofline of the dominant kernel: the bound is whichever of MFMA time and HBM time of its
+    # algorithmic work is larger; `achieved` is that work over the measured launch time
+    fpf, bpf, bpl = work[rk]
+    flops, nbytes = fpf * B * T, bpf * B * T + bpl
+    t_s = k_avg_ms * 1e-3
+    if flops / (PEAK_TFLOPS[args.dtype] * 1e12) >= nbytes / (PEAK_HBM_GBS * 1e9):
+        bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
+    else:
+        bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
     traffic, tsrc = profiled_traffic(rk, args.dtype)
     traffic_src = (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+WRITE_SIZE, "
                    "bytes per launch)") if tsrc else None
@@ -210,9 +236,10 @@ def main():
         "config": {"workload": f"IMPALA procgen learner step, NatureCNN actor-critic, "
                                f"B={B}/GPU T={T} A={A}, global B={B * world}",
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": rk, "achieved": round(achieved, 2),
-                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+        "roofline": {"bound": bound, "kernel": rk, "achieved": round(achieved, 2),
+                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic": {"flops": flops, "bytes": nbytes},
                      "avg_launch_us": round(k_avg_ms * 1e3, 2),
                      "launches": k_n},
         "step_tflops": round(STEP_FLOPS_PER_FRAME * value / world / 1e12, 2),

@@ -77,13 +77,15 @@ DEV void c1_stash_frame(T* img, int tid, const uint4 v[3]) {
 }
 
 // ---------------------------------------------------------------------------------------
-// forward: act1[n][p][oc] = relu(sum W'[oc][k'] s2d * 1/255 + b1), weights in registers.
+// forward: act1[n][p][oc] = relu(sum W'[oc][k'] s2d * 1/255 + b1), weights in registers;
+// optionally the ReLU bit mask mask[n][p] (bit oc = act1 > 0) for the fused backward.
 // ---------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__ x,
                                                      const T* __restrict__ w,  // [32][192] k'
                                                      const float* __restrict__ bias,
-                                                     T* __restrict__ out, int N) {
+                                                     T* __restrict__ out,
+                                                     uint32_t* __restrict__ mask, int N) {
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int LDI = c1::L<T>::LDI;
@@ -124,52 +126,101 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
         acc[1] = F::mma(wa[1][ks], b, acc[1]);
       }
       const int pc = tile * 16 + (lane & 15);
-      if (pc < c1::NPIX) {
+      uint32_t bits = 0;  // ReLU mask of this pixel's 32 channels (bit oc), for the backward
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          float v[4];
+      for (int i = 0; i < 2; ++i) {
+        float v[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[i][q] * (1.f / 255.f) + bb[i][q], 0.f);
-          store4(out + ((size_t)f * c1::NPIX + pc) * OC1 + 16 * i + 4 * (lane >> 4), v);
+        for (int q = 0; q < 4; ++q) {
+          v[q] = fmaxf(acc[i][q] * (1.f / 255.f) + bb[i][q], 0.f);
+          bits |= (v[q] > 0.f ? 1u : 0u) << (16 * i + 4 * (lane >> 4) + q);
         }
+        if (pc < c1::NPIX) store4(out + ((size_t)f * c1::NPIX + pc) * OC1 + 16 * i + 4 * (lane >> 4), v);
       }
+      bits |= __shfl_xor(bits, 16, 64);
+      bits |= __shfl_xor(bits, 32, 64);
+      if (mask && pc < c1::NPIX && lane < 16) mask[(size_t)f * c1::NPIX + pc] = bits;
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// weight gradient: dW'[oc][k'] = sum_{frames, p} dY[p][oc] * s2d[row(p, tap)][ch]  (1/255 at
-// the end), reduction over the 225 (padded 256) pixels of each frame.  Wave w owns tap w
-// (48 channels = 3 column tiles) for both 16-row oc tiles.  The workgroup handles a
-// contiguous run of frames and writes one fp32 partial slab [32][192] (k' order) + bias sums.
+// conv2 input gradient + ReLU mask + conv1 weight gradient, one frame at a time, fused:
+//
+//   dY1[p][ci] = [act1 > 0] * sum_{kh,kw,oc: iy = 2 oy + kh, ix = 2 ox + kw} dY2[oy][ox][oc] W2[oc][kh][kw][ci]
+//   dW1'[oc][k'] += sum_p dY1[p][oc] * s2d[row(p, tap)][ch]     (1/255 at the end)
+//
+// dY1 (the 15x15x32 conv2 input gradient) never leaves LDS.  The conv2 dgrad is split into the
+// four stride-parity classes (iy % 2, ix % 2): each class is a GEMM [32 ci] x [8x8 cells] with
+// K = 4 taps x 64 oc, and wave w owns class w for the whole kernel, so its W2 fragments (the
+// A operand, ci x oc) stay in registers; the B operand is a 16-byte LDS read of the frame's
+// dY2 held in a zero-bordered 9x9 cell grid (no bounds tests).  The ReLU mask of act1 comes
+// from the bit mask conv1_fwd_s2d writes (one 32-bit word per pixel).  The conv1 weight
+// gradient then reads dY1 and the frame's s2d image from LDS: wave w owns tap w (48 channels
+// = 3 column tiles) for both 16-row oc tiles.  Each workgroup takes a contiguous run of frames
+// and writes one fp32 partial slab [32][192] (k' order) + bias sums, reduced by reduce_grads.
 // ---------------------------------------------------------------------------------------
-template <typename T> constexpr int c1_wgrad_groups() { return sizeof(T) == 2 ? 2 : 1; }
+namespace c12 {
+constexpr int QG = 9;                          // dY2 cell grid: oy = r - 1, r in [0, 9)
+constexpr int NCELL = QG * QG;
+}  // namespace c12
+
+// G 4-wave groups per workgroup take alternating frames of the run (G frames in flight per CU
+// on top of the one-frame register prefetch); their partials are summed in a fixed order.
+template <typename T> constexpr int c12_groups() { return sizeof(T) == 2 ? 2 : 1; }
 
 template <typename T>
-__global__ __launch_bounds__(256 * c1_wgrad_groups<T>()) void conv1_wgrad_s2d(const uint8_t* __restrict__ x,
-                                                       const T* __restrict__ dy,  // [N][225][32]
-                                                       float* __restrict__ slab,
-                                                       float* __restrict__ slab_bias, int N,
-                                                       int fpw) {
-  // two 4-wave groups per workgroup work on alternating frames of the workgroup's run (two
-  // frames in flight per CU on top of the one-frame register prefetch); their accumulators are
-  // summed in a fixed order at the end.
+__global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const uint8_t* __restrict__ x,
+                                                      const T* __restrict__ w2,     // [64][512]
+                                                      const T* __restrict__ dy2,    // [N][36][64]
+                                                      const uint32_t* __restrict__ mask1,  // [N][225]
+                                                      float* __restrict__ slab,
+                                                      float* __restrict__ slab_bias, int N,
+                                                      int fpw) {
   using F = Frag<T>;
   typedef typename F::vec V;
+  constexpr int KPL = F::KPL, KS = F::KSTEP;
   constexpr int LDI = c1::L<T>::LDI;
   constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int LDX = OC1 + VEC;                      // dY tile row (elements)
-  constexpr int DYV = c1::NPIX * OC1 / VEC;           // 16-byte vectors per dY frame
-  constexpr int NDY = (DYV + 255) / 256;
+  constexpr int LDX = OC1 + VEC;                      // dY1 tile row (elements)
+  constexpr int LD2 = OC2 + VEC;                      // dY2 cell row (elements)
   constexpr int IMGSZ = c1::GRID * c1::GRID * LDI, DYSZ = c1::NPAD * LDX;
-  constexpr int G = c1_wgrad_groups<T>();
-  __shared__ __attribute__((aligned(16))) T smem[G * (IMGSZ + DYSZ)];
+  constexpr int D2V = P2 * OC2 / VEC;                 // 16-byte vectors of one dY2 frame
+  constexpr int ND2 = (D2V + 255) / 256;
+  constexpr int NOK = OC2 / KS;                       // k-steps per tap
+  constexpr int G = c12_groups<T>();
+  constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;  // elements of one group's tiles
+  __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
+  __shared__ uint32_t msk_all[G][c1::NPIX];
+  __shared__ float bred[8 * OC1];
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-  T* img = smem + grp * (IMGSZ + DYSZ);
+  T* img = smem + grp * GSZ;
   T* dyt = img + IMGSZ;
+  T* d2s = dyt + DYSZ;
+  uint32_t* msk = msk_all[grp];
   const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
-  // zero the padding rows 225..255 of the dY tile once (never overwritten)
+  // zero the dY1 padding rows 225..255 and the dY2 cell grid once (the border stays zero)
   for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX; e += 256) dyt[c1::NPIX * LDX + e] = (T)0.f;
+  for (int e = tid; e < c12::NCELL * LD2; e += 256) d2s[e] = (T)0.f;
+  // class of this wave: output pixels iy = 2 qy + py, ix = 2 qx + px; taps kh = py + 2 j1,
+  // kw = px + 2 j2 read dY2 at (qy - j1, qx - j2)
+  const int py = wave >> 1, px = wave & 1;
+  V wa[4][2][NOK];  // [tap j1*2+j2][ci tile][k-step]: A[ci][oc] = W2[oc][kh][kw][ci]
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < NOK; ++ks) {
+        const T* src = w2 + (size_t)(ks * KS + KPL * (lane >> 4)) * K2 + (kh * KS2 + kw) * OC1 +
+                       16 * i + (lane & 15);
+        V v;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) v[j] = src[(size_t)j * K2];
+        wa[t][i][ks] = v;
+      }
+  }
   f32x4 acc[2][3];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -177,38 +228,73 @@ __global__ __launch_bounds__(256 * c1_wgrad_groups<T>()) void conv1_wgrad_s2d(co
     for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bias_acc = 0.f;
   uint4 nv[3];
-  V ndy[NDY];
+  V nd2[ND2];
+  uint32_t nmk = 0;
   auto fetch = [&](int f) {
     c1_load_frame<T>(x + (size_t)f * IMG, tid, nv);
-    const T* src = dy + (size_t)f * c1::NPIX * OC1;
+    const T* src = dy2 + (size_t)f * P2 * OC2;
 #pragma unroll
-    for (int i = 0; i < NDY; ++i) {
+    for (int i = 0; i < ND2; ++i) {
       const int e = tid + i * 256;
-      ndy[i] = e < DYV ? *reinterpret_cast<const V*>(src + e * VEC) : F::zero();
+      nd2[i] = e < D2V ? *reinterpret_cast<const V*>(src + e * VEC) : F::zero();
     }
+    if (tid < c1::NPIX) nmk = mask1[(size_t)f * c1::NPIX + tid];
   };
   if (f0 + grp < f1) fetch(f0 + grp);
   const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDI;
+  const int kl = KPL * (lane >> 4);
   const int n_it = (f1 - f0 + G - 1) / G;
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
     const bool active = f < f1;
-    __syncthreads();
+    __syncthreads();  // the previous frame's readers are done
     if (active) {
-      c1_stash_frame<T>(img, tid, nv);
+    c1_stash_frame<T>(img, tid, nv);
 #pragma unroll
-      for (int i = 0; i < NDY; ++i) {
-        const int e = tid + i * 256;
-        if (e < DYV) {
-          const int row = (e * VEC) / OC1, col = (e * VEC) % OC1;
-          *reinterpret_cast<V*>(dyt + row * LDX + col) = ndy[i];
-        }
+    for (int i = 0; i < ND2; ++i) {
+      const int e = tid + i * 256;
+      if (e < D2V) {
+        const int cell = (e * VEC) / OC2, oc = (e * VEC) % OC2;
+        const int oy = cell / H2, ox = cell - oy * H2;
+        *reinterpret_cast<V*>(d2s + ((oy + 1) * c12::QG + ox + 1) * LD2 + oc) = nd2[i];
       }
+    }
+    if (tid < c1::NPIX) msk[tid] = nmk;
     }
     __syncthreads();
     if (f + G < f1) fetch(f + G);
+    // ---- conv2 dgrad of class `wave` -> masked dY1 rows in LDS ----
+#pragma unroll
+    for (int nt = 0; nt < 4 && active; ++nt) {  // 16-cell column tiles of the 8x8 class grid
+      const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
+      f32x4 d[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const T* brow = d2s + ((qy - (t >> 1) + 1) * c12::QG + qx - (t & 1) + 1) * LD2 + kl;
+#pragma unroll
+        for (int ks = 0; ks < NOK; ++ks) {
+          const V bv = *reinterpret_cast<const V*>(brow + ks * KS);
+          d[0] = F::mma(wa[t][0][ks], bv, d[0]);
+          d[1] = F::mma(wa[t][1][ks], bv, d[1]);
+        }
+      }
+      const int iy = 2 * qy + py, ix = 2 * qx + px;
+      if (iy < H1 && ix < H1) {
+        const int p = iy * H1 + ix;
+        const uint32_t m = msk[p];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int ci = 16 * i + 4 * (lane >> 4);
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = (m >> (ci + q)) & 1u ? d[i][q] : 0.f;
+          store4(dyt + p * LDX + ci, v);
+        }
+      }
+    }
+    __syncthreads();  // (every group reaches it: no early exit for an idle group)
     if (!active) continue;
-    {  // bias: 8 row groups x 32 channels, partial sums kept per thread across frames
+    {  // conv1 bias: 8 row groups x 32 channels, partial sums kept per thread across frames
       const int oc = tid & 31, rg = tid >> 5;
       float s0 = 0.f, s1 = 0.f;
       int r = rg;
@@ -219,8 +305,9 @@ __global__ __launch_bounds__(256 * c1_wgrad_groups<T>()) void conv1_wgrad_s2d(co
       if (r < c1::NPIX) s0 += (float)dyt[r * LDX + oc];
       bias_acc += s0 + s1;
     }
+    // ---- conv1 weight gradient: reduction over the frame's (padded) 256 pixels ----
 #pragma unroll 2
-    for (int kk = 0; kk < c1::NPAD; kk += F::KSTEP) {
+    for (int kk = 0; kk < c1::NPAD; kk += KS) {
       V a[2], b[3];
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
@@ -257,36 +344,38 @@ __global__ __launch_bounds__(256 * c1_wgrad_groups<T>()) void conv1_wgrad_s2d(co
         for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
     }
   }
-  // fixed-order combine: group 1 -> LDS -> group 0; bias row groups likewise
-  __syncthreads();
+  // fixed-order combine of the groups: group g > 0 -> LDS -> group 0, one group at a time
   float* red = reinterpret_cast<float*>(smem);
-  if (G > 1 && grp == 1) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int g = 1; g < G; ++g) {
+    __syncthreads();
+    if (grp == g) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) red[((i * 3 + j) * 4 + q) * 256 + tid] = acc[i][j][q];
-    red[24 * 256 + tid] = bias_acc;
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) red[((i * 3 + j) * 4 + q) * 256 + tid] = acc[i][j][q];
+      red[24 * 256 + tid] = bias_acc;
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * 3 + j) * 4 + q) * 256 + tid];
+      bias_acc += red[24 * 256 + tid];
+    }
   }
-  __syncthreads();
-  if (G > 1 && grp == 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * 3 + j) * 4 + q) * 256 + tid];
-    bias_acc += red[24 * 256 + tid];
-  }
-  __syncthreads();
-  if (grp == 0) red[tid] = bias_acc;
+  if (grp == 0) bred[tid] = bias_acc;
   __syncthreads();
   if (grp != 0) return;
   if (tid < OC1) {
     float bsum = 0.f;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) bsum += red[g * 32 + tid];
+    for (int g = 0; g < 8; ++g) bsum += bred[g * 32 + tid];
     slab_bias[(size_t)blockIdx.x * OC1 + tid] = bsum;
   }
   const size_t so = (size_t)blockIdx.x * OC1 * K1;

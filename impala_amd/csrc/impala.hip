@@ -76,15 +76,14 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 
 // kernel ids for the live launch timer (impala_timer_*)
 enum KernelId {
-  K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV3_FWD, K_LN_FWD, K_FC_FWD, K_HEADS_FWD, K_LOSS,
-  K_HEADS_DGRAD, K_FC_DGRAD, K_LN_BWD, K_CONV3_DGRAD, K_CONV2_DGRAD, K_HEADS_WGRAD,
-  K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV1_WGRAD, K_REDUCE, K_SUMSQ, K_ADAM,
-  K_COUNT
+  K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
+  K_LN_BWD, K_CONV3_DGRAD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
+  K_SUMSQ, K_ADAM, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
-    "conv1_fwd", "conv2_fwd", "conv3_fwd", "ln_fwd", "fc_fwd", "heads_fwd", "head_step",
-    "heads_dgrad", "fc_dgrad", "ln_bwd", "conv3_dgrad", "conv2_dgrad", "heads_wgrad",
-    "fc_wgrad", "conv3_wgrad", "conv2_wgrad", "conv1_wgrad", "reduce_grads", "sumsq", "adam"};
+    "conv1_fwd", "conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
+    "ln_bwd", "conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
+    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam"};
 
 struct impala_learner {
   impala_config cfg;
@@ -102,7 +101,8 @@ struct impala_learner {
   size_t ws_bytes = 0;
   void* shadow = nullptr;
   float* vecs = nullptr;
-  void *act1, *act2, *act3, *y, *h, *dH, *dz, *dact3, *dact2, *dact1;
+  void *act1, *act2, *act3, *y, *h, *dH, *dz, *dact3, *dact2;
+  uint32_t* mask1;  // conv1 ReLU bit mask [N][225]
   float *lnstat, *z, *heads, *dy;
   float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
   float *loss_part, *sumsq_part;
@@ -117,6 +117,7 @@ struct impala_learner {
   bool use_side = true;
   // live launch timer: hipEvent pairs around every launch of one kernel id
   int n_cu = 256;
+  int red_mode = 2;           // slab reductions: 0 all at the end, 1 per branch, 2 side + conv1
   int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
   hipEvent_t* timer_ev = nullptr;
@@ -155,7 +156,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   const float* vv = h->vecs;
   timer_begin(h, K_CONV1_FWD, st);
   conv1_fwd_s2d<T><<<min(n, h->n_cu * 4), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
-                                                         (T*)h->act1, n);
+                                                         (T*)h->act1, h->mask1, n);
   timer_end(h, K_CONV1_FWD, st);
   CK_LAUNCH("conv1_fwd");
   {
@@ -192,6 +193,18 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   return 0;
 }
 
+// slab-reduction segment groups (indices into RedArgs::seg, in the order create() adds them)
+enum { RS_CONV1 = 0, RS_CONV2 = 2, RS_CONV3 = 4, RS_FC = 7, RS_END = 11 };
+
+int reduce_segments(impala_learner* h, int s_lo, int s_hi, hipStream_t st, int fin) {
+  const int n = h->red.wg_start[s_hi] - h->red.wg_start[s_lo];
+  timer_begin(h, K_REDUCE, st);
+  reduce_grads_kernel<<<n, 256, 0, st>>>(h->red, s_lo, fin);
+  timer_end(h, K_REDUCE, st);
+  CK_LAUNCH("reduce_grads");
+  return 0;
+}
+
 template <typename T>
 int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   using namespace net;
@@ -219,9 +232,9 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     ha.cpg = h->cfg.clip_pg_rho_threshold; ha.ent_coef = h->cfg.entropy_coeff;
     ha.dz = h->dz; ha.partials = h->loss_part; ha.slab_h = h->s_h; ha.slab_bh = h->s_bh;
     ha.heads_out = h->heads;
-    timer_begin(h, K_LOSS, st);
+    timer_begin(h, K_HEAD_STEP, st);
     head_step_kernel<T><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
-    timer_end(h, K_LOSS, st);
+    timer_end(h, K_HEAD_STEP, st);
     CK_LAUNCH("head_step");
   }
   if (int r = fork(1)) return r;  // dz ready
@@ -233,6 +246,8 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
         op, h->s_fc, h->s_bfc, h->spfc.mps);
     timer_end(h, K_FC_WGRAD, ss);
     CK_LAUNCH("fc_wgrad");
+    if (h->red_mode == 1)
+      if (int r = reduce_segments(h, RS_FC, RS_END, ss, 0)) return r;  // fc + heads slabs
   }
   {
     FcDgrad<T> op{N, sw + sh.wfc, (const T*)h->dz, h->dy};
@@ -256,6 +271,8 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
         op, h->s_w3, h->s_b3, h->sp3.mps);
     timer_end(h, K_CONV3_WGRAD, ss);
     CK_LAUNCH("conv3_wgrad");
+    if (h->red_mode == 1)
+      if (int r = reduce_segments(h, RS_CONV3, RS_FC, ss, 0)) return r;  // conv3 + LayerNorm
   }
   {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
@@ -273,30 +290,33 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
         op, h->s_w2, h->s_b2, h->sp2.mps);
     timer_end(h, K_CONV2_WGRAD, ss);
     CK_LAUNCH("conv2_wgrad");
+    if (h->red_mode == 1) {
+      if (int r = reduce_segments(h, RS_CONV2, RS_CONV3, ss, 0)) return r;
+    } else if (h->red_mode == 2) {
+      if (int r = reduce_segments(h, RS_CONV2, RS_END, ss, 0)) return r;
+    }
   }
-  {
-    const int NC = (N * 64 + 127) / 128 * 128;  // class stride, multiple of the tile width
-    Conv2Dgrad<T> op{4 * NC, NC, N * 64, sw + sh.w2, (const T*)h->dact2, (const T*)h->act1,
-                     (T*)h->dact1};
-    timer_begin(h, K_CONV2_DGRAD, st);
-    gemm_tile<T, 32, 128, BK(64), 1, 4><<<persist_grid(h, (long)(4 * NC / 128) * (1)), 256, 0, st>>>(op, 1);
-    timer_end(h, K_CONV2_DGRAD, st);
-    CK_LAUNCH("conv2_dgrad");
+  // conv2 input gradient (ReLU-masked) + conv1 weight gradient, fused per frame
+  timer_begin(h, K_CONV12_BWD, st);
+  conv12_bwd_s2d<T><<<h->c1_wg, 256 * c12_groups<T>(), 0, st>>>(b->obs, sw + sh.w2, (const T*)h->dact2, h->mask1,
+                                              h->s_w1, h->s_b1, N, h->c1_fpw);
+  timer_end(h, K_CONV12_BWD, st);
+  CK_LAUNCH("conv2_dgrad_conv1_wgrad");
+  // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were
+  // reduced on the side stream right after their weight gradients ----
+  if (h->red_mode == 0) {
+    if (h->use_side) {  // join
+      CK(hipEventRecord(h->ev_join, ss));
+      CK(hipStreamWaitEvent(st, h->ev_join, 0));
+    }
+    if (int r = reduce_segments(h, RS_CONV1, RS_END, st, 1)) return r;
+  } else {
+    if (int r = reduce_segments(h, RS_CONV1, RS_CONV2, st, 1)) return r;
+    if (h->use_side) {  // join
+      CK(hipEventRecord(h->ev_join, ss));
+      CK(hipStreamWaitEvent(st, h->ev_join, 0));
+    }
   }
-  timer_begin(h, K_CONV1_WGRAD, st);
-  conv1_wgrad_s2d<T><<<h->c1_wg, 256 * c1_wgrad_groups<T>(), 0, st>>>(b->obs, (const T*)h->dact1, h->s_w1, h->s_b1, N,
-                                               h->c1_fpw);
-  timer_end(h, K_CONV1_WGRAD, st);
-  CK_LAUNCH("conv1_wgrad");
-  if (h->use_side) {  // join
-    CK(hipEventRecord(h->ev_join, ss));
-    CK(hipStreamWaitEvent(st, h->ev_join, 0));
-  }
-  // ---- slab reduction -> canonical grads, sum of squares, loss metrics, step += 1 ----
-  timer_begin(h, K_REDUCE, st);
-  reduce_grads_kernel<<<h->n_red_wg, 256, 0, st>>>(h->red);
-  timer_end(h, K_REDUCE, st);
-  CK_LAUNCH("reduce_grads");
   return 0;
 }
 
@@ -432,7 +452,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t o_dz = take((size_t)N * HID * es);
   const size_t o_dact3 = take((size_t)N * FLAT * es);
   const size_t o_dact2 = take((size_t)N * P2 * OC2 * es);
-  const size_t o_dact1 = take((size_t)N * P1 * OC1 * es);
+  const size_t o_mask1 = take((size_t)N * P1 * 4);
   const size_t o_lnstat = take((size_t)N * 2 * 4);
   const size_t o_z = take((size_t)N * HID * 4);
   const size_t o_heads = take((size_t)N * HEADS * 4);
@@ -468,7 +488,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->vecs = (float*)(w + o_vecs);
   h->act1 = w + o_act1; h->act2 = w + o_act2; h->act3 = w + o_act3; h->y = w + o_y;
   h->h = w + o_h; h->dH = w + o_dH; h->dz = w + o_dz; h->dact3 = w + o_dact3;
-  h->dact2 = w + o_dact2; h->dact1 = w + o_dact1;
+  h->dact2 = w + o_dact2; h->mask1 = (uint32_t*)(w + o_mask1);
   h->lnstat = (float*)(w + o_lnstat); h->z = (float*)(w + o_z); h->heads = (float*)(w + o_heads);
   h->dy = (float*)(w + o_dy);
   h->s_w1 = (float*)(w + o_sw1); h->s_b1 = (float*)(w + o_sb1);
@@ -478,6 +498,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->s_h = (float*)(w + o_sh); h->s_bh = (float*)(w + o_sbh);
   h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
   h->step = (int64_t*)(w + o_step);
+  if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   const char* serial = std::getenv("IMPALA_SERIAL_STREAM");  // profiling: one stream only
   if (serial && serial[0] == '1') {
     h->use_side = false;
@@ -514,6 +535,10 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     add(h->s_h, h->sph.S, HEADS * HID, RK_HEADS_W, 0);
     add(h->s_bh, h->sph.S, HEADS, RK_HEADS_B, 0);
     h->n_red_wg = ra.wg_start[ns];
+    if (ns != RS_END) {
+      impala_destroy(h);
+      return fail(IMPALA_E_STATE, "reduce segment table out of sync");
+    }
     ra.nseg = ns;
     ra.cn = h->cn;
     ra.sumsq_part = h->sumsq_part;

@@ -459,16 +459,20 @@ DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
 // Each segment is processed by workgroups of 256 threads = (256/SG) float4 columns x SG
 // split groups; split group g sums splits g, g+SG, ... and the SG partials are combined in
 // LDS in a fixed order (deterministic for a given SG).  wg_start[] holds each segment's
-// first workgroup.
-__global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a) {
+// first workgroup.  One launch reduces segments [s_lo, s_hi) (grid = their workgroups), so
+// each weight-gradient branch can be reduced as soon as its slab is complete; the workgroup's
+// global index (wg_start[s_lo] + blockIdx.x) names its sum-of-squares partial, so the partial
+// order -- and the norm -- does not depend on how the segments were grouped into launches.
+__global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int s_lo, int fin) {
   __shared__ f32x4 part[256];
   __shared__ float red[4];
-  int s = 0;
-  while ((int)blockIdx.x >= a.wg_start[s + 1]) ++s;
+  const int wg = a.wg_start[s_lo] + (int)blockIdx.x;
+  int s = s_lo;
+  while (wg >= a.wg_start[s + 1]) ++s;
   const RedSeg& sg = a.seg[s];
   const int SG = sg.sg, cols = 256 / SG;
   const int col = threadIdx.x % cols, grp = threadIdx.x / cols;
-  const int v4 = (blockIdx.x - a.wg_start[s]) * cols + col;  // float4 index in the segment
+  const int v4 = (wg - a.wg_start[s]) * cols + col;  // float4 index in the segment
   const bool in = v4 * 4 < sg.count;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   if (in) {
@@ -504,8 +508,8 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a) {
   sq = wave_sum(sq);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
-  if (threadIdx.x == 0) a.sumsq_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-  if (blockIdx.x == 0 && threadIdx.x == 64) {
+  if (threadIdx.x == 0) a.sumsq_part[wg] = red[0] + red[1] + red[2] + red[3];
+  if (fin && blockIdx.x == 0 && threadIdx.x == 64) {
     finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
     *a.step += 1;
   }

@@ -43,7 +43,7 @@ def test_host_only_entry_points():
     assert abs(cfg.lr - 1e-4) < 1e-9 and abs(cfg.adam_eps - 1e-5) < 1e-12
     assert abs(cfg.max_grad_norm - 0.5) < 1e-9 and abs(cfg.entropy_coeff - 0.01) < 1e-9
     names = [lib.impala_kernel_name(i).decode() for i in range(lib.impala_kernel_count())]
-    assert "conv1_wgrad" in names and "adam" in names and len(names) == len(set(names))
+    assert "conv2_dgrad_conv1_wgrad" in names and "adam" in names and len(names) == len(set(names))
 
 
 @pytest.mark.parametrize("field,value", [("batch_size", 0), ("rollout_length", 1),

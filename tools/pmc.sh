@@ -5,7 +5,7 @@ TAG=${1:-pmc}; shift
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--steps 10 --warmup 2 --no-cpu-baseline --roofline-kernel conv1_wgrad $@"
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline --roofline-kernel conv2_dgrad_conv1_wgrad $@"
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES" \

@@ -20,8 +20,8 @@ def short(name):
     n = name.split("(")[0]
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
-    if "conv1_wgrad_s2d" in n:
-        return "Conv1Wgrad"
+    if "conv12_bwd_s2d" in n:
+        return "Conv12Bwd"
     if "head_step" in n:
         return "head_step"
     if "gemm_tile" in n or "gemm_wg" in n or "gemm_rc" in n:
