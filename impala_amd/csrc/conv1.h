@@ -188,11 +188,12 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
   constexpr int D2V = P2 * OC2 / VEC;                 // 16-byte vectors of one dY2 frame
   constexpr int ND2 = (D2V + 255) / 256;
   constexpr int NOK = OC2 / KS;                       // k-steps per tap
+  constexpr int PFB = sizeof(T) == 2 ? 2 : 1;         // dgrad B-fragment buffers (prefetch)
   constexpr int G = c12_groups<T>();
   constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;  // elements of one group's tiles
   __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
   __shared__ uint32_t msk_all[G][c1::NPIX];
-  __shared__ float bred[8 * OC1];
+  __shared__ float bred[4 * G * OC1];
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   T* img = smem + grp * GSZ;
   T* dyt = img + IMGSZ;
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bias_acc = 0.f;
+  float bsum[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // conv1 bias partials
   uint4 nv[3];
   V nd2[ND2];
   uint32_t nmk = 0;
@@ -263,52 +264,59 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
     }
     __syncthreads();
     if (f + G < f1) fetch(f + G);
-    // ---- conv2 dgrad of class `wave` -> masked dY1 rows in LDS ----
+    // ---- conv2 dgrad of class `wave` -> masked dY1 rows in LDS (+ conv1 bias partials) ----
+    if (active) {
+      V bq[PFB][4 * NOK];  // B fragments of PFB consecutive 16-cell column tiles
+      auto load_b = [&](int nt, V* bb) {
+        const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
 #pragma unroll
-    for (int nt = 0; nt < 4 && active; ++nt) {  // 16-cell column tiles of the 8x8 class grid
-      const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
-      f32x4 d[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        for (int t = 0; t < 4; ++t) {
+          const T* brow = d2s + ((qy - (t >> 1) + 1) * c12::QG + qx - (t & 1) + 1) * LD2 + kl;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const T* brow = d2s + ((qy - (t >> 1) + 1) * c12::QG + qx - (t & 1) + 1) * LD2 + kl;
-#pragma unroll
-        for (int ks = 0; ks < NOK; ++ks) {
-          const V bv = *reinterpret_cast<const V*>(brow + ks * KS);
-          d[0] = F::mma(wa[t][0][ks], bv, d[0]);
-          d[1] = F::mma(wa[t][1][ks], bv, d[1]);
+          for (int ks = 0; ks < NOK; ++ks) bb[t * NOK + ks] = *reinterpret_cast<const V*>(brow + ks * KS);
         }
-      }
-      const int iy = 2 * qy + py, ix = 2 * qx + px;
-      if (iy < H1 && ix < H1) {
-        const int p = iy * H1 + ix;
-        const uint32_t m = msk[p];
+      };
+      if constexpr (PFB == 2) load_b(0, bq[0]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int ci = 16 * i + 4 * (lane >> 4);
-          float v[4];
+      for (int nt = 0; nt < 4; ++nt) {  // 16-cell column tiles of the 8x8 class grid
+        V* cur = bq[PFB == 2 ? (nt & 1) : 0];
+        if constexpr (PFB == 2) {
+          if (nt + 1 < 4) load_b(nt + 1, bq[(nt + 1) & 1]);
+        } else {
+          load_b(nt, cur);
+        }
+        f32x4 d[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = (m >> (ci + q)) & 1u ? d[i][q] : 0.f;
-          store4(dyt + p * LDX + ci, v);
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int ks = 0; ks < NOK; ++ks) {
+            d[0] = F::mma(wa[t][0][ks], cur[t * NOK + ks], d[0]);
+            d[1] = F::mma(wa[t][1][ks], cur[t * NOK + ks], d[1]);
+          }
+        const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
+        const int iy = 2 * qy + py, ix = 2 * qx + px;
+        if (iy < H1 && ix < H1) {
+          const int p = iy * H1 + ix;
+          const uint32_t m = msk[p];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int ci = 16 * i + 4 * (lane >> 4);
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[q] = (m >> (ci + q)) & 1u ? d[i][q] : 0.f;
+              bsum[i][q] += v[q];
+            }
+            store4(dyt + p * LDX + ci, v);
+          }
         }
       }
     }
     __syncthreads();  // (every group reaches it: no early exit for an idle group)
     if (!active) continue;
-    {  // conv1 bias: 8 row groups x 32 channels, partial sums kept per thread across frames
-      const int oc = tid & 31, rg = tid >> 5;
-      float s0 = 0.f, s1 = 0.f;
-      int r = rg;
-      for (; r + 8 < c1::NPIX; r += 16) {
-        s0 += (float)dyt[r * LDX + oc];
-        s1 += (float)dyt[(r + 8) * LDX + oc];
-      }
-      if (r < c1::NPIX) s0 += (float)dyt[r * LDX + oc];
-      bias_acc += s0 + s1;
-    }
-    // ---- conv1 weight gradient: reduction over the frame's (padded) 256 pixels ----
-#pragma unroll 2
-    for (int kk = 0; kk < c1::NPAD; kk += KS) {
-      V a[2], b[3];
+    // ---- conv1 weight gradient: reduction over the frame's (padded) 256 pixels, fragments
+    // software-pipelined one k-step ahead ----
+    auto frag = [&](int kk, V* a, V* b) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
       if constexpr (sizeof(T) == 2) {
@@ -338,13 +346,40 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
           b[j] = v;
         }
       }
+    };
+    constexpr int NKK = c1::NPAD / KS;
+    V fa[2][2], fb[2][3];
+    frag(0, fa[0], fb[0]);
+#pragma unroll
+    for (int s2 = 0; s2 < NKK; ++s2) {
+      if (s2 + 1 < NKK) frag((s2 + 1) * KS, fa[(s2 + 1) & 1], fb[(s2 + 1) & 1]);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
     }
   }
-  // fixed-order combine of the groups: group g > 0 -> LDS -> group 0, one group at a time
+  // conv1 bias: sum each lane's partials over the 16 lanes of its channel group (fixed
+  // butterfly order), then over the 4 class waves and the G groups in LDS, in a fixed order
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = bsum[i][q];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      bsum[i][q] = v;
+    }
+  __syncthreads();  // all groups are done with their tiles
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bred[(grp * 4 + wave) * OC1 + 16 * i + 4 * (lane >> 4) + q] = bsum[i][q];
+  }
+  // fixed-order combine of the groups' weight-gradient partials: group g > 0 -> LDS -> group 0
   float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int g = 1; g < G; ++g) {
@@ -356,7 +391,6 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
         for (int j = 0; j < 3; ++j)
 #pragma unroll
           for (int q = 0; q < 4; ++q) red[((i * 3 + j) * 4 + q) * 256 + tid] = acc[i][j][q];
-      red[24 * 256 + tid] = bias_acc;
     }
     __syncthreads();
     if (grp == 0) {
@@ -366,17 +400,15 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
         for (int j = 0; j < 3; ++j)
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[i][j][q] += red[((i * 3 + j) * 4 + q) * 256 + tid];
-      bias_acc += red[24 * 256 + tid];
     }
   }
-  if (grp == 0) bred[tid] = bias_acc;
   __syncthreads();
   if (grp != 0) return;
   if (tid < OC1) {
-    float bsum = 0.f;
+    float bs = 0.f;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) bsum += bred[g * 32 + tid];
-    slab_bias[(size_t)blockIdx.x * OC1 + tid] = bsum;
+    for (int g = 0; g < 4 * G; ++g) bs += bred[g * OC1 + tid];
+    slab_bias[(size_t)blockIdx.x * OC1 + tid] = bs;
   }
   const size_t so = (size_t)blockIdx.x * OC1 * K1;
 #pragma unroll

@@ -235,6 +235,29 @@ def test_train_step_deterministic(dtype):
     np.testing.assert_array_equal(flats[0][1], flats[1][1])
 
 
+@pytest.mark.parametrize("env", [{"IMPALA_GRAPH": "1"}, {"IMPALA_SERIAL_STREAM": "1"}])
+def test_launch_modes_bitwise_equal(env, monkeypatch):
+    """hipGraph replay (opt-in) and the single-stream schedule give bit-identical steps to the
+    default direct launches with the weight-gradient side stream."""
+    dev = _dev()
+    batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(8, 20, 15, seed=6)]
+
+    def run():
+        m = _model(dev, "bf16", seed=0)
+        e = _engine(m, 8, 20)
+        for _ in range(3):
+            e.train_step(*batch)
+        torch.cuda.synchronize()
+        return m.flat.cpu().numpy().copy(), e.metrics.cpu().numpy().copy()
+
+    base = run()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    alt = run()
+    np.testing.assert_array_equal(base[0], alt[0])
+    np.testing.assert_array_equal(base[1], alt[1])
+
+
 def test_full_size_bf16_step_properties():
     """B=64, T=20 (BASELINE config 2): finite, loss decreases on a repeated batch,
     grad norm positive, params move by <= ~lr per step (Adam bound)."""
