@@ -145,6 +145,128 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
+// conv1 + conv2 forward, fused per frame: the frame's act1 (15x15x32) is produced into LDS and
+// consumed there by conv2 (it is also written to HBM, with its ReLU bit mask, for the backward).
+//   conv1: as conv1_fwd_s2d (weights in registers, 15 pixel tiles over the 4 waves)
+//   conv2: act2[p][oc] = relu(sum_k W2[oc][k] act1[2oy+kh][2ox+kw][ci] + b2), k = tap*32 + ci;
+//          wave w owns oc tile w (its W2 rows stay in registers), 3 tiles of 16 output pixels,
+//          B fragments are 16-byte LDS reads of the act1 tile (one tap per 32-wide k-step).
+// G 4-wave groups per workgroup take alternating frames of the workgroup's run.
+// ---------------------------------------------------------------------------------------
+template <typename T> constexpr int c12f_groups() { return sizeof(T) == 2 ? 2 : 1; }
+
+template <typename T>
+__global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
+    const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
+    const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
+    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw) {
+  using F = Frag<T>;
+  typedef typename F::vec V;
+  constexpr int KPL = F::KPL, KS = F::KSTEP;
+  constexpr int LDI = c1::L<T>::LDI;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int LDA1 = OC1 + VEC;                    // act1 tile row (elements)
+  constexpr int NKS1 = K1 / KS, NKS2 = K2 / KS;
+  constexpr int G = c12f_groups<T>();
+  constexpr int IMGSZ = c1::GRID * c1::GRID * LDI, GSZ = IMGSZ + c1::NPIX * LDA1;
+  constexpr bool W2REG = sizeof(T) == 2;             // bf16: conv2 weights in registers
+  __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
+  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  T* img = smem + grp * GSZ;
+  T* a1s = img + IMGSZ;
+  const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
+  const int kl = KPL * (lane >> 4);
+  uint4 nv[3];
+  if (f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, tid, nv);
+  V wa1[2][NKS1];  // conv1: rows oc = 16 i + (lane & 15), all of K
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int ks = 0; ks < NKS1; ++ks) wa1[i][ks] = F::load(w1 + (16 * i + (lane & 15)) * K1 + ks * KS + kl);
+  float bb1[2][4], bb2[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bb1[i][q] = b1[16 * i + 4 * (lane >> 4) + q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bb2[q] = b2[16 * wave + 4 * (lane >> 4) + q];
+  const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
+  V wa2[W2REG ? NKS2 : 1];
+  if constexpr (W2REG) {
+#pragma unroll
+    for (int ks = 0; ks < NKS2; ++ks) wa2[ks] = F::load(w2row + ks * KS);
+  }
+  const int n_it = (f1 - f0 + G - 1) / G;
+  for (int it = 0; it < n_it; ++it) {
+    const int f = f0 + G * it + grp;
+    const bool active = f < f1;
+    __syncthreads();  // the previous frame's readers of img / a1s are done
+    if (active) c1_stash_frame<T>(img, tid, nv);
+    __syncthreads();
+    if (f + G < f1) c1_load_frame<T>(x + (size_t)(f + G) * IMG, tid, nv);
+    if (active) {
+      // ---- conv1 -> act1 (HBM + LDS) and its ReLU bit mask ----
+      for (int tile = wave; tile < 15; tile += 4) {
+        const int p = min(tile * 16 + (lane & 15), c1::NPIX - 1);
+        const int base = c1_row(p, 0) * LDI;
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < NKS1; ++ks) {
+          const int k = ks * KS + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
+          const int off = ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
+          const V b = *reinterpret_cast<const V*>(img + base + off);
+          acc[0] = F::mma(wa1[0][ks], b, acc[0]);
+          acc[1] = F::mma(wa1[1][ks], b, acc[1]);
+        }
+        const int pc = tile * 16 + (lane & 15);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[q] = fmaxf(acc[i][q] * (1.f / 255.f) + bb1[i][q], 0.f);
+            bits |= (v[q] > 0.f ? 1u : 0u) << (16 * i + 4 * (lane >> 4) + q);
+          }
+          if (pc < c1::NPIX) {
+            const int oc = 16 * i + 4 * (lane >> 4);
+            store4(act1 + ((size_t)f * c1::NPIX + pc) * OC1 + oc, v);
+            store4(a1s + pc * LDA1 + oc, v);
+          }
+        }
+        bits |= __shfl_xor(bits, 16, 64);
+        bits |= __shfl_xor(bits, 32, 64);
+        if (pc < c1::NPIX && lane < 16) mask[(size_t)f * c1::NPIX + pc] = bits;
+      }
+    }
+    __syncthreads();
+    if (active) {
+      // ---- conv2 from the LDS act1 tile -> act2 ----
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) {
+        const int px = min(pt * 16 + (lane & 15), P2 - 1), oy = px / H2, ox = px - oy * H2;
+        const T* brow = a1s + ((ST2 * oy) * H1 + ST2 * ox) * LDA1 + kl;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS2; ++ks) {
+          const int k = ks * KS, tap = k >> 5, ci = k & 31;
+          const V b = *reinterpret_cast<const V*>(brow + ((tap >> 2) * H1 + (tap & 3)) * LDA1 + ci);
+          if constexpr (W2REG) acc = F::mma(wa2[ks], b, acc);
+          else acc = F::mma(F::load(w2row + ks * KS), b, acc);
+        }
+        const int pc = pt * 16 + (lane & 15);
+        if (pc < P2) {
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[q] + bb2[q], 0.f);
+          store4(act2 + ((size_t)f * P2 + pc) * OC2 + 16 * wave + 4 * (lane >> 4), v);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // conv2 input gradient + ReLU mask + conv1 weight gradient, one frame at a time, fused:
 //
 //   dY1[p][ci] = [act1 > 0] * sum_{kh,kw,oc: iy = 2 oy + kh, ix = 2 ox + kw} dY2[oy][ox][oc] W2[oc][kh][kw][ci]
@@ -160,6 +282,27 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
 // = 3 column tiles) for both 16-row oc tiles.  Each workgroup takes a contiguous run of frames
 // and writes one fp32 partial slab [32][192] (k' order) + bias sums, reduced by reduce_grads.
 // ---------------------------------------------------------------------------------------
+// lane move within rows of 16 lanes (DPP row_shr / row_shl); lanes without a source get 0
+template <int CTRL, typename V>
+DEV V dpp_move(const V& v) {
+  constexpr int NW = sizeof(V) / 4;
+  union U { V v; int w[NW]; } a, r;
+  a.v = v;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = __builtin_amdgcn_update_dpp(0, a.w[i], CTRL, 0xF, 0xF, false);
+  return r.v;
+}
+template <typename V>
+DEV V vor(const V& x, const V& y) {  // bitwise OR (one side is all-zero bits lane-wise)
+  constexpr int NW = sizeof(V) / 4;
+  union U { V v; int w[NW]; } a, b, r;
+  a.v = x;
+  b.v = y;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] | b.w[i];
+  return r.v;
+}
+
 namespace c12 {
 constexpr int QG = 9;                          // dY2 cell grid: oy = r - 1, r in [0, 9)
 constexpr int NCELL = QG * QG;
@@ -188,7 +331,6 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
   constexpr int D2V = P2 * OC2 / VEC;                 // 16-byte vectors of one dY2 frame
   constexpr int ND2 = (D2V + 255) / 256;
   constexpr int NOK = OC2 / KS;                       // k-steps per tap
-  constexpr int PFB = sizeof(T) == 2 ? 2 : 1;         // dgrad B-fragment buffers (prefetch)
   constexpr int G = c12_groups<T>();
   constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;  // elements of one group's tiles
   __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
@@ -200,28 +342,6 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
   T* d2s = dyt + DYSZ;
   uint32_t* msk = msk_all[grp];
   const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
-  // zero the dY1 padding rows 225..255 and the dY2 cell grid once (the border stays zero)
-  for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX; e += 256) dyt[c1::NPIX * LDX + e] = (T)0.f;
-  for (int e = tid; e < c12::NCELL * LD2; e += 256) d2s[e] = (T)0.f;
-  // class of this wave: output pixels iy = 2 qy + py, ix = 2 qx + px; taps kh = py + 2 j1,
-  // kw = px + 2 j2 read dY2 at (qy - j1, qx - j2)
-  const int py = wave >> 1, px = wave & 1;
-  V wa[4][2][NOK];  // [tap j1*2+j2][ci tile][k-step]: A[ci][oc] = W2[oc][kh][kw][ci]
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int ks = 0; ks < NOK; ++ks) {
-        const T* src = w2 + (size_t)(ks * KS + KPL * (lane >> 4)) * K2 + (kh * KS2 + kw) * OC1 +
-                       16 * i + (lane & 15);
-        V v;
-#pragma unroll
-        for (int j = 0; j < KPL; ++j) v[j] = src[(size_t)j * K2];
-        wa[t][i][ks] = v;
-      }
-  }
   f32x4 acc[2][3];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -241,7 +361,63 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
     }
     if (tid < c1::NPIX) nmk = mask1[(size_t)f * c1::NPIX + tid];
   };
-  if (f0 + grp < f1) fetch(f0 + grp);
+  if (f0 + grp < f1) fetch(f0 + grp);  // the first frame is in flight during the prologue
+  // class of this wave: output pixels iy = 2 qy + py, ix = 2 qx + px; taps kh = py + 2 j1,
+  // kw = px + 2 j2 read dY2 at (qy - j1, qx - j2)
+  const int py = wave >> 1, px = wave & 1;
+  V wa[4][2][NOK];  // [tap j1*2+j2][ci tile][k-step]: A[ci][oc] = W2[oc][kh][kw][ci]
+  if constexpr (sizeof(T) == 2) {
+    // bf16: W2 [64][512] staged through LDS with 16-byte loads (rows padded to 520), the
+    // fragments (k = oc along the lane's 8 values) read with the transposing LDS read
+    constexpr int LDW = K2 + VEC, NWV = OC2 * K2 / VEC, NT = 256 * G, NPT = NWV / NT;
+    static_assert(NWV % NT == 0 && OC2 * LDW <= G * GSZ, "w2 staging");
+    T* w2s = smem;
+    V wv[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = (int)threadIdx.x + i * NT;
+      wv[i] = *reinterpret_cast<const V*>(w2 + (size_t)e * VEC);
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = (int)threadIdx.x + i * NT, row = e / (K2 / VEC), c = (e % (K2 / VEC)) * VEC;
+      *reinterpret_cast<V*>(w2s + row * LDW + c) = wv[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < NOK; ++ks)
+          wa[t][i][ks] = lds_frag_k(w2s + ks * KS * LDW + (kh * KS2 + kw) * OC1 + 16 * i, LDW, lane);
+    }
+    __syncthreads();  // the staging area becomes the frame tiles
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < NOK; ++ks) {
+          const T* src = w2 + (size_t)(ks * KS + KPL * (lane >> 4)) * K2 + (kh * KS2 + kw) * OC1 +
+                         16 * i + (lane & 15);
+          V v;
+#pragma unroll
+          for (int j = 0; j < KPL; ++j) v[j] = src[(size_t)j * K2];
+          wa[t][i][ks] = v;
+        }
+    }
+  }
+  // zero the dY1 padding rows 225..255 and the dY2 cell grid once (the border stays zero)
+  static_assert((c1::NPAD - c1::NPIX) * LDX % VEC == 0 && c12::NCELL * LD2 % VEC == 0 &&
+                c1::NPIX * LDX % VEC == 0, "16-byte zero fill");
+  for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX / VEC; e += 256)
+    *reinterpret_cast<V*>(dyt + c1::NPIX * LDX + e * VEC) = F::zero();
+  for (int e = tid; e < c12::NCELL * LD2 / VEC; e += 256)
+    *reinterpret_cast<V*>(d2s + e * VEC) = F::zero();
   const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDI;
   const int kl = KPL * (lane >> 4);
   const int n_it = (f1 - f0 + G - 1) / G;
@@ -265,34 +441,39 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
     __syncthreads();
     if (f + G < f1) fetch(f + G);
     // ---- conv2 dgrad of class `wave` -> masked dY1 rows in LDS (+ conv1 bias partials) ----
+    // Only the tap-(0,0) B fragments are read from LDS (cells (qy, qx) of all 4 column tiles);
+    // the shifted taps are lane moves: the 16 lanes of a fragment row are cells qx = l & 7 of
+    // rows qy = 2 nt + ((l >> 3) & 1), so qx - 1 is a DPP row shift right by one (zero in at
+    // qx = 0: lane 7 -> 8 carries the always-zero column qx = 7) and qy - 1 is a shift by 8,
+    // taking the lower half from the previous tile.
     if (active) {
-      V bq[PFB][4 * NOK];  // B fragments of PFB consecutive 16-cell column tiles
-      auto load_b = [&](int nt, V* bb) {
+      V b0[4][NOK];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
         const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
+        const T* brow = d2s + ((qy + 1) * c12::QG + qx + 1) * LD2 + kl;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const T* brow = d2s + ((qy - (t >> 1) + 1) * c12::QG + qx - (t & 1) + 1) * LD2 + kl;
-#pragma unroll
-          for (int ks = 0; ks < NOK; ++ks) bb[t * NOK + ks] = *reinterpret_cast<const V*>(brow + ks * KS);
-        }
-      };
-      if constexpr (PFB == 2) load_b(0, bq[0]);
+        for (int ks = 0; ks < NOK; ++ks) b0[nt][ks] = *reinterpret_cast<const V*>(brow + ks * KS);
+      }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {  // 16-cell column tiles of the 8x8 class grid
-        V* cur = bq[PFB == 2 ? (nt & 1) : 0];
-        if constexpr (PFB == 2) {
-          if (nt + 1 < 4) load_b(nt + 1, bq[(nt + 1) & 1]);
-        } else {
-          load_b(nt, cur);
-        }
         f32x4 d[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int ks = 0; ks < NOK; ++ks) {
-            d[0] = F::mma(wa[t][0][ks], cur[t * NOK + ks], d[0]);
-            d[1] = F::mma(wa[t][1][ks], cur[t * NOK + ks], d[1]);
-          }
+        for (int ks = 0; ks < NOK; ++ks) {
+          const V bt0 = b0[nt][ks];
+          const V bt1 = dpp_move<0x111>(bt0);                       // (qy, qx - 1)
+          V bt2 = dpp_move<0x118>(bt0);                             // (qy - 1, qx): odd rows
+          if (nt > 0) bt2 = vor(bt2, dpp_move<0x108>(b0[nt - 1][ks]));  // even rows
+          const V bt3 = dpp_move<0x111>(bt2);                       // (qy - 1, qx - 1)
+          d[0] = F::mma(wa[0][0][ks], bt0, d[0]);
+          d[1] = F::mma(wa[0][1][ks], bt0, d[1]);
+          d[0] = F::mma(wa[1][0][ks], bt1, d[0]);
+          d[1] = F::mma(wa[1][1][ks], bt1, d[1]);
+          d[0] = F::mma(wa[2][0][ks], bt2, d[0]);
+          d[1] = F::mma(wa[2][1][ks], bt2, d[1]);
+          d[0] = F::mma(wa[3][0][ks], bt3, d[0]);
+          d[1] = F::mma(wa[3][1][ks], bt3, d[1]);
+        }
         const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
         const int iy = 2 * qy + py, ix = 2 * qx + px;
         if (iy < H1 && ix < H1) {

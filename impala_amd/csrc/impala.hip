@@ -117,6 +117,7 @@ struct impala_learner {
   bool use_side = true;
   // live launch timer: hipEvent pairs around every launch of one kernel id
   int n_cu = 256;
+  bool fwd_fused = true;       // conv1 + conv2 forward in one per-frame kernel
   int red_mode = 2;           // slab reductions: 0 all at the end, 1 per branch, 2 side + conv1
   int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
@@ -169,12 +170,20 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
-  timer_begin(h, K_CONV1_FWD, st);
-  conv1_fwd_s2d<T><<<min(n, h->n_cu * 4), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
-                                                         (T*)h->act1, h->mask1, n);
-  timer_end(h, K_CONV1_FWD, st);
-  CK_LAUNCH("conv1_fwd");
-  {
+  if (h->fwd_fused) {  // conv1 + conv2 per frame (act1 consumed from LDS)
+    const int fpw = std::max(1, cdiv(n, h->n_cu));
+    timer_begin(h, K_CONV1_FWD, st);
+    conv12_fwd_s2d<T><<<cdiv(n, fpw), 256 * c12f_groups<T>(), 0, st>>>(
+        obs, sw + sh.w1, vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
+        (T*)h->act2, n, fpw);
+    timer_end(h, K_CONV1_FWD, st);
+    CK_LAUNCH("conv12_fwd");
+  } else {
+    timer_begin(h, K_CONV1_FWD, st);
+    conv1_fwd_s2d<T><<<min(n, h->n_cu * 4), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
+                                                           (T*)h->act1, h->mask1, n);
+    timer_end(h, K_CONV1_FWD, st);
+    CK_LAUNCH("conv1_fwd");
     Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
     timer_begin(h, K_CONV2_FWD, st);
     gemm_tile<T, 64, 128, BK(64), 1, 4><<<persist_grid(h, (long)(cdiv((long)n * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
@@ -521,6 +530,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
   h->step = (int64_t*)(w + o_step);
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
+  if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default

@@ -549,8 +549,27 @@ template <typename T>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   __shared__ float red[4];
   __shared__ float sc[3];  // step_size, sqrt(bias_correction2), coef
+  // this thread's 4 parameters first: their loads overlap the norm reduction below
+  const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int n = i0 < a.cn.total ? (int)min((size_t)4, a.cn.total - i0) : 0;
+  float g[4], m[4], v[4], p[4];
+  if (n == 4) {
+    const f32x4 G = *reinterpret_cast<const f32x4*>(a.grads + i0);
+    const f32x4 M = *reinterpret_cast<const f32x4*>(a.m + i0);
+    const f32x4 Vv = *reinterpret_cast<const f32x4*>(a.v + i0);
+    const f32x4 P = *reinterpret_cast<const f32x4*>(a.params + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { g[k] = G[k]; m[k] = M[k]; v[k] = Vv[k]; p[k] = P[k]; }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = k < n;
+      g[k] = ok ? a.grads[i0 + k] : 0.f; m[k] = ok ? a.m[i0 + k] : 0.f;
+      v[k] = ok ? a.v[i0 + k] : 0.f;     p[k] = ok ? a.params[i0 + k] : 0.f;
+    }
+  }
   float s = 0.f;
-  for (int p = threadIdx.x; p < a.n_part; p += 256) s += a.sumsq_part[p];
+  for (int q = threadIdx.x; q < a.n_part; q += 256) s += a.sumsq_part[q];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -568,26 +587,9 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     }
   }
   __syncthreads();
+  if (n == 0) return;
   const float step_size = sc[0], bc2s = sc[1], gscale = a.inv_world * sc[2];
   const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
-  const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i0 >= a.cn.total) return;
-  const int n = (int)min((size_t)4, a.cn.total - i0);
-  float g[4], m[4], v[4], p[4];
-  if (n == 4) {
-    const f32x4 G = *reinterpret_cast<const f32x4*>(a.grads + i0);
-    const f32x4 M = *reinterpret_cast<const f32x4*>(a.m + i0);
-    const f32x4 Vv = *reinterpret_cast<const f32x4*>(a.v + i0);
-    const f32x4 P = *reinterpret_cast<const f32x4*>(a.params + i0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { g[k] = G[k]; m[k] = M[k]; v[k] = Vv[k]; p[k] = P[k]; }
-  } else {
-    for (int k = 0; k < 4; ++k) {
-      const bool ok = k < n;
-      g[k] = ok ? a.grads[i0 + k] : 0.f; m[k] = ok ? a.m[i0 + k] : 0.f;
-      v[k] = ok ? a.v[i0 + k] : 0.f;     p[k] = ok ? a.params[i0 + k] : 0.f;
-    }
-  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     g[k] = g[k] * gscale;

@@ -235,7 +235,8 @@ def test_train_step_deterministic(dtype):
     np.testing.assert_array_equal(flats[0][1], flats[1][1])
 
 
-@pytest.mark.parametrize("env", [{"IMPALA_GRAPH": "1"}, {"IMPALA_SERIAL_STREAM": "1"}])
+@pytest.mark.parametrize("env", [{"IMPALA_GRAPH": "1"}, {"IMPALA_SERIAL_STREAM": "1"},
+                                 {"IMPALA_FWD_FUSED": "0"}])
 def test_launch_modes_bitwise_equal(env, monkeypatch):
     """hipGraph replay (opt-in) and the single-stream schedule give bit-identical steps to the
     default direct launches with the weight-gradient side stream."""
