@@ -50,6 +50,9 @@ def kernel_work(es):
         "fc_wgrad": (2 * 256 * 1024, 256 * es + a3, 0),
         "conv3_wgrad": (2 * 16 * 64 * 576, a3 + a2, 0),
         "conv2_wgrad": (2 * 36 * 64 * 512, a2 + a1, 0),
+        # per-parameter traffic: grads, m, v, params read + written, shadow weight written
+        "adam": (0, 0, 344_496 * (8 * 4 + es)),
+        "reduce_grads": (0, 0, 0),
     }
 
 
@@ -187,7 +190,7 @@ def main():
             ms, n = eng.timer_read()
             if n:
                 probe[kname] = ms / n
-        rk = max((k for k in probe if k in work), key=probe.get)
+        rk = max((k for k in probe if k in work and work[k][0]), key=probe.get)
     torch.cuda.synchronize()
 
     eng.timer_start(rk, args.steps)

@@ -178,11 +178,52 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
   const int kl = KPL * (lane >> 4);
   uint4 nv[3];
   if (f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, tid, nv);
+  // Weights: every wave needs all of W1 and its 16 rows of W2 as MFMA fragments.  For bf16
+  // both are staged once per workgroup through LDS with coalesced 16-byte loads (76 KB per
+  // workgroup instead of 8 waves x 28 KB of fragment loads through the CU's L2 port).
   V wa1[2][NKS1];  // conv1: rows oc = 16 i + (lane & 15), all of K
+  const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
+  V wa2[W2REG ? NKS2 : 1];
+  if constexpr (W2REG) {
+    constexpr int LW1 = K1 + VEC, LW2 = K2 + VEC, NT = 256 * G;
+    constexpr int NV1 = OC1 * K1 / VEC, NV2 = OC2 * K2 / VEC;
+    static_assert(OC1 * LW1 + OC2 * LW2 <= G * GSZ, "weight staging");
+    T* w1s = smem;
+    T* w2s = smem + OC1 * LW1;
+    constexpr int NPT = (NV1 + NV2 + NT - 1) / NT;
+    V wv[NPT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NPT; ++i) {
+      const int e = (int)threadIdx.x + i * NT;
+      if (e < NV1) wv[i] = *reinterpret_cast<const V*>(w1 + (size_t)e * VEC);
+      else if (e < NV1 + NV2) wv[i] = *reinterpret_cast<const V*>(w2 + (size_t)(e - NV1) * VEC);
+    }
 #pragma unroll
-    for (int ks = 0; ks < NKS1; ++ks) wa1[i][ks] = F::load(w1 + (16 * i + (lane & 15)) * K1 + ks * KS + kl);
+    for (int i = 0; i < NPT; ++i) {
+      const int e = (int)threadIdx.x + i * NT;
+      if (e < NV1) {
+        *reinterpret_cast<V*>(w1s + (e / (K1 / VEC)) * LW1 + (e % (K1 / VEC)) * VEC) = wv[i];
+      } else if (e < NV1 + NV2) {
+        const int e2 = e - NV1;
+        *reinterpret_cast<V*>(w2s + (e2 / (K2 / VEC)) * LW2 + (e2 % (K2 / VEC)) * VEC) = wv[i];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < NKS1; ++ks)
+        wa1[i][ks] = *reinterpret_cast<const V*>(w1s + (16 * i + (lane & 15)) * LW1 + ks * KS + kl);
+#pragma unroll
+    for (int ks = 0; ks < NKS2; ++ks)
+      wa2[ks] = *reinterpret_cast<const V*>(w2s + (16 * wave + (lane & 15)) * LW2 + ks * KS + kl);
+    __syncthreads();  // the staging area becomes the frame tiles
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < NKS1; ++ks) wa1[i][ks] = F::load(w1 + (16 * i + (lane & 15)) * K1 + ks * KS + kl);
+  }
   float bb1[2][4], bb2[4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -190,12 +231,6 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
     for (int q = 0; q < 4; ++q) bb1[i][q] = b1[16 * i + 4 * (lane >> 4) + q];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bb2[q] = b2[16 * wave + 4 * (lane >> 4) + q];
-  const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
-  V wa2[W2REG ? NKS2 : 1];
-  if constexpr (W2REG) {
-#pragma unroll
-    for (int ks = 0; ks < NKS2; ++ks) wa2[ks] = F::load(w2row + ks * KS);
-  }
   const int n_it = (f1 - f0 + G - 1) / G;
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
