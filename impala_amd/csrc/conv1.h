@@ -231,6 +231,12 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
     for (int q = 0; q < 4; ++q) bb1[i][q] = b1[16 * i + 4 * (lane >> 4) + q];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bb2[q] = b2[16 * wave + 4 * (lane >> 4) + q];
+  // consume the bias loads here: waits for them placed inside the loop would (merged over the
+  // back-edge) also stall every iteration on its in-flight frame prefetch
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    asm volatile("" ::"v"(bb1[0][q]), "v"(bb1[1][q]), "v"(bb2[q]));
+  }
   const int n_it = (f1 - f0 + G - 1) / G;
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
@@ -241,7 +247,11 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
     if (f + G < f1) c1_load_frame<T>(x + (size_t)(f + G) * IMG, tid, nv);
     if (active) {
       // ---- conv1 -> act1 (HBM + LDS) and its ReLU bit mask ----
-      for (int tile = wave; tile < 15; tile += 4) {
+      // (unrolled: a loop back-edge here makes the compiler wait for the frame prefetch)
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj) {
+        const int tile = wave + 4 * tj;
+        if (tile >= 15) break;
         const int p = min(tile * 16 + (lane & 15), c1::NPIX - 1);
         const int base = c1_row(p, 0) * LDI;
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
