@@ -38,6 +38,8 @@ def kernel_work(es):
     return {
         "conv1_fwd": (2 * 225 * 32 * 192, obs + a1 + m1, 32 * 192 * es),
         "conv2_fwd": (2 * 36 * 64 * 512, a1 + a2, 64 * 512 * es),
+        "conv1_fwd_conv2_fwd": (2 * 225 * 32 * 192 + 2 * 36 * 64 * 512, obs + a1 + m1 + a2,
+                                (32 * 192 + 64 * 512) * es),
         "conv3_fwd": (2 * 16 * 64 * 576, a2 + 2 * a3 + 8, 64 * 576 * es + 2 * 1024 * 4),
         "fc_fwd": (2 * 256 * 1024, a3 + 256 * 4 + 256 * es, 256 * 1024 * es),
         "head_step": (2 * 3 * 16 * 256, 256 * es + 256 * 4 + 8 + 4 + 4 + 15 * 4 + 256 * es,
@@ -98,7 +100,7 @@ def cpu_baseline(B, T, A, seconds):
                       f"{threads} threads, {cpu}) after 2 warm-up; median step {med * 1e3:.1f} ms"}
 
 
-PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
+PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
                  "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "head_step": "head_step",
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
                  "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "fc_wgrad": "FcWgrad",

@@ -76,12 +76,12 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 
 // kernel ids for the live launch timer (impala_timer_*)
 enum KernelId {
-  K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
+  K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
   K_LN_BWD, K_CONV3_DGRAD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
   K_SUMSQ, K_ADAM, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
-    "conv1_fwd", "conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
+    "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
     "ln_bwd", "conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
     "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam"};
 
@@ -172,11 +172,11 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   const float* vv = h->vecs;
   if (h->fwd_fused) {  // conv1 + conv2 per frame (act1 consumed from LDS)
     const int fpw = std::max(1, cdiv(n, h->n_cu));
-    timer_begin(h, K_CONV1_FWD, st);
+    timer_begin(h, K_CONV12_FWD, st);
     conv12_fwd_s2d<T><<<cdiv(n, fpw), 256 * c12f_groups<T>(), 0, st>>>(
         obs, sw + sh.w1, vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
         (T*)h->act2, n, fpw);
-    timer_end(h, K_CONV1_FWD, st);
+    timer_end(h, K_CONV12_FWD, st);
     CK_LAUNCH("conv12_fwd");
   } else {
     timer_begin(h, K_CONV1_FWD, st);
