@@ -105,7 +105,7 @@ struct impala_learner {
   uint32_t* mask1;  // conv1 ReLU bit mask [N][225]
   float *lnstat, *z, *heads, *dy;
   float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
-  float *loss_part, *sumsq_part;
+  float *loss_part, *sumsq_part, *adam_sc;
   int64_t* step;
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
@@ -350,7 +350,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.params = h->params; aa.grads = h->grads; aa.m = h->exp_avg; aa.v = h->exp_avg_sq;
   aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_red_wg;
   aa.step = h->step;
-  aa.lr = dec(h->cfg.lr); aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
+  aa.sc = h->adam_sc; aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
   aa.eps = h->cfg.adam_eps; aa.max_norm = h->cfg.max_grad_norm;
   aa.inv_world = 1.f / (float)h->cfg.world_size;
   aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
@@ -500,7 +500,8 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t o_sh = take((size_t)h->sph.S * HEADS * HID * 4);
   const size_t o_sbh = take((size_t)h->sph.S * HEADS * 4);
   const size_t o_lpart = take((size_t)h->n_loss_wg * 8 * 4);
-  const size_t o_spart = take((size_t)h->n_red_wg * 4);
+  const size_t o_spart = take((size_t)(h->n_red_wg + 3) / 4 * 16);  // zero tail: float4 reads
+  const size_t o_adsc = take(2 * 4);
   const size_t o_step = take(8);
   h->ws_bytes = off;
   hipError_t e = hipMalloc(&h->ws, off);
@@ -528,6 +529,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->s_ln = (float*)(w + o_sln); h->s_fc = (float*)(w + o_sfc); h->s_bfc = (float*)(w + o_sbfc);
   h->s_h = (float*)(w + o_sh); h->s_bh = (float*)(w + o_sbh);
   h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
+  h->adam_sc = (float*)(w + o_adsc);
   h->step = (int64_t*)(w + o_step);
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
@@ -589,6 +591,8 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     ra.A = h->A;
     ra.ent_coef = cfg->entropy_coeff;
     ra.step = h->step;
+    ra.lr = dec(cfg->lr); ra.b1 = dec(cfg->adam_beta1); ra.b2 = dec(cfg->adam_beta2);
+    ra.adam_sc = h->adam_sc;
   }
   *out = h;
   return 0;

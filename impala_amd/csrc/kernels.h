@@ -416,6 +416,8 @@ struct RedArgs {
   float ent_coef;
   float* metrics;
   int64_t* step;
+  double lr, b1, b2;  // Adam bias corrections for the step this reduction completes
+  float* adam_sc;     // [2]: lr / (1 - b1^t), sqrt(1 - b2^t)
 };
 
 DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
@@ -509,9 +511,14 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
   if (threadIdx.x == 0) a.sumsq_part[wg] = red[0] + red[1] + red[2] + red[3];
-  if (fin && blockIdx.x == 0 && threadIdx.x == 64) {
+  if (fin && blockIdx.x == 0 && threadIdx.x == 64)
     finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
-    *a.step += 1;
+  if (fin && blockIdx.x == 0 && threadIdx.x == 128) {  // step += 1 and its bias corrections
+    const int64_t t = *a.step + 1;
+    *a.step = t;
+    const double bc1 = 1.0 - pow(a.b1, (double)t), bc2 = 1.0 - pow(a.b2, (double)t);
+    a.adam_sc[0] = (float)(a.lr / bc1);
+    a.adam_sc[1] = (float)sqrt(bc2);
   }
 }
 
@@ -538,18 +545,22 @@ struct AdamArgs {
   const float* sumsq_part;
   int n_part;
   const int64_t* step;
-  double lr, b1, b2;
+  const float* sc;  // [2] step size and sqrt(bias correction 2), written by reduce_grads
+  double b1, b2;
   float eps, max_norm, inv_world;
   ShadowPtrs sp;
   Canon cn;
   Shadow sh;
 };
 
+// clip + Adam on 4 consecutive parameters per thread; re-emits the kernel-layout weights.
+// (A row-wise variant that re-emits the big matrices through an LDS permutation with 16-byte
+// stores measured no faster: the scattered 2-byte shadow stores are absorbed by L2.)
 template <typename T>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   __shared__ float red[4];
-  __shared__ float sc[3];  // step_size, sqrt(bias_correction2), coef
-  // this thread's 4 parameters first: their loads overlap the norm reduction below
+  // this thread's 4 parameters, the step scalars and the norm partials are all loaded up
+  // front (one memory round trip), then one barrier combines the norm
   const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
   const int n = i0 < a.cn.total ? (int)min((size_t)4, a.cn.total - i0) : 0;
   float g[4], m[4], v[4], p[4];
@@ -568,27 +579,23 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       v[k] = ok ? a.v[i0 + k] : 0.f;     p[k] = ok ? a.params[i0 + k] : 0.f;
     }
   }
-  float s = 0.f;
-  for (int q = threadIdx.x; q < a.n_part; q += 256) s += a.sumsq_part[q];
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float tot = red[0] + red[1] + red[2] + red[3];
-    const float norm = sqrtf(tot) * a.inv_world;
-    const double stepd = (double)*a.step;
-    const double bc1 = 1.0 - pow(a.b1, stepd), bc2 = 1.0 - pow(a.b2, stepd);
-    sc[0] = (float)(a.lr / bc1);
-    sc[1] = (float)sqrt(bc2);
-    sc[2] = fminf(a.max_norm / (norm + 1e-6f), 1.f);
-    if (blockIdx.x == 0) {
-      a.metrics[6] = norm;
-      a.metrics[7] = (float)stepd;
-    }
+  const float step_size = a.sc[0], bc2s = a.sc[1];
+  float sq = 0.f;  // partials are zero-padded to a multiple of 4 (see impala_create)
+  for (int q = threadIdx.x; q * 4 < a.n_part; q += 256) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(a.sumsq_part + 4 * q);
+    sq += (x[0] + x[1]) + (x[2] + x[3]);
   }
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
+  const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]) * a.inv_world;
+  const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.f);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.metrics[6] = norm;
+    a.metrics[7] = (float)*a.step;
+  }
   if (n == 0) return;
-  const float step_size = sc[0], bc2s = sc[1], gscale = a.inv_world * sc[2];
+  const float gscale = a.inv_world * coef;
   const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
