@@ -1,0 +1,42 @@
+// LayerNorm of one frame's conv3 output (models/common.py:120-126: ReLU, then LayerNorm over
+// the 1024 = 16 pixels x 64 channels features), shared by the tiled conv3 GEMM epilogue and the
+// fused forward trunk so both produce bit-identical act3 / y / stats.
+#pragma once
+#include "common.h"
+#include "net.h"
+
+// One wavefront per frame; lane owns features 16*lane .. 16*lane+15 (pixel lane/4, channels
+// 16*(lane%4) ..).  et: fp32 conv3 accumulators of the frame, [16 px][ldt] channels-contiguous.
+// Writes act3 = relu(acc + b3), y = LN(act3) (gamma, beta in p*64+c order) and (mean, rstd).
+template <typename T>
+DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const float* b3,
+                           const float* gam, const float* bet, T* act3, T* y, float* stats) {
+  using namespace net;
+  const int p = lane >> 2, c0 = (lane & 3) * 16;
+  const float* src = et + p * ldt + c0;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = fmaxf(src[i] + b3[c0 + i], 0.f);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sum += v[i];
+  const float mean = wave_sum(sum) * (1.f / FLAT);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) q += (v[i] - mean) * (v[i] - mean);
+  const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / FLAT) + LN_EPS);
+  const size_t o = (size_t)frame * FLAT + lane * 16;
+#pragma unroll
+  for (int i = 0; i < 16; i += 4) {
+    float yy[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      yy[k] = (v[i + k] - mean) * rstd * gam[lane * 16 + i + k] + bet[lane * 16 + i + k];
+    store4(act3 + o + i, v + i);
+    store4(y + o + i, yy);
+  }
+  if (lane == 0) {
+    stats[2 * frame] = mean;
+    stats[2 * frame + 1] = rstd;
+  }
+}

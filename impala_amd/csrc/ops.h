@@ -3,6 +3,7 @@
 // (batch-major flatten of agents/impala/learning.py:143).
 #pragma once
 #include "gemm.h"
+#include "lnorm.h"
 #include "net.h"
 
 using namespace net;
@@ -164,34 +165,8 @@ template <typename T> struct Conv3LnFwd : Conv3Fwd<T> {
     const int lane = tid & 63, wave = tid >> 6;
     const int frame = cc0 / P3 + wave;
     if ((frame + 1) * P3 > this->C) return;
-    // lane owns features j = 16*lane .. 16*lane+15  (pixel p = lane/4, channels 16*(lane%4)..)
-    const int p = lane >> 2, c0 = (lane & 3) * 16;
-    const float* src = et + (wave * P3 + p) * ldt + c0;
-    float v[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = fmaxf(src[i] + this->b[c0 + i], 0.f);
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sum += v[i];
-    const float mean = wave_sum(sum) * (1.f / FLAT);
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) q += (v[i] - mean) * (v[i] - mean);
-    const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / FLAT) + LN_EPS);
-    const size_t o = (size_t)frame * FLAT + lane * 16;
-#pragma unroll
-    for (int i = 0; i < 16; i += 4) {
-      float yy[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        yy[k] = (v[i + k] - mean) * rstd * gam[lane * 16 + i + k] + bet[lane * 16 + i + k];
-      store4(this->out + o + i, v + i);
-      store4(y + o + i, yy);
-    }
-    if (lane == 0) {
-      stats[2 * frame] = mean;
-      stats[2 * frame + 1] = rstd;
-    }
+    ln_frame_epilogue<T>(et + wave * P3 * ldt, ldt, frame, lane, this->b, gam, bet, this->out, y,
+                         stats);
   }
 };
 
