@@ -69,6 +69,15 @@ template <> struct Frag<__bf16> {
   }
 };
 
+// Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.  Remap a linear
+// dispatch id so that consecutive work items (which share an operand: the row tiles of one
+// column tile, the column tiles of one split) run on the same XCD and share its L2.
+DEV int xcd_swizzle(int bid, int nb) {
+  constexpr int NXCD = 8;
+  const int x = bid % NXCD, q = nb / NXCD, r = nb % NXCD;
+  return x * q + min(x, r) + bid / NXCD;
+}
+
 template <typename T> DEV T to_t(float x) { return (T)x; }
 template <typename T> DEV float to_f(T x) { return (float)x; }
 

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   auto srow = [&](int i) { return (tid + i * 256) / KV; };
   auto skv = [&](int i) { return (tid + i * 256) % KV; };
   const int n_tiles = n_rtiles * ((op.C + BC - 1) / BC);
-  const int ft = blockIdx.x;  // first tile of this workgroup
+  const int ft = xcd_swizzle(blockIdx.x, gridDim.x);  // first tile of this workgroup
   if (ft >= n_tiles) return;
   // per-thread staging contexts of the fetch tile
   const T* arow[NA];
@@ -270,11 +270,15 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
                 "LDS reuse for the group reduction");
   __shared__ __attribute__((aligned(16))) T smem[STAGE * 2 * G];
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-  const int c0 = blockIdx.x * BC, r0 = blockIdx.y * BR, split = blockIdx.z;
+  // work item (column tile fastest) from the XCD-swizzled dispatch id
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int wid = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
+  const int bx = wid % gridDim.x, by = (wid / gridDim.x) % gridDim.y, split = wid / (gridDim.x * gridDim.y);
+  const int c0 = bx * BC, r0 = by * BR;
   const int m_beg = split * m_per_split;
   const int m_end = min(op.M, m_beg + m_per_split);
   const int wr = wave / WC, wc = wave % WC;
-  const bool do_bias = slab_bias != nullptr && blockIdx.x == 0;
+  const bool do_bias = slab_bias != nullptr && bx == 0;
   f32x4 acc[TRW][TCW];
 #pragma unroll
   for (int i = 0; i < TRW; ++i)
