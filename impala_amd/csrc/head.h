@@ -82,48 +82,69 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     r = a.rew[n];
     g = a.disc[n];
   }
-  // ---- phase 1: stage h, zero dH, heads forward ----
-  for (int e = tid; e < 64 * (HID / VEC); e += 256) {
-    const int f = e / (HID / VEC), c = (e % (HID / VEC)) * VEC;
-    V v = f < nf ? *reinterpret_cast<const V*>(hg + (f0 + f) * HID + c) : F::zero();
-    *reinterpret_cast<V*>(hs + f * LDH + c) = v;
+  // ---- every global load of the kernel is issued here, in one round trip: h rows, this
+  // workgroup's z slice, the heads weights (both orientations) and bias ----
+  constexpr int NHV = 64 * (HID / VEC) / 256, NZV = 64 * (HEAD_JC / 4) / 256;
+  constexpr int NKH = HID / F::KSTEP, NKT = HPAD / F::KSTEP;
+  const int kl = F::KPL * (lane >> 4);
+  V hv[NHV];
+  f32x4 zv[NZV];
+#pragma unroll
+  for (int i = 0; i < NHV; ++i) {
+    const int e = tid + i * 256, f = e / (HID / VEC), c = (e % (HID / VEC)) * VEC;
+    hv[i] = f < nf ? *reinterpret_cast<const V*>(hg + (f0 + f) * HID + c) : F::zero();
   }
-  for (int e = tid; e < 64 * LDD; e += 256) dHs[e] = (T)0.f;
+#pragma unroll
+  for (int i = 0; i < NZV; ++i) {
+    const int e = tid + i * 256, f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
+    zv[i] = f < nf ? *reinterpret_cast<const f32x4*>(a.z + (f0 + f) * HID + jw + c)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  V whf[NKH], wtf[NKT];
+  {
+    const T* wh = reinterpret_cast<const T*>(a.wh);
+    const T* wht = reinterpret_cast<const T*>(a.wht);
+#pragma unroll
+    for (int ks = 0; ks < NKH; ++ks) whf[ks] = F::load(wh + (lane & 15) * HID + ks * F::KSTEP + kl);
+#pragma unroll
+    for (int ks = 0; ks < NKT; ++ks)
+      wtf[ks] = F::load(wht + (jw + wave * 16 + (lane & 15)) * HPAD + ks * F::KSTEP + kl);
+  }
+  float bhv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bhv[q] = a.bh[4 * (lane >> 4) + q];
+  // ---- phase 1: stage h and z, zero dH, heads forward ----
+#pragma unroll
+  for (int i = 0; i < NHV; ++i) {
+    const int e = tid + i * 256, f = e / (HID / VEC), c = (e % (HID / VEC)) * VEC;
+    *reinterpret_cast<V*>(hs + f * LDH + c) = hv[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NZV; ++i) {
+    const int e = tid + i * 256, f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
+    *reinterpret_cast<f32x4*>(zs + f * (HEAD_JC + 4) + c) = zv[i];
+  }
+  for (int e = tid; e < 64 * LDD / VEC; e += 256) *reinterpret_cast<V*>(dHs + e * VEC) = F::zero();
   __syncthreads();
   {
-    const int kl = F::KPL * (lane >> 4);
-    const T* wh = reinterpret_cast<const T*>(a.wh);
     const int f = wave * 16 + (lane & 15);
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int k = 0; k < HID; k += F::KSTEP) {
-      const V wa = F::load(wh + (lane & 15) * HID + k + kl);
-      const V hb = *reinterpret_cast<const V*>(hs + f * LDH + k + kl);
-      acc = F::mma(wa, hb, acc);
-    }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int o = 4 * (lane >> 4) + q;
-      lg_s[f][o] = acc[q] + a.bh[o];
-    }
+    for (int ks = 0; ks < NKH; ++ks)
+      acc = F::mma(whf[ks], *reinterpret_cast<const V*>(hs + f * LDH + ks * F::KSTEP + kl), acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lg_s[f][4 * (lane >> 4) + q] = acc[q] + bhv[q];
   }
   __syncthreads();
   if (a.heads_out && lead) {
     for (int e = tid; e < nf * HEADS; e += 256)
       a.heads_out[(f0 + e / HEADS) * HEADS + e % HEADS] = lg_s[e / HEADS][e % HEADS];
   }
-  // ---- phase 2: loss head on wave 0 (one lane per (trajectory, t)); waves 1..3 stage z ----
-  if (wave != 0) {
-    for (int e = tid - 64; e < 64 * (HEAD_JC / 4); e += 192) {
-      const int f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
-      const f32x4 zv = f < nf ? *reinterpret_cast<const f32x4*>(a.z + (f0 + f) * HID + jw + c)
-                              : f32x4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f32x4*>(zs + f * (HEAD_JC + 4) + c) = zv;
-    }
-  } else {
+  // ---- phase 2: loss head on wave 0 (one lane per (trajectory, t)) ----
+  if (wave == 0) {
     const int f = fl;
     float lg[MAX_A], p[MAX_A], logp[MAX_A];
-    float H = 0.f, kl = 0.f, logpa = 0.f, rho = 0.f;
+    float H = 0.f, kld = 0.f, logpa = 0.f, rho = 0.f;
     float v = lg_s[f][VCOL];
     float m = -INFINITY, mm = -INFINITY;
 #pragma unroll
@@ -149,14 +170,14 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         p[j] *= inv_s;
         const float lmu = mu[j] - lse_mu;
         H -= p[j] * logp[j];
-        kl += p[j] * (logp[j] - lmu);
+        kld += p[j] * (logp[j] - lmu);
         if (j == act) { logpa = logp[j]; logmua = lmu; }
       } else {
         logp[j] = 0.f;
       }
     }
     rho = fast_exp(logpa - logmua);
-    if (!valid) { H = 0.f; kl = 0.f; rho = 0.f; v = 0.f; r = 0.f; g = 0.f; }
+    if (!valid) { H = 0.f; kld = 0.f; rho = 0.f; v = 0.f; r = 0.f; g = 0.f; }
     const float v_n = __shfl_down(v, 1, 64);
     const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
     const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
@@ -177,7 +198,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     }
     float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
     s0 = wave_sum(s0); s1 = wave_sum(s1);
-    const float s2 = wave_sum(H), s3 = wave_sum(kl), s4 = wave_sum(rho);
+    const float s2 = wave_sum(H), s3 = wave_sum(kld), s4 = wave_sum(rho);
     if (lane == 0 && lead) {
       float* pp = a.partials + blockIdx.x * 8;
       pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
@@ -186,22 +207,16 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   __syncthreads();
   // ---- phase 3: dz = gelu'(z) * (dH . Wh)   rows j (256: wave w -> 4 row tiles), cols f ----
   {
-    const int kl = F::KPL * (lane >> 4);
-    const T* wht = reinterpret_cast<const T*>(a.wht);
     T* dz = reinterpret_cast<T*>(a.dz);
     {
       const int j0 = jw + wave * 16;
-      V wa[HPAD / F::KSTEP];
-#pragma unroll
-      for (int ks = 0; ks < HPAD / F::KSTEP; ++ks)
-        wa[ks] = F::load(wht + (j0 + (lane & 15)) * HPAD + ks * F::KSTEP + kl);
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         const int f = ct * 16 + (lane & 15);
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < HPAD / F::KSTEP; ++ks)
-          acc = F::mma(wa[ks], *reinterpret_cast<const V*>(dHs + f * LDD + ks * F::KSTEP + kl), acc);
+          acc = F::mma(wtf[ks], *reinterpret_cast<const V*>(dHs + f * LDD + ks * F::KSTEP + kl), acc);
         if (f < nf) {
           const int j = j0 + 4 * (lane >> 4);
           const f32x4 zz = *reinterpret_cast<const f32x4*>(zs + f * (HEAD_JC + 4) + j - jw);
