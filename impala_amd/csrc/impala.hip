@@ -108,7 +108,7 @@ struct impala_learner {
   float *loss_part, *sumsq_part, *adam_sc;
   int64_t* step;
   Split sp1, sp2, sp3, spfc, sph;
-  int n_ln_wg = 0, ln_fpw = 4, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
+  int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   RedArgs red{};
   // side stream for the weight-gradient branches (fork/join with events, graph-capturable)
   hipStream_t side = nullptr;

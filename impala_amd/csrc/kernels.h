@@ -275,16 +275,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     db[i] = 0.f;
     gm[i] = gam[lane * 16 + i];
   }
-  for (int f = 0; f < fpw; ++f) {
-    const int n = (blockIdx.x * 4 + wave) * fpw + f;
-    if (n >= N) break;
-    const float mean = stats[2 * n], rstd = stats[2 * n + 1];
-    float xv[16], d[16], xh[16];
+  // the next frame's x / dy / stats are loaded while the current one is computed
+  const int nb = (blockIdx.x * 4 + wave) * fpw;
+  const int nf = max(0, min(fpw, N - nb));
+  float xn[16], dn[16], mn = 0.f, rn = 0.f;
+  auto fetch = [&](int n) {
 #pragma unroll
     for (int i = 0; i < 16; i += 4) {
-      load4(x + (size_t)n * FLAT + lane * 16 + i, xv + i);
-      load4(dy + (size_t)n * FLAT + lane * 16 + i, d + i);
+      load4(x + (size_t)n * FLAT + lane * 16 + i, xn + i);
+      load4(dy + (size_t)n * FLAT + lane * 16 + i, dn + i);
     }
+    mn = stats[2 * n];
+    rn = stats[2 * n + 1];
+  };
+  if (nf > 0) fetch(nb);
+  for (int f = 0; f < nf; ++f) {
+    const int n = nb + f;
+    float xv[16], d[16], xh[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { xv[i] = xn[i]; d[i] = dn[i]; }
+    const float mean = mn, rstd = rn;
+    if (f + 1 < nf) fetch(n + 1);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
