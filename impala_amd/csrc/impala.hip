@@ -196,7 +196,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     op.out = (T*)h->act3; op.gam = vv + Vecs::lng; op.bet = vv + Vecs::lnb; op.y = (T*)h->y;
     op.stats = h->lnstat;
     timer_begin(h, K_CONV3_FWD, st);
-    gemm_tile<T, 64, 64, BK(64), 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
+    gemm_tile<T, 64, 64, BK(96), 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_FWD, st);
     CK_LAUNCH("conv3_fwd");
   }
