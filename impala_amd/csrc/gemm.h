@@ -78,6 +78,17 @@ DEV Frag<float>::vec lds_frag_k(const float* tile, int ld, int lane) {
   return f32x4{a0[0], a0[ld], a0[2 * ld], a0[3 * ld]};
 }
 
+// epilogue operand types of a gemm_tile op: per-tile Epi for store(), or per-workgroup
+// EpiConst for a TILE_EPI tile_epilogue()
+template <class Op, bool TE = Op::TILE_EPI> struct EpiTypes {
+  typedef typename Op::Epi Epi;
+  struct EpiConst {};
+};
+template <class Op> struct EpiTypes<Op, true> {
+  struct Epi {};
+  typedef typename Op::EpiConst EpiConst;
+};
+
 // LDS-staged, persistent tile GEMM for the same operand definitions as gemm_rc:
 //   D[r][c] = sum_k A[r][k] * B(c, k),  WG tile BR x BC, K chunk BK.
 // A persistent grid walks the (row-tile, col-tile) list; every K chunk of A (weights) and B
@@ -165,8 +176,20 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   const int kl = F::KPL * (lane >> 4);
   set_ctx(ft);
   fetch(0);
+  [[maybe_unused]] typename EpiTypes<Op>::EpiConst econst{};
+  if constexpr (Op::TILE_EPI) econst = op.epi_const(tid);
   for (int t = ft; t < n_tiles; t += gridDim.x) {
     const int cr0 = fr0, cc0 = fc0;  // coordinates of tile t (the fetch cursor is on it)
+    // the epilogue's global reads, issued now so they land under the K loop
+    [[maybe_unused]] typename EpiTypes<Op>::Epi ep[TRW][TCW];
+    if constexpr (!Op::TILE_EPI) {
+#pragma unroll
+      for (int j = 0; j < TCW; ++j)
+#pragma unroll
+        for (int i = 0; i < TRW; ++i)
+          ep[i][j] = op.epi(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4),
+                            min(cc0 + (wc * TCW + j) * 16 + (lane & 15), op.C - 1));
+    }
     f32x4 acc[TRW][TCW];
 #pragma unroll
     for (int i = 0; i < TRW; ++i)
@@ -218,7 +241,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
           *reinterpret_cast<f32x4*>(et + cl * (BR + 4) + rl0) = acc[i][j];
         }
       __syncthreads();
-      op.tile_epilogue(et, BR + 4, cr0, cc0, tid);
+      op.tile_epilogue(et, BR + 4, cr0, cc0, tid, econst);
       __syncthreads();  // the next tile's stash reuses the LDS
     } else {
       if constexpr (NK % 2 == 1) __syncthreads();  // next tile reuses buffer 0 first
@@ -229,7 +252,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
 #pragma unroll
           for (int i = 0; i < TRW; ++i) {
             float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);
+            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v, ep[i][j]);
           }
         }
       }

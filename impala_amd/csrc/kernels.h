@@ -216,47 +216,6 @@ __global__ void finalize_loss_kernel(const float* part, int nparts, int B, int T
   if (threadIdx.x == 0) finalize_loss_metrics(part, nparts, B, T, ent_coef, metrics);
 }
 
-// =========================================================================================
-// LayerNorm(1024, eps 1e-5) over the flattened conv features (models/models.py:66), one wave
-// per frame, 16 contiguous features per lane.  Features are in (p*64 + c) order; gamma/beta
-// are stored permuted to match.
-// =========================================================================================
-template <typename T>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x,
-                                                     const float* __restrict__ gam,
-                                                     const float* __restrict__ bet,
-                                                     T* __restrict__ y, float* __restrict__ stats,
-                                                     int N) {
-  const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n >= N) return;
-  const T* xr = x + (size_t)n * FLAT + lane * 16;
-  float v[16];
-#pragma unroll
-  for (int i = 0; i < 16; i += 4) load4(xr + i, v + i);
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s += v[i];
-  const float mean = wave_sum(s) * (1.f / FLAT);
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) q += (v[i] - mean) * (v[i] - mean);
-  const float var = wave_sum(q) * (1.f / FLAT);
-  const float rstd = 1.f / sqrtf(var + LN_EPS);
-  T* yr = y + (size_t)n * FLAT + lane * 16;
-#pragma unroll
-  for (int i = 0; i < 16; i += 4) {
-    float o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      o[k] = (v[i + k] - mean) * rstd * gam[lane * 16 + i + k] + bet[lane * 16 + i + k];
-    store4(yr + i, o);
-  }
-  if (lane == 0) {
-    stats[2 * n] = mean;
-    stats[2 * n + 1] = rstd;
-  }
-}
 
 // LayerNorm backward + conv3 ReLU mask; per-workgroup partials of d gamma, d beta.
 template <typename T>

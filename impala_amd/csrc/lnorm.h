@@ -5,18 +5,34 @@
 #include "common.h"
 #include "net.h"
 
-// One wavefront per frame; lane owns features 16*lane .. 16*lane+15 (pixel lane/4, channels
-// 16*(lane%4) ..).  et: fp32 conv3 accumulators of the frame, [16 px][ldt] channels-contiguous.
-// Writes act3 = relu(acc + b3), y = LN(act3) (gamma, beta in p*64+c order) and (mean, rstd).
+// The per-lane constants of the epilogue (lane owns features 16*lane .. 16*lane+15: pixel
+// lane/4, channels 16*(lane%4) ..): conv3 bias, LayerNorm gamma / beta (p*64+c order).
+struct LnLane {
+  float b[16], g[16], e[16];
+};
+DEV LnLane ln_lane_consts(int lane, const float* b3, const float* gam, const float* bet) {
+  LnLane c;
+  const int c0 = (lane & 3) * 16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    c.b[i] = b3[c0 + i];
+    c.g[i] = gam[lane * 16 + i];
+    c.e[i] = bet[lane * 16 + i];
+  }
+  return c;
+}
+
+// One wavefront per frame.  et: fp32 conv3 accumulators of the frame, [16 px][ldt]
+// channels-contiguous.  Writes act3 = relu(acc + b3), y = LN(act3) and (mean, rstd).
 template <typename T>
-DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const float* b3,
-                           const float* gam, const float* bet, T* act3, T* y, float* stats) {
+DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const LnLane& k,
+                           T* act3, T* y, float* stats) {
   using namespace net;
   const int p = lane >> 2, c0 = (lane & 3) * 16;
   const float* src = et + p * ldt + c0;
   float v[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = fmaxf(src[i] + b3[c0 + i], 0.f);
+  for (int i = 0; i < 16; ++i) v[i] = fmaxf(src[i] + k.b[i], 0.f);
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) sum += v[i];
@@ -30,8 +46,8 @@ DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const 
   for (int i = 0; i < 16; i += 4) {
     float yy[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      yy[k] = (v[i + k] - mean) * rstd * gam[lane * 16 + i + k] + bet[lane * 16 + i + k];
+    for (int q = 0; q < 4; ++q)
+      yy[q] = (v[i + q] - mean) * rstd * k.g[i + q] + k.e[i + q];
     store4(act3 + o + i, v + i);
     store4(y + o + i, yy);
   }

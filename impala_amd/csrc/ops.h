@@ -1,4 +1,7 @@
-// Operand definitions plugged into gemm_rc / gemm_wg for each layer of the step.
+// Operand definitions plugged into gemm_rc / gemm_tile / gemm_wg for each layer of the step.
+// Output-side ops of gemm_tile split their epilogue into epi(r, c) -- the epilogue's own global
+// reads (bias, ReLU mask), issued at the start of the tile so they land under the K loop -- and
+// store(r, c, v, e).
 // Activations are channels-last (pixel-major, channel-contiguous); frame n = b*T + t
 // (batch-major flatten of agents/impala/learning.py:143).
 #pragma once
@@ -7,43 +10,6 @@
 #include "net.h"
 
 using namespace net;
-
-// ------------------------------- forward ------------------------------------------------
-// conv1: rows oc (32), cols pixel (n, oh, ow) in N*225, k = ci*64 + kh*8 + kw over u8 NCHW
-// input (the x/255 of models/models.py:73 is folded into the epilogue: raw bytes are exact
-// in bf16).  Epilogue: *1/255 + bias, ReLU -> act1[n][oh][ow][oc].
-template <typename T> struct Conv1Fwd {
-  static constexpr bool A_KMAJOR = false;
-  static constexpr bool TILE_EPI = false;
-  static constexpr int K = K1;
-  int C;
-  const T* w;
-  const float* b;
-  const uint8_t* x;
-  T* out;
-  struct ColCtx { const uint8_t* p; };
-  DEV ColCtx col_ctx(int c) const {
-    const int n = c / P1, p = c - n * P1, oh = p / H1, ow = p - oh * H1;
-    return ColCtx{x + (size_t)n * IMG + (ST1 * oh) * H0 + ST1 * ow};
-  }
-  DEV const T* a_row(int r, int) const { return w + r * K; }
-  DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const {
-    const int ci = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
-    const uint8_t* p = cc.p + ci * (H0 * H0) + kh * H0 + kw;
-    if constexpr (sizeof(T) == 4) {
-      return Frag<float>::from_u8(*reinterpret_cast<const uint32_t*>(p));
-    } else {
-      return Frag<__bf16>::from_u8_2(*reinterpret_cast<const uint32_t*>(p),
-                                     *reinterpret_cast<const uint32_t*>(p + 4));
-    }
-  }
-  DEV void store(int r, int c, float v[4]) const {
-    float o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = fmaxf(v[i] * (1.f / 255.f) + b[r + i], 0.f);
-    store4(out + (size_t)c * OC1 + r, o);
-  }
-};
 
 // conv2: rows oc (64), cols (n, oh, ow) in N*36, k = (kh*4+kw)*32 + ci over act1.
 template <typename T> struct Conv2Fwd {
@@ -65,10 +31,12 @@ template <typename T> struct Conv2Fwd {
     const int tap = k >> 5, ci = k & 31, kh = tap >> 2, kw = tap & 3;
     return Frag<T>::load(cc.p + (kh * H1 + kw) * OC1 + ci);
   }
-  DEV void store(int r, int c, float v[4]) const {
+  struct Epi { float b[4]; };
+  DEV Epi epi(int r, int) const { return Epi{{b[r], b[r + 1], b[r + 2], b[r + 3]}}; }
+  DEV void store(int r, int c, float v[4], const Epi& e) const {
     float o[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = fmaxf(v[i] + b[r + i], 0.f);
+    for (int i = 0; i < 4; ++i) o[i] = fmaxf(v[i] + e.b[i], 0.f);
     store4(out + (size_t)c * OC2 + r, o);
   }
 };
@@ -94,10 +62,12 @@ template <typename T> struct Conv3Fwd {
     const int tap = k >> 6, ci = k & 63, kh = tap / 3, kw = tap - kh * 3;
     return Frag<T>::load(cc.p + (kh * H2 + kw) * OC2 + ci);
   }
-  DEV void store(int r, int c, float v[4]) const {
+  struct Epi { float b[4]; };
+  DEV Epi epi(int r, int) const { return Epi{{b[r], b[r + 1], b[r + 2], b[r + 3]}}; }
+  DEV void store(int r, int c, float v[4], const Epi& e) const {
     float o[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = fmaxf(v[i] + b[r + i], 0.f);
+    for (int i = 0; i < 4; ++i) o[i] = fmaxf(v[i] + e.b[i], 0.f);
     store4(out + (size_t)c * OC3 + r, o);
   }
 };
@@ -118,11 +88,13 @@ template <typename T> struct FcFwd {
   DEV ColCtx col_ctx(int c) const { return ColCtx{y + (size_t)c * FLAT}; }
   DEV const T* a_row(int r, int) const { return w + r * K; }
   DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const { return Frag<T>::load(cc.p + k); }
-  DEV void store(int r, int c, float v[4]) const {
+  struct Epi { float b[4]; };
+  DEV Epi epi(int r, int) const { return Epi{{b[r], b[r + 1], b[r + 2], b[r + 3]}}; }
+  DEV void store(int r, int c, float v[4], const Epi& e) const {
     float zz[4], hh[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      zz[i] = v[i] + b[r + i];
+      zz[i] = v[i] + e.b[i];
       hh[i] = gelu_f(zz[i]);
     }
     store4(z + (size_t)c * HID + r, zz);
@@ -161,89 +133,14 @@ template <typename T> struct Conv3LnFwd : Conv3Fwd<T> {
   const float* bet;
   T* y;
   float* stats;
-  DEV void tile_epilogue(const float* et, int ldt, int, int cc0, int tid) const {
+  typedef LnLane EpiConst;  // loaded once per workgroup (gemm_tile)
+  DEV EpiConst epi_const(int tid) const { return ln_lane_consts(tid & 63, this->b, gam, bet); }
+  DEV void tile_epilogue(const float* et, int ldt, int, int cc0, int tid,
+                         const EpiConst& k) const {
     const int lane = tid & 63, wave = tid >> 6;
     const int frame = cc0 / P3 + wave;
     if ((frame + 1) * P3 > this->C) return;
-    ln_frame_epilogue<T>(et + wave * P3 * ldt, ldt, frame, lane, this->b, gam, bet, this->out, y,
-                         stats);
-  }
-};
-
-// projection Linear + GELU + actor/critic heads fused: a 256(o) x 32(frame) tile holds whole
-// h rows; the heads (16 x 256) are applied from LDS in the epilogue (wave 0..1: 16 frames each).
-template <typename T> struct FcHeadsFwd : FcFwd<T> {
-  static constexpr bool TILE_EPI = true;
-  const T* wh;       // [16][256]
-  const float* bh;   // [16]
-  float* heads;      // [n][16]
-  DEV void tile_epilogue(const float* et, int ldt, int, int cc0, int tid) const {
-    // 1) z = acc + b, h = gelu(z): write z, h to HBM, h (fp32) back into the LDS tile
-    float* etw = const_cast<float*>(et);
-    for (int e = tid; e < 32 * (HID / 4); e += 256) {
-      const int f = e / (HID / 4), r = (e % (HID / 4)) * 4;
-      const int c = cc0 + f;
-      float zz[4], hh[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        zz[k] = et[f * ldt + r + k] + this->b[r + k];
-        hh[k] = gelu_f(zz[k]);
-      }
-      if (c < this->C) {
-        store4(this->z + (size_t)c * HID + r, zz);
-        store4(this->h + (size_t)c * HID + r, hh);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) etw[f * ldt + r + k] = (float)(T)hh[k];  // as stored (T)
-    }
-    __syncthreads();
-    // 2) heads: out[f][o'] = sum_j wh[o'][j] h[f][j] + bh[o'], one 16x16 tile per wave 0..1
-    const int lane = tid & 63, wave = tid >> 6;
-    if (wave < 2) {
-      using F = Frag<T>;
-      const int kl = F::KPL * (lane >> 4);
-      const int f = wave * 16 + (lane & 15);
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int k = 0; k < HID; k += F::KSTEP) {
-        const typename F::vec a = F::load(wh + (lane & 15) * HID + k + kl);
-        typename F::vec bv;
-#pragma unroll
-        for (int q = 0; q < F::KPL; ++q) bv[q] = (T)et[f * ldt + k + kl + q];
-        acc = F::mma(a, bv, acc);
-      }
-      const int c = cc0 + f;
-      if (c < this->C) {
-        float o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = acc[q] + bh[4 * (lane >> 4) + q];
-        store4(heads + (size_t)c * HEADS + 4 * (lane >> 4), o);
-      }
-    }
-  }
-};
-
-// ------------------------------- backward (dgrad) ---------------------------------------
-// dh = dH . Wh  then GELU backward:  dz[n][j] = dh[n][j] * gelu'(z[n][j]).  K = 32 (padded).
-template <typename T> struct HeadsDgrad {
-  static constexpr bool A_KMAJOR = false;
-  static constexpr bool TILE_EPI = false;
-  static constexpr int K = HPAD;
-  int C;
-  const T* wt;  // [256][32]
-  const T* dH;  // [n][32]
-  const float* z;
-  T* dz;
-  struct ColCtx { const T* p; };
-  DEV ColCtx col_ctx(int c) const { return ColCtx{dH + (size_t)c * HPAD}; }
-  DEV const T* a_row(int r, int) const { return wt + r * K; }
-  DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const { return Frag<T>::load(cc.p + k); }
-  DEV void store(int r, int c, float v[4]) const {
-    float zz[4], o[4];
-    load4(z + (size_t)c * HID + r, zz);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = v[i] * gelu_grad(zz[i]);
-    store4(dz + (size_t)c * HID + r, o);
+    ln_frame_epilogue<T>(et + wave * P3 * ldt, ldt, frame, lane, k, this->out, y, stats);
   }
 };
 
@@ -262,7 +159,9 @@ template <typename T> struct FcDgrad {
   DEV const T* a_row(int, int) const { return nullptr; }
   DEV const T* a_kptr(int k, int r, int) const { return w + (size_t)k * FLAT + r; }
   DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const { return Frag<T>::load(cc.p + k); }
-  DEV void store(int r, int c, float v[4]) const { store4(dy + (size_t)c * FLAT + r, v); }
+  struct Epi {};
+  DEV Epi epi(int, int) const { return Epi{}; }
+  DEV void store(int r, int c, float v[4], const Epi&) const { store4(dy + (size_t)c * FLAT + r, v); }
 };
 
 // conv3 dgrad (gather form): rows ci (64), cols input pixel (n, iy, ix) in N*36,
@@ -293,79 +192,20 @@ template <typename T> struct Conv3Dgrad {
     if (oy < 0 || oy >= H3 || ox < 0 || ox >= H3) return Frag<T>::zero();
     return Frag<T>::load(cc.p + (oy * H3 + ox) * OC3 + oc);
   }
-  DEV void store(int r, int c, float v[4]) const {
-    float a[4], o[4];
-    load4(act + (size_t)c * OC2 + r, a);
+  struct Epi { float a[4]; };  // act2 at the output position (conv2's ReLU mask)
+  DEV Epi epi(int r, int c) const {
+    Epi e;
+    load4(act + (size_t)c * OC2 + r, e.a);
+    return e;
+  }
+  DEV void store(int r, int c, float v[4], const Epi& e) const {
+    float o[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = a[i] > 0.f ? v[i] : 0.f;
+    for (int i = 0; i < 4; ++i) o[i] = e.a[i] > 0.f ? v[i] : 0.f;
     store4(dx + (size_t)c * OC2 + r, o);
   }
 };
 
-// conv2 dgrad by stride-parity class (sub-pixel decomposition, no zero taps inside):
-// cols = cls*NC + n*64 + iy'*8 + ix'  with ih = 2*iy' + py, iw = 2*ix' + px, cls = py*2+px;
-// NC = N*64 rounded up to the tile width so no tile straddles two classes (columns
-// q >= N*64 of a class are padding); rows ci (32); k = (j1*2+j2)*64 + oc with
-// kh = py + 2*j1, kw = px + 2*j2, oh = iy' - j1.
-// Epilogue applies conv1's ReLU mask (act1 > 0); ih/iw == 15 are outside the 15x15 map.
-template <typename T> struct Conv2Dgrad {
-  static constexpr bool A_KMAJOR = true;
-  static constexpr bool TILE_EPI = false;
-  static constexpr int K = 4 * OC2;
-  int C;        // 4 * NC
-  int NC;       // columns per class (multiple of the tile width)
-  int NQ;       // valid columns per class = N * 64
-  const T* w;   // w2 [64 oc][512 = (kh*4+kw)*32 + ci]; A[ci][t*64 + oc] read k-major
-  const T* dy;  // dact2 [n][36][64]
-  const T* act; // act1 (mask)
-  T* dx;        // dact1
-  struct ColCtx { const T* p; int iy, ix; };
-  DEV ColCtx col_ctx(int c) const {
-    const int cl = c / NC, q = min(c - cl * NC, NQ - 1), n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
-    return ColCtx{dy + (size_t)n * P2 * OC2, iy, ix};
-  }
-  DEV const T* a_row(int, int) const { return nullptr; }
-  DEV const T* a_kptr(int k, int r, int cw) const {
-    const int cl = cw / NC, t = k >> 6, oc = k & 63;
-    const int kh = (cl >> 1) + 2 * (t >> 1), kw = (cl & 1) + 2 * (t & 1);
-    return w + (size_t)oc * K2 + (kh * KS2 + kw) * OC1 + r;
-  }
-  DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const {
-    const int t = k >> 6, oc = k & 63, j1 = t >> 1, j2 = t & 1;
-    const int oy = cc.iy - j1, ox = cc.ix - j2;
-    if (oy < 0 || oy >= H2 || ox < 0 || ox >= H2) return Frag<T>::zero();
-    return Frag<T>::load(cc.p + (oy * H2 + ox) * OC2 + oc);
-  }
-  DEV void store(int r, int c, float v[4]) const {
-    const int cl = c / NC, q = c - cl * NC;
-    if (q >= NQ) return;
-    const int n = q >> 6, iy = (q >> 3) & 7, ix = q & 7;
-    const int ih = 2 * iy + (cl >> 1), iw = 2 * ix + (cl & 1);
-    if (ih >= H1 || iw >= H1) return;
-    const size_t o = ((size_t)(n * H1 + ih) * H1 + iw) * OC1 + r;
-    float a[4], out[4];
-    load4(act + o, a);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = a[i] > 0.f ? v[i] : 0.f;
-    store4(dx + o, out);
-  }
-};
-
-// ------------------------------- backward (wgrad) ---------------------------------------
-// D[r][c] = sum_m X[m][r] * Y(m, c); X row-major [M][x_ld]; load_y returns 16 bytes of T
-// (VEC consecutive c of one run: channels for conv2/3/FC/heads, kw for conv1).
-template <typename T> struct HeadsWgrad {  // dWh[o'][j] = sum_n dH[n][o'] h[n][j]
-  static constexpr int R = HEADS, C = HID;
-  int M;
-  float out_scale = 1.f;
-  const T* x;  // dH [n][32]
-  int x_ld = HPAD;
-  const T* h;
-  DEV const T* y_row(int m) const { return h + (size_t)m * HID; }
-  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
-    return *reinterpret_cast<const typename Frag<T>::vec*>(row + c);
-  }
-};
 template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
   static constexpr int R = HID, C = FLAT;
   int M;
@@ -408,27 +248,5 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
   DEV typename Frag<T>::vec load_y(const T* row, int c) const {
     const int tap = c >> 5, ci = c & 31, kh = tap >> 2, kw = tap & 3;
     return *reinterpret_cast<const typename Frag<T>::vec*>(row + (kh * H1 + kw) * OC1 + ci);
-  }
-};
-template <typename T> struct Conv1Wgrad {  // m = (n, oy, ox) in N*225; c = ci*64 + kh*8 + kw
-  static constexpr int R = OC1, C = K1;
-  int M;
-  float out_scale = 1.f / 255.f;
-  const T* x;  // dact1
-  int x_ld = OC1;
-  const uint8_t* img;
-  DEV const uint8_t* y_row(int m) const {
-    const int n = m / P1, p = m - n * P1, oy = p / H1, ox = p - oy * H1;
-    return img + (size_t)n * IMG + (ST1 * oy) * H0 + ST1 * ox;
-  }
-  DEV typename Frag<T>::vec load_y(const uint8_t* row, int c) const {
-    const int ci = c >> 6, kh = (c >> 3) & 7, kw = c & 7;
-    const uint8_t* q = row + ci * (H0 * H0) + kh * H0 + kw;
-    if constexpr (sizeof(T) == 4) {
-      return Frag<float>::from_u8(*reinterpret_cast<const uint32_t*>(q));
-    } else {
-      return Frag<__bf16>::from_u8_2(*reinterpret_cast<const uint32_t*>(q),
-                                     *reinterpret_cast<const uint32_t*>(q + 4));
-    }
   }
 };
