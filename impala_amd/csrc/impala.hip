@@ -18,6 +18,7 @@
 #include "../../include/impala_hip.h"
 #include "head.h"
 #include "kernels.h"
+#include "lnc3.h"
 #include "ops.h"
 
 namespace {
@@ -77,12 +78,12 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 // kernel ids for the live launch timer (impala_timer_*)
 enum KernelId {
   K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
-  K_LN_BWD, K_CONV3_DGRAD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
+  K_LN_BWD, K_CONV3_DGRAD, K_LNC3_BWD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
   K_SUMSQ, K_ADAM, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
-    "ln_bwd", "conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
+    "ln_bwd", "conv3_dgrad", "ln_bwd_conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
     "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam"};
 
 struct impala_learner {
@@ -117,8 +118,9 @@ struct impala_learner {
   bool use_side = true;
   // live launch timer: hipEvent pairs around every launch of one kernel id
   int n_cu = 256;
+  bool lnc3_fused = true;      // LayerNorm backward + conv3 dgrad in one per-frame kernel
   bool fwd_fused = true;       // conv1 + conv2 forward in one per-frame kernel
-  int red_mode = 2;           // slab reductions: 0 all at the end, 1 per branch, 2 side + conv1
+  int red_mode = 0;           // slab reductions: 0 all at the end, 1 per branch, 2 side + conv1
   int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
   hipEvent_t* timer_ev = nullptr;
@@ -280,12 +282,21 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     timer_end(h, K_FC_DGRAD, st);
     CK_LAUNCH("fc_dgrad");
   }
-  timer_begin(h, K_LN_BWD, st);
-  ln_bwd_kernel<T><<<h->n_ln_wg, 256, 0, st>>>(h->dy, (const T*)h->act3, h->lnstat,
-                                                h->vecs + Vecs::lng, (T*)h->dact3, h->s_ln, N,
-                                                h->ln_fpw);
-  timer_end(h, K_LN_BWD, st);
-  CK_LAUNCH("ln_bwd");
+  if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
+    timer_begin(h, K_LNC3_BWD, st);
+    lnc3_bwd<T><<<h->n_ln_wg, 256 * lnc3_groups<T>(), 0, st>>>(
+        h->dy, (const T*)h->act3, h->lnstat, h->vecs + Vecs::lng, sw + sh.w3,
+        (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, N, h->ln_fpw);
+    timer_end(h, K_LNC3_BWD, st);
+    CK_LAUNCH("ln_bwd_conv3_dgrad");
+  } else {
+    timer_begin(h, K_LN_BWD, st);
+    ln_bwd_kernel<T><<<h->n_ln_wg, 256, 0, st>>>(h->dy, (const T*)h->act3, h->lnstat,
+                                                  h->vecs + Vecs::lng, (T*)h->dact3, h->s_ln, N,
+                                                  h->ln_fpw);
+    timer_end(h, K_LN_BWD, st);
+    CK_LAUNCH("ln_bwd");
+  }
   if (int r = fork(2)) return r;  // dact3 ready
   {
     Conv3Wgrad<T> op{};
@@ -298,7 +309,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     if (h->red_mode == 1)
       if (int r = reduce_segments(h, RS_CONV3, RS_FC, ss, 0)) return r;  // conv3 + LayerNorm
   }
-  {
+  if (!h->lnc3_fused) {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
     timer_begin(h, K_CONV3_DGRAD, st);
     gemm_tile<T, 64, 128, BK(64), 1, 4><<<persist_grid(h, (long)(cdiv((long)N * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
@@ -452,7 +463,13 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t es = h->bf16 ? 2 : 4;
   h->S_seg = next_pow2(cfg->rollout_length);
   h->n_loss_wg = cdiv(cfg->batch_size, 64 / h->S_seg);  // fused head: 64/S trajectories per WG
-  h->n_ln_wg = cdiv(N, 4 * h->ln_fpw);
+  if (const char* lf = std::getenv("IMPALA_LNC3_FUSED")) h->lnc3_fused = lf[0] != '0';
+  if (h->lnc3_fused) {  // frames per workgroup of the fused kernel (one slab each)
+    h->ln_fpw = std::max(1, cdiv(N, h->n_cu));
+    h->n_ln_wg = cdiv(N, h->ln_fpw);
+  } else {
+    h->n_ln_wg = cdiv(N, 4 * h->ln_fpw);
+  }
 
   // upper bound on the reduce workgroups (each segment: count/4 float4 columns, >= 16 per WG)
   h->n_red_wg = 11 + (OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT + HID * FLAT +
@@ -541,8 +558,11 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     impala_destroy(h);
     return fail(IMPALA_E_STATE, "hipStreamCreate (capture stream) failed");
   }
-  const char* serial = std::getenv("IMPALA_SERIAL_STREAM");  // profiling: one stream only
-  if (serial && serial[0] == '1') {
+  // The weight-gradient branches may run on a side stream (IMPALA_SIDE_STREAM=1).  Measured on
+  // MI355X the kernels do not overlap usefully and the fork / join costs more than it hides
+  // (DESIGN.md §7), so one stream is the default.
+  const char* side = std::getenv("IMPALA_SIDE_STREAM");
+  if (!side || side[0] != '1') {
     h->use_side = false;
   } else if (hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess) {
     h->use_side = false;

@@ -1,0 +1,192 @@
+// LayerNorm backward + conv3 ReLU mask + conv3 input gradient + conv2 ReLU mask, fused per
+// frame (the backward of models/models.py:66 LayerNorm and models/common.py:117-118 conv3).
+//
+//   dact3 = relu'(act3) * LN_bwd(dy)                  (dy from the FC dgrad, fp32)
+//   dact2[iy][ix][ci] = relu'(act2) * sum_{kh,kw,oc} dact3[iy-kh][ix-kw][oc] W3[oc][kh][kw][ci]
+//
+// One frame per 4-wave group at a time, G groups per workgroup on alternating frames:
+//   LN: wave w owns features 256 w .. 256 w + 255 (lane: 4 consecutive), the two per-frame
+//       sums are combined through LDS; dact3 goes to HBM (for the conv3 weight gradient) and to
+//       a zero-bordered 8x8 cell grid in LDS, so the conv3 dgrad gather needs no bounds tests
+//   dgrad: wave w owns ci tile w (its W3 fragments, k-major through the LDS transpose read, in
+//       registers), 3 tiles of 16 input pixels, K = 9 taps x 64 oc
+// LN gamma / beta gradient partials are kept per lane and written as one fp32 slab per
+// workgroup (fixed-order combine of the groups), reduced by reduce_grads like the others.
+#pragma once
+#include "gemm.h"
+#include "net.h"
+
+using namespace net;
+
+namespace lc3 {
+constexpr int QG = 8;  // dact3 cell grid: oy = r - 2, r in [0, 8)
+}
+
+template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 1; }
+
+template <typename T>
+__global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
+    const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
+    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ act2,
+    T* __restrict__ dact3, T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw) {
+  using F = Frag<T>;
+  typedef typename F::vec V;
+  constexpr int KPL = F::KPL, KS = F::KSTEP;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int LD3 = OC3 + VEC;                     // dact3 cell row (elements)
+  constexpr int LW = K3 + VEC;                       // staged W3 row
+  constexpr int NKS = K3 / KS;
+  constexpr int G = lnc3_groups<T>();
+  constexpr int GSZ = lc3::QG * lc3::QG * LD3;       // one group's cell grid
+  constexpr bool REG = sizeof(T) == 2;               // bf16: W3 fragments in registers
+  constexpr int SMEM = (REG && OC3 * LW > G * GSZ) ? OC3 * LW : G * GSZ;
+  __shared__ __attribute__((aligned(16))) T smem[SMEM];
+  __shared__ float red[G][4][2];
+  __shared__ float comb[2 * FLAT];
+  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  T* d3g = smem + grp * GSZ;
+  const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
+  const int kl = KPL * (lane >> 4);
+  // this lane's LN features j = 256 w + 4 lane + q  (pixel p = j / 64, channel c = j % 64)
+  const int j0 = 256 * wave + 4 * lane, p0 = j0 >> 6, c0 = j0 & 63;
+  // conv3 dgrad: ci tile = wave, 3 tiles of 16 input pixels
+  const int ci0 = 16 * wave + 4 * (lane >> 4);
+
+  // ---- per-frame inputs, prefetched one frame ahead ----
+  f32x4 ndy = f32x4{0.f, 0.f, 0.f, 0.f};
+  float nx[4] = {0.f, 0.f, 0.f, 0.f}, nm = 0.f, nr = 0.f, na[3][4];
+  auto fetch = [&](int f) {
+    ndy = *reinterpret_cast<const f32x4*>(dy + (size_t)f * FLAT + j0);
+    load4(act3 + (size_t)f * FLAT + j0, nx);
+    nm = stats[2 * f];
+    nr = stats[2 * f + 1];
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt) {
+      const int px = min(pt * 16 + (lane & 15), P2 - 1);
+      load4(act2 + ((size_t)f * P2 + px) * OC2 + ci0, na[pt]);
+    }
+  };
+  if (f0 + grp < f1) fetch(f0 + grp);
+  float gm[4], dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gm[q] = gam[j0 + q];
+
+  // ---- W3 fragments: A[ci][k = tap*64 + oc] = W3[oc][tap][ci] (k-major) ----
+  V wa[REG ? NKS : 1];
+  if constexpr (REG) {
+    constexpr int NV = OC3 * K3 / VEC, NT = 256 * G;
+    for (int e = (int)threadIdx.x; e < NV; e += NT) {
+      const int r = e / (K3 / VEC), c = (e % (K3 / VEC)) * VEC;
+      *reinterpret_cast<V*>(smem + r * LW + c) = *reinterpret_cast<const V*>(w3 + (size_t)e * VEC);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
+      wa[ks] = lds_frag_k(smem + oc0 * LW + tap * OC2 + 16 * wave, LW, lane);
+    }
+    __syncthreads();  // the staging area becomes the cell grids
+  }
+  // zero the cell grids once (the border stays zero)
+  static_assert(GSZ % VEC == 0, "zero fill");
+  for (int e = tid; e < GSZ / VEC; e += 256) *reinterpret_cast<V*>(d3g + e * VEC) = F::zero();
+  // consume the prologue loads before the loop (see conv1.h: waits merged over the back-edge)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(gm[q]));
+
+  const int n_it = (f1 - f0 + G - 1) / G;
+  for (int it = 0; it < n_it; ++it) {
+    const int f = f0 + G * it + grp;
+    const bool active = f < f1;
+    __syncthreads();  // the previous frame's readers of the cell grid / red are done
+    float d[4], x[4], xh[4], am[3][4];
+    const float mean = nm, rstd = nr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { d[q] = ndy[q]; x[q] = nx[q]; }
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) am[pt][q] = na[pt][q];
+    // ---- LayerNorm backward: the two per-frame sums ----
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xh[q] = (x[q] - mean) * rstd;
+      const float gd = d[q] * gm[q];
+      s1 += gd;
+      s2 += gd * xh[q];
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) { red[grp][wave][0] = s1; red[grp][wave][1] = s2; }
+    __syncthreads();
+    if (f + G < f1) fetch(f + G);
+    if (active) {
+      const float S1 = (red[grp][0][0] + red[grp][1][0] + red[grp][2][0] + red[grp][3][0]) * (1.f / FLAT);
+      const float S2 = (red[grp][0][1] + red[grp][1][1] + red[grp][2][1] + red[grp][3][1]) * (1.f / FLAT);
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dg[q] += d[q] * xh[q];
+        db[q] += d[q];
+        const float gx = rstd * (d[q] * gm[q] - S1 - xh[q] * S2);
+        o[q] = x[q] > 0.f ? gx : 0.f;
+      }
+      store4(dact3 + (size_t)f * FLAT + j0, o);
+      const int oy = p0 >> 2, ox = p0 & 3;
+      store4(d3g + ((oy + 2) * lc3::QG + ox + 2) * LD3 + c0, o);
+    }
+    __syncthreads();
+    if (active) {
+      // ---- conv3 dgrad from the LDS cell grid -> dact2 (conv2's ReLU mask) ----
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) {
+        const int px = min(pt * 16 + (lane & 15), P2 - 1), iy = px / H2, ix = px - iy * H2;
+        const T* brow = d3g + ((iy + 2) * lc3::QG + ix + 2) * LD3 + kl;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto bfrag = [&](int ks) {
+          const int k = ks * KS, tap = k >> 6, oc0 = k & 63, kh = tap / 3, kw = tap - 3 * kh;
+          return *reinterpret_cast<const V*>(brow - (kh * lc3::QG + kw) * LD3 + oc0);
+        };
+        if constexpr (REG) {
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks) acc = F::mma(wa[ks], bfrag(ks), acc);
+        } else {  // fp32: the A fragment straight from L2 (parity mode)
+#pragma unroll 2
+          for (int ks = 0; ks < NKS; ++ks) {
+            const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
+            V a;
+#pragma unroll
+            for (int jj = 0; jj < KPL; ++jj)
+              a[jj] = w3[(size_t)(oc0 + kl + jj) * K3 + tap * OC2 + 16 * wave + (lane & 15)];
+            acc = F::mma(a, bfrag(ks), acc);
+          }
+        }
+        const int pc = pt * 16 + (lane & 15);
+        if (pc < P2) {
+          float o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = am[pt][q] > 0.f ? acc[q] : 0.f;
+          store4(dact2 + ((size_t)f * P2 + pc) * OC2 + ci0, o);
+        }
+      }
+    }
+  }
+  // ---- gamma / beta partials: fixed-order combine of the groups -> slab [2][1024] ----
+  __syncthreads();
+  if (grp == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { comb[j0 + q] = dg[q]; comb[FLAT + j0 + q] = db[q]; }
+  }
+  for (int g = 1; g < G; ++g) {
+    __syncthreads();
+    if (grp == g) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { comb[j0 + q] += dg[q]; comb[FLAT + j0 + q] += db[q]; }
+    }
+  }
+  __syncthreads();
+  for (int e = (int)threadIdx.x; e < 2 * FLAT / 4; e += 256 * G)
+    *reinterpret_cast<f32x4*>(slab + (size_t)blockIdx.x * 2 * FLAT + 4 * e) =
+        *reinterpret_cast<const f32x4*>(comb + 4 * e);
+}

@@ -235,11 +235,14 @@ def test_train_step_deterministic(dtype):
     np.testing.assert_array_equal(flats[0][1], flats[1][1])
 
 
-@pytest.mark.parametrize("env", [{"IMPALA_GRAPH": "1"}, {"IMPALA_SERIAL_STREAM": "1"},
-                                 {"IMPALA_FWD_FUSED": "0"}])
-def test_launch_modes_bitwise_equal(env, monkeypatch):
-    """hipGraph replay (opt-in) and the single-stream schedule give bit-identical steps to the
-    default direct launches with the weight-gradient side stream."""
+@pytest.mark.parametrize("env,exact", [({"IMPALA_GRAPH": "1"}, True),
+                                       ({"IMPALA_SIDE_STREAM": "1"}, True),
+                                       ({"IMPALA_FWD_FUSED": "0"}, True),
+                                       ({"IMPALA_LNC3_FUSED": "0"}, False)])
+def test_launch_modes_agree(env, exact, monkeypatch):
+    """hipGraph replay (opt-in), the single-stream schedule and the unfused conv1/conv2 forward
+    give bit-identical steps to the default; the unfused LayerNorm backward sums its per-frame
+    reductions in another order, so it agrees to fp32 rounding (params after 3 Adam steps)."""
     dev = _dev()
     batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(8, 20, 15, seed=6)]
 
@@ -255,8 +258,12 @@ def test_launch_modes_bitwise_equal(env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     alt = run()
-    np.testing.assert_array_equal(base[0], alt[0])
-    np.testing.assert_array_equal(base[1], alt[1])
+    if exact:
+        np.testing.assert_array_equal(base[0], alt[0])
+        np.testing.assert_array_equal(base[1], alt[1])
+    else:
+        np.testing.assert_allclose(base[0], alt[0], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(base[1], alt[1], rtol=1e-2, atol=1e-4)
 
 
 def test_full_size_bf16_step_properties():

@@ -8,7 +8,7 @@ VARIANTS = {
             "  long long stamps[32] = {0}; " + S(0) + "\n  const int kl = F::KPL * (lane >> 4);\n  set_ctx(ft);\n  fetch(0);"),
         (G, "      stash(buf);\n      __syncthreads();\n",
             "      stash(buf);\n      __syncthreads();\n      if (t == ft) { " + S("1 + kc") + "}\n"),
-        (G, "            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);\n          }\n        }\n      }\n    }\n  }\n}",
-            "            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v);\n          }\n        }\n      }\n    }\n  }\n  " + S(20) + "\n  if " + COND + ' { printf("TILE"); for (int q = 1; q < 21; ++q) printf(" %lld", stamps[q] ? stamps[q] - stamps[0] : -1); printf("\\n"); }\n}'),
+        (G, "            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v, ep[i][j]);\n          }\n        }\n      }\n    }\n  }\n}",
+            "            op.store(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4), c, v, ep[i][j]);\n          }\n        }\n      }\n    }\n  }\n  " + S(20) + "\n  if " + COND + ' { printf("TILE"); for (int q = 1; q < 21; ++q) printf(" %lld", stamps[q] ? stamps[q] - stamps[0] : -1); printf("\\n"); }\n}'),
     ],
 }
