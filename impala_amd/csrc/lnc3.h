@@ -74,10 +74,20 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
   // ---- W3 fragments: A[ci][k = tap*64 + oc] = W3[oc][tap][ci] (k-major) ----
   V wa[REG ? NKS : 1];
   if constexpr (REG) {
-    constexpr int NV = OC3 * K3 / VEC, NT = 256 * G;
-    for (int e = (int)threadIdx.x; e < NV; e += NT) {
-      const int r = e / (K3 / VEC), c = (e % (K3 / VEC)) * VEC;
-      *reinterpret_cast<V*>(smem + r * LW + c) = *reinterpret_cast<const V*>(w3 + (size_t)e * VEC);
+    constexpr int NV = OC3 * K3 / VEC, NT = 256 * G, NPT = (NV + NT - 1) / NT;
+    V wv[NPT];  // all loads in flight at once, then the LDS stores
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = (int)threadIdx.x + i * NT;
+      if (e < NV) wv[i] = *reinterpret_cast<const V*>(w3 + (size_t)e * VEC);
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = (int)threadIdx.x + i * NT;
+      if (e < NV) {
+        const int r = e / (K3 / VEC), c = (e % (K3 / VEC)) * VEC;
+        *reinterpret_cast<V*>(smem + r * LW + c) = wv[i];
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -139,34 +149,48 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
     __syncthreads();
     if (active) {
       // ---- conv3 dgrad from the LDS cell grid -> dact2 (conv2's ReLU mask) ----
+      // the 3 pixel tiles advance together: 3 independent LDS reads per A fragment
+      const T* brow[3];
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt) {
         const int px = min(pt * 16 + (lane & 15), P2 - 1), iy = px / H2, ix = px - iy * H2;
-        const T* brow = d3g + ((iy + 2) * lc3::QG + ix + 2) * LD3 + kl;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto bfrag = [&](int ks) {
-          const int k = ks * KS, tap = k >> 6, oc0 = k & 63, kh = tap / 3, kw = tap - 3 * kh;
-          return *reinterpret_cast<const V*>(brow - (kh * lc3::QG + kw) * LD3 + oc0);
-        };
-        if constexpr (REG) {
+        brow[pt] = d3g + ((iy + 2) * lc3::QG + ix + 2) * LD3 + kl;
+      }
+      auto boff = [&](int ks) {
+        const int k = ks * KS, tap = k >> 6, oc0 = k & 63, kh = tap / 3, kw = tap - 3 * kh;
+        return -(kh * lc3::QG + kw) * LD3 + oc0;
+      };
+      f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                      f32x4{0.f, 0.f, 0.f, 0.f}};
+      if constexpr (REG) {
 #pragma unroll
-          for (int ks = 0; ks < NKS; ++ks) acc = F::mma(wa[ks], bfrag(ks), acc);
-        } else {  // fp32: the A fragment straight from L2 (parity mode)
-#pragma unroll 2
-          for (int ks = 0; ks < NKS; ++ks) {
-            const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
-            V a;
+        for (int ks = 0; ks < NKS; ++ks) {
+          V b[3];
 #pragma unroll
-            for (int jj = 0; jj < KPL; ++jj)
-              a[jj] = w3[(size_t)(oc0 + kl + jj) * K3 + tap * OC2 + 16 * wave + (lane & 15)];
-            acc = F::mma(a, bfrag(ks), acc);
-          }
+          for (int pt = 0; pt < 3; ++pt) b[pt] = *reinterpret_cast<const V*>(brow[pt] + boff(ks));
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma(wa[ks], b[pt], acc[pt]);
         }
+      } else {  // fp32: the A fragment straight from L2 (parity mode)
+#pragma unroll 2
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
+          V a;
+#pragma unroll
+          for (int jj = 0; jj < KPL; ++jj)
+            a[jj] = w3[(size_t)(oc0 + kl + jj) * K3 + tap * OC2 + 16 * wave + (lane & 15)];
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt)
+            acc[pt] = F::mma(a, *reinterpret_cast<const V*>(brow[pt] + boff(ks)), acc[pt]);
+        }
+      }
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) {
         const int pc = pt * 16 + (lane & 15);
         if (pc < P2) {
           float o[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = am[pt][q] > 0.f ? acc[q] : 0.f;
+          for (int q = 0; q < 4; ++q) o[q] = am[pt][q] > 0.f ? acc[pt][q] : 0.f;
           store4(dact2 + ((size_t)f * P2 + pc) * OC2 + ci0, o);
         }
       }
