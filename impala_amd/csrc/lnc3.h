@@ -6,10 +6,14 @@
 //
 // One frame per 4-wave group at a time, G groups per workgroup on alternating frames:
 //   LN: wave w owns features 256 w .. 256 w + 255 (lane: 4 consecutive), the two per-frame
-//       sums are combined through LDS; dact3 goes to HBM (for the conv3 weight gradient) and to
-//       a zero-bordered 8x8 cell grid in LDS, so the conv3 dgrad gather needs no bounds tests
-//   dgrad: wave w owns ci tile w (its W3 fragments, k-major through the LDS transpose read, in
-//       registers), 3 tiles of 16 input pixels, K = 9 taps x 64 oc
+//       sums are combined through LDS; dact3 goes to HBM (for the conv3 weight gradient) and
+//       to LDS
+//   dgrad in scatter form: Z[p][tap][ci] = sum_oc dact3[p][oc] W3[oc][tap][ci] for the 16
+//       conv3 output pixels p (one MFMA row tile; wave w owns ci tile w of every tap, its W3
+//       fragments -- read k-major through the LDS transpose read -- in registers; K = 64),
+//       then each input pixel gathers its <= 9 (p, tap) contributions from the fp32 Z in LDS
+//       in a fixed order.  72 MFMAs per frame instead of the 216 of the gather form, and no
+//       shifted-window LDS reads.
 // LN gamma / beta gradient partials are kept per lane and written as one fp32 slab per
 // workgroup (fixed-order combine of the groups), reduced by reduce_grads like the others.
 #pragma once
@@ -19,7 +23,7 @@
 using namespace net;
 
 namespace lc3 {
-constexpr int QG = 8;  // dact3 cell grid: oy = r - 2, r in [0, 8)
+constexpr int ZR = 9 * OC2 + 4;  // Z row (fp32): [tap][ci] of one output pixel, padded
 }
 
 template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 1; }
@@ -33,24 +37,27 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
   constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int LD3 = OC3 + VEC;                     // dact3 cell row (elements)
+  constexpr int LD3 = OC3 + VEC;                     // dact3 row (elements)
   constexpr int LW = K3 + VEC;                       // staged W3 row
   constexpr int NKS = K3 / KS;
+  constexpr int NKO = OC3 / KS;                      // k-steps per tap (K = oc)
   constexpr int G = lnc3_groups<T>();
-  constexpr int GSZ = lc3::QG * lc3::QG * LD3;       // one group's cell grid
+  // one group's LDS: Z (fp32 [16][ZR]) then the dact3 tile (T [16][LD3]), in bytes
+  constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
   constexpr bool REG = sizeof(T) == 2;               // bf16: W3 fragments in registers
-  constexpr int SMEM = (REG && OC3 * LW > G * GSZ) ? OC3 * LW : G * GSZ;
-  __shared__ __attribute__((aligned(16))) T smem[SMEM];
+  constexpr int SMEM = (REG && OC3 * LW * (int)sizeof(T) > G * GB) ? OC3 * LW * (int)sizeof(T) : G * GB;
+  static_assert(GB % 16 == 0, "group alignment");
+  __shared__ __attribute__((aligned(16))) char smem_b[SMEM];
   __shared__ float red[G][4][2];
   __shared__ float comb[2 * FLAT];
+  T* smem = reinterpret_cast<T*>(smem_b);
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-  T* d3g = smem + grp * GSZ;
+  float* zs = reinterpret_cast<float*>(smem_b + grp * GB);
+  T* d3s = reinterpret_cast<T*>(smem_b + grp * GB + ZB);
   const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
   const int kl = KPL * (lane >> 4);
   // this lane's LN features j = 256 w + 4 lane + q  (pixel p = j / 64, channel c = j % 64)
   const int j0 = 256 * wave + 4 * lane, p0 = j0 >> 6, c0 = j0 & 63;
-  // conv3 dgrad: ci tile = wave, 3 tiles of 16 input pixels
-  const int ci0 = 16 * wave + 4 * (lane >> 4);
 
   // ---- per-frame inputs, prefetched one frame ahead ----
   f32x4 ndy = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -61,9 +68,9 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
     nm = stats[2 * f];
     nr = stats[2 * f + 1];
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt) {
-      const int px = min(pt * 16 + (lane & 15), P2 - 1);
-      load4(act2 + ((size_t)f * P2 + px) * OC2 + ci0, na[pt]);
+    for (int r = 0; r < 3; ++r) {  // gather items e = tid + 256 r: pixel e / 16, channels 4 (e % 16)
+      const int e = min(tid + 256 * r, P2 * 16 - 1);
+      load4(act2 + ((size_t)f * P2 + (e >> 4)) * OC2 + 4 * (e & 15), na[r]);
     }
   };
   if (f0 + grp < f1) fetch(f0 + grp);
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
 #pragma unroll
   for (int q = 0; q < 4; ++q) gm[q] = gam[j0 + q];
 
-  // ---- W3 fragments: A[ci][k = tap*64 + oc] = W3[oc][tap][ci] (k-major) ----
+  // ---- W3 fragments: B[k = oc][n = ci] = W3[oc][tap][ci] of every tap (k-major) ----
   V wa[REG ? NKS : 1];
   if constexpr (REG) {
     constexpr int NV = OC3 * K3 / VEC, NT = 256 * G, NPT = (NV + NT - 1) / NT;
@@ -95,11 +102,8 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
       const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
       wa[ks] = lds_frag_k(smem + oc0 * LW + tap * OC2 + 16 * wave, LW, lane);
     }
-    __syncthreads();  // the staging area becomes the cell grids
+    __syncthreads();  // the staging area becomes the Z / dact3 tiles
   }
-  // zero the cell grids once (the border stays zero)
-  static_assert(GSZ % VEC == 0, "zero fill");
-  for (int e = tid; e < GSZ / VEC; e += 256) *reinterpret_cast<V*>(d3g + e * VEC) = F::zero();
   // consume the prologue loads before the loop (see conv1.h: waits merged over the back-edge)
 #pragma unroll
   for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(gm[q]));
@@ -143,55 +147,57 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
         o[q] = x[q] > 0.f ? gx : 0.f;
       }
       store4(dact3 + (size_t)f * FLAT + j0, o);
-      const int oy = p0 >> 2, ox = p0 & 3;
-      store4(d3g + ((oy + 2) * lc3::QG + ox + 2) * LD3 + c0, o);
+      store4(d3s + p0 * LD3 + c0, o);
     }
     __syncthreads();
     if (active) {
-      // ---- conv3 dgrad from the LDS cell grid -> dact2 (conv2's ReLU mask) ----
-      // the 3 pixel tiles advance together: 3 independent LDS reads per A fragment
-      const T* brow[3];
+      // ---- Z[p][tap][ci] = sum_oc dact3[p][oc] W3[oc][tap][ci]: wave w, ci tile w ----
+      V a[NKO];
 #pragma unroll
-      for (int pt = 0; pt < 3; ++pt) {
-        const int px = min(pt * 16 + (lane & 15), P2 - 1), iy = px / H2, ix = px - iy * H2;
-        brow[pt] = d3g + ((iy + 2) * lc3::QG + ix + 2) * LD3 + kl;
-      }
-      auto boff = [&](int ks) {
-        const int k = ks * KS, tap = k >> 6, oc0 = k & 63, kh = tap / 3, kw = tap - 3 * kh;
-        return -(kh * lc3::QG + kw) * LD3 + oc0;
-      };
-      f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
-                      f32x4{0.f, 0.f, 0.f, 0.f}};
-      if constexpr (REG) {
+      for (int ko = 0; ko < NKO; ++ko)
+        a[ko] = *reinterpret_cast<const V*>(d3s + (lane & 15) * LD3 + ko * KS + kl);
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          V b[3];
+      for (int tap = 0; tap < 9; ++tap) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) b[pt] = *reinterpret_cast<const V*>(brow[pt] + boff(ks));
+        for (int ko = 0; ko < NKO; ++ko) {
+          const int ks = tap * NKO + ko;
+          if constexpr (REG) {
+            acc = F::mma(a[ko], wa[ks], acc);
+          } else {  // fp32: the B fragment straight from L2 (parity mode)
+            V b;
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma(wa[ks], b[pt], acc[pt]);
+            for (int jj = 0; jj < KPL; ++jj)
+              b[jj] = w3[(size_t)(ko * KS + kl + jj) * K3 + tap * OC2 + 16 * wave + (lane & 15)];
+            acc = F::mma(a[ko], b, acc);
+          }
         }
-      } else {  // fp32: the A fragment straight from L2 (parity mode)
-#pragma unroll 2
-        for (int ks = 0; ks < NKS; ++ks) {
-          const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
-          V a;
 #pragma unroll
-          for (int jj = 0; jj < KPL; ++jj)
-            a[jj] = w3[(size_t)(oc0 + kl + jj) * K3 + tap * OC2 + 16 * wave + (lane & 15)];
-#pragma unroll
-          for (int pt = 0; pt < 3; ++pt)
-            acc[pt] = F::mma(a, *reinterpret_cast<const V*>(brow[pt] + boff(ks)), acc[pt]);
-        }
+        for (int q = 0; q < 4; ++q)
+          zs[(4 * (lane >> 4) + q) * lc3::ZR + tap * OC2 + 16 * wave + (lane & 15)] = acc[q];
       }
+    }
+    __syncthreads();
+    if (active) {
+      // ---- col2im gather in a fixed (kh, kw) order + conv2's ReLU mask -> dact2 ----
 #pragma unroll
-      for (int pt = 0; pt < 3; ++pt) {
-        const int pc = pt * 16 + (lane & 15);
-        if (pc < P2) {
+      for (int r = 0; r < 3; ++r) {
+        const int e = tid + 256 * r;
+        if (e < P2 * 16) {
+          const int px = e >> 4, ci = 4 * (e & 15), iy = px / H2, ix = px - iy * H2;
+          f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              const int oy = iy - kh, ox = ix - kw;
+              if (oy >= 0 && oy < H3 && ox >= 0 && ox < H3)
+                sum += *reinterpret_cast<const f32x4*>(zs + (oy * H3 + ox) * lc3::ZR + (kh * 3 + kw) * OC2 + ci);
+            }
           float o[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = am[pt][q] > 0.f ? acc[pt][q] : 0.f;
-          store4(dact2 + ((size_t)f * P2 + pc) * OC2 + ci0, o);
+          for (int q = 0; q < 4; ++q) o[q] = am[r][q] > 0.f ? sum[q] : 0.f;
+          store4(dact2 + ((size_t)f * P2 + px) * OC2 + ci, o);
         }
       }
     }
