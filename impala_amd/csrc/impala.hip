@@ -239,7 +239,9 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   const Shadow& sh = h->sh;
   // ---- dgrad chain on `st`; each weight-gradient branch forks onto the side stream as soon
   // as its inputs exist and joins before the slab reduction ----
-  constexpr int WBM = sizeof(T) == 4 ? 32 : 64;  // m-chunk of gemm_wg (LDS budget of f32)
+  // gemm_wg: 32-row m-chunks, several 4-wave groups per workgroup on interleaved chunks (more
+  // chunk loads in flight per CU); fp32 (parity mode) keeps one group for its LDS budget
+  constexpr int WG4 = sizeof(T) == 2 ? 4 : 1, WG2 = sizeof(T) == 2 ? 2 : 1;
   hipStream_t ss = h->use_side ? h->side : st;
   auto fork = [&](int i) -> int {
     if (!h->use_side) return 0;
@@ -268,7 +270,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     FcWgrad<T> op{};
     op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
     timer_begin(h, K_FC_WGRAD, ss);
-    gemm_wg<T, 64, 256, 1, 4, WBM, 1><<<dim3(FLAT / 256, HID / 64, h->spfc.S), 256, 0, ss>>>(
+    gemm_wg<T, 64, 256, 1, 4, 32, WG2><<<dim3(FLAT / 256, HID / 64, h->spfc.S), 256 * WG2, 0, ss>>>(
         op, h->s_fc, h->s_bfc, h->spfc.mps);
     timer_end(h, K_FC_WGRAD, ss);
     CK_LAUNCH("fc_wgrad");
@@ -302,7 +304,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     Conv3Wgrad<T> op{};
     op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
     timer_begin(h, K_CONV3_WGRAD, ss);
-    gemm_wg<T, 64, 192, 1, 4, WBM, 2><<<dim3(K3 / 192, 1, h->sp3.S), 512, 0, ss>>>(
+    gemm_wg<T, 64, 192, 1, 4, 32, WG4><<<dim3(K3 / 192, 1, h->sp3.S), 256 * WG4, 0, ss>>>(
         op, h->s_w3, h->s_b3, h->sp3.mps);
     timer_end(h, K_CONV3_WGRAD, ss);
     CK_LAUNCH("conv3_wgrad");
@@ -321,7 +323,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     Conv2Wgrad<T> op{};
     op.M = N * P2; op.x = (const T*)h->dact2; op.in = (const T*)h->act1;
     timer_begin(h, K_CONV2_WGRAD, ss);
-    gemm_wg<T, 64, 128, 1, 4, WBM, 2><<<dim3(K2 / 128, 1, h->sp2.S), 512, 0, ss>>>(
+    gemm_wg<T, 64, 128, 1, 4, 32, WG4><<<dim3(K2 / 128, 1, h->sp2.S), 256 * WG4, 0, ss>>>(
         op, h->s_w2, h->s_b2, h->sp2.mps);
     timer_end(h, K_CONV2_WGRAD, ss);
     CK_LAUNCH("conv2_wgrad");
