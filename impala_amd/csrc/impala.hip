@@ -197,6 +197,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     op.C = n * P3; op.w = sw + sh.w3; op.b = vv + Vecs::b3; op.x = (const T*)h->act2;
     op.out = (T*)h->act3; op.gam = vv + Vecs::lng; op.bet = vv + Vecs::lnb; op.y = (T*)h->y;
     op.stats = h->lnstat;
+    op.frames_per_tile = 64 / P3;
     timer_begin(h, K_CONV3_FWD, st);
     gemm_tile<T, 64, 64, BK(96), 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
     timer_end(h, K_CONV3_FWD, st);
@@ -205,7 +206,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
     timer_begin(h, K_FC_FWD, st);
-    gemm_tile<T, 64, 64, BK(256), 2, 2><<<persist_grid(h, (long)cdiv(n, 64) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
+    gemm_tile<T, 64, 32, BK(256), 2, 2><<<persist_grid(h, (long)cdiv(n, 32) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
     timer_end(h, K_FC_FWD, st);
     CK_LAUNCH("fc_fwd");
   }

@@ -133,13 +133,14 @@ template <typename T> struct Conv3LnFwd : Conv3Fwd<T> {
   const float* bet;
   T* y;
   float* stats;
+  int frames_per_tile;  // tile width / 16 (<= 4: one wave per frame)
   typedef LnLane EpiConst;  // loaded once per workgroup (gemm_tile)
   DEV EpiConst epi_const(int tid) const { return ln_lane_consts(tid & 63, this->b, gam, bet); }
   DEV void tile_epilogue(const float* et, int ldt, int, int cc0, int tid,
                          const EpiConst& k) const {
     const int lane = tid & 63, wave = tid >> 6;
     const int frame = cc0 / P3 + wave;
-    if ((frame + 1) * P3 > this->C) return;
+    if (wave >= frames_per_tile || (frame + 1) * P3 > this->C) return;
     ln_frame_epilogue<T>(et + wave * P3 * ldt, ldt, frame, lane, k, this->out, y, stats);
   }
 };
