@@ -448,19 +448,17 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   const bool in = v4 * 4 < sg.count;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   if (in) {
+    // 8 split loads in flight per round (the split count is >= 4 x SG by construction)
     const float* p = sg.slab + (size_t)v4 * 4;
-    int q = grp;
-    for (; q + 3 * SG < sg.S; q += 4 * SG) {
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + (size_t)q * sg.count);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + SG) * sg.count);
-      const f32x4 v2 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 2 * SG) * sg.count);
-      const f32x4 v3 = *reinterpret_cast<const f32x4*>(p + (size_t)(q + 3 * SG) * sg.count);
-      acc += v0;
-      acc += v1;
-      acc += v2;
-      acc += v3;
+    for (int q = grp; q < sg.S; q += 8 * SG) {
+      f32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = q + j * SG < sg.S ? *reinterpret_cast<const f32x4*>(p + (size_t)(q + j * SG) * sg.count)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j];
     }
-    for (; q < sg.S; q += SG) acc += *reinterpret_cast<const f32x4*>(p + (size_t)q * sg.count);
   }
   part[threadIdx.x] = acc;
   __syncthreads();
