@@ -47,6 +47,8 @@ def kernel_work(es):
         "fc_dgrad": (2 * 256 * 1024, 256 * es + 1024 * 4, 256 * 1024 * es),
         "ln_bwd": (10 * 1024, 1024 * 4 + 2 * a3 + 8, 2 * 1024 * 4),
         "conv3_dgrad": (2 * 16 * 64 * 576, a3 + 2 * a2, 64 * 576 * es),
+        "ln_bwd_conv3_dgrad": (2 * 16 * 64 * 576 + 10 * 1024, 1024 * 4 + 2 * a3 + 8 + 2 * a2,
+                               64 * 576 * es + 1024 * 4 * 2),
         "conv2_dgrad_conv1_wgrad": (2 * 36 * 64 * 512 + 2 * 225 * 32 * 192, obs + a2 + m1,
                                     64 * 512 * es),
         "fc_wgrad": (2 * 256 * 1024, 256 * es + a3, 0),
@@ -103,7 +105,7 @@ def cpu_baseline(B, T, A, seconds):
 PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
                  "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "head_step": "head_step",
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
-                 "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "fc_wgrad": "FcWgrad",
+                 "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "ln_bwd_conv3_dgrad": "LnConv3Bwd", "fc_wgrad": "FcWgrad",
                  "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
                  "reduce_grads": "reduce_grads", "adam": "adam"}
 

@@ -24,6 +24,8 @@ def short(name):
         return "Conv12Bwd"
     if "conv12_fwd_s2d" in n:
         return "Conv12Fwd"
+    if "lnc3_bwd" in n:
+        return "LnConv3Bwd"
     if "head_step" in n:
         return "head_step"
     if "gemm_tile" in n or "gemm_wg" in n or "gemm_rc" in n:
