@@ -97,16 +97,67 @@ DEV void load4(const __bf16* p, float v[4]) {
   v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3];
 }
 
-DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- cross-lane moves without the LDS crossbar: DPP within rows of 16 lanes, the gfx950
+// permlane swaps across rows.  Every reduction below combines symmetric pairs only, so all
+// lanes end with the bit-identical result (and runs are deterministic). ----
+template <int CTRL> DEV float dppf(float v) {  // lanes without a source read 0
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL> DEV uint32_t dppu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROW_MIRROR = 0x140,
+             DPP_ROW_HALF_MIRROR = 0x141, DPP_WAVE_SHL1 = 0x130 };
+// x[lane ^ 16] (resp. ^ 32) exchanges across rows with v_permlane16/32_swap_b32.  Inline asm
+// with two read-write operands keeps the two copies in distinct registers: the builtin lets the
+// compiler tie both operands to one register, which swaps a register with itself.  The s_nop
+// covers the VALU-write -> permlane-read hazard the compiler cannot see through inline asm.
+DEV void swap16(uint32_t& a, uint32_t& b) { asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+DEV void swap32(uint32_t& a, uint32_t& b) { asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+DEV float xor16_sum(float v) {  // v[lane & ~16] + v[lane | 16] on every lane
+  uint32_t a = __builtin_bit_cast(uint32_t, v), b = a;
+  swap16(a, b);
+  return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);
+}
+DEV float xor32_sum(float v) {
+  uint32_t a = __builtin_bit_cast(uint32_t, v), b = a;
+  swap32(a, b);
+  return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);
+}
+DEV uint32_t xor16_or(uint32_t v) {
+  uint32_t a = v, b = v;
+  swap16(a, b);
+  return a | b;
+}
+DEV uint32_t xor32_or(uint32_t v) {
+  uint32_t a = v, b = v;
+  swap32(a, b);
+  return a | b;
+}
+// sum over the 16 lanes of each row (all 16 lanes get the row sum)
+DEV float row16_sum(float v) {
+  v += dppf<DPP_QP_1032>(v);
+  v += dppf<DPP_QP_2301>(v);
+  v += dppf<DPP_ROW_HALF_MIRROR>(v);
+  v += dppf<DPP_ROW_MIRROR>(v);
   return v;
 }
+DEV float wave_sum(float v) { return xor32_sum(xor16_sum(row16_sum(v))); }
 DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dppf<DPP_QP_1032>(v));
+  v = fmaxf(v, dppf<DPP_QP_2301>(v));
+  v = fmaxf(v, dppf<DPP_ROW_HALF_MIRROR>(v));
+  v = fmaxf(v, dppf<DPP_ROW_MIRROR>(v));
+  uint32_t a = __builtin_bit_cast(uint32_t, v), b = a;
+  swap16(a, b);
+  v = fmaxf(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b));
+  a = __builtin_bit_cast(uint32_t, v);
+  b = a;
+  swap32(a, b);
+  return fmaxf(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b));
 }
+// lane i reads lane i + 1 (lane 63 reads 0): __shfl_down(v, 1) without the LDS crossbar
+DEV float shift_down1(float v) { return dppf<DPP_WAVE_SHL1>(v); }
 
 // exact (erf) GELU, models/models.py:68 nn.GELU() default approximate='none'
 DEV float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752440f)); }

@@ -137,8 +137,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
         }
         if (pc < c1::NPIX) store4(out + ((size_t)f * c1::NPIX + pc) * OC1 + 16 * i + 4 * (lane >> 4), v);
       }
-      bits |= __shfl_xor(bits, 16, 64);
-      bits |= __shfl_xor(bits, 32, 64);
+      bits = xor32_or(xor16_or(bits));
       if (mask && pc < c1::NPIX && lane < 16) mask[(size_t)f * c1::NPIX + pc] = bits;
     }
   }
@@ -279,8 +278,7 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
             store4(a1s + pc * LDA1 + oc, v);
           }
         }
-        bits |= __shfl_xor(bits, 16, 64);
-        bits |= __shfl_xor(bits, 32, 64);
+        bits = xor32_or(xor16_or(bits));
         if (pc < c1::NPIX && lane < 16) mask[(size_t)f * c1::NPIX + pc] = bits;
       }
     }
@@ -592,10 +590,7 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float v = bsum[i][q];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
+      v = row16_sum(v);
       bsum[i][q] = v;
     }
   __syncthreads();  // all groups are done with their tiles

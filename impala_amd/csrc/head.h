@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) {
       lg[j] = j < A ? lg_s[f][j] : -INFINITY;
-      if (j >= A) mu[j] = -INFINITY;
+      mu[j] = j < A ? mu[j] : -INFINITY;
       m = fmaxf(m, lg[j]);
       mm = fmaxf(mm, mu[j]);
     }
@@ -163,28 +163,28 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     }
     const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm), inv_s = 1.f / s;
     float logmua = 0.f;
+    // selects, not branches on the runtime action count: a uniform `if (j < A)` per action
+    // makes the compiler carry whole copies of the p/logp arrays through every branch
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) {
-      if (j < A) {
-        logp[j] = lg[j] - lse;
-        p[j] *= inv_s;
-        const float lmu = mu[j] - lse_mu;
-        H -= p[j] * logp[j];
-        kld += p[j] * (logp[j] - lmu);
-        if (j == act) { logpa = logp[j]; logmua = lmu; }
-      } else {
-        logp[j] = 0.f;
-      }
+      const bool on = j < A;
+      logp[j] = on ? lg[j] - lse : 0.f;
+      p[j] *= inv_s;  // 0 for padded actions
+      const float lmu = on ? mu[j] - lse_mu : 0.f;
+      H -= p[j] * logp[j];
+      kld += p[j] * (logp[j] - lmu);
+      logpa = j == act ? logp[j] : logpa;
+      logmua = j == act ? lmu : logmua;
     }
     rho = fast_exp(logpa - logmua);
     if (!valid) { H = 0.f; kld = 0.f; rho = 0.f; v = 0.f; r = 0.f; g = 0.f; }
-    const float v_n = __shfl_down(v, 1, 64);
+    const float v_n = shift_down1(v);
     const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
     const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
     const float e = seg_rev_scan(aa, td, t, L, S);
     const float tgt = e + v;
     const float err = tgt - v;
-    const float tgt_n = __shfl_down(tgt, 1, 64);
+    const float tgt_n = shift_down1(tgt);
     const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
     const float qq = r + g * boot;
     const float adv = fminf(a.cpg, rho) * (qq - v);
@@ -243,8 +243,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
       const int o = tid & 15, fg = tid >> 4;
       float b = 0.f;
       for (int f = fg; f < nf; f += 16) b += (float)dHs[f * LDD + o];
-      b += __shfl_xor(b, 16, 64);
-      b += __shfl_xor(b, 32, 64);
+      b = xor32_sum(xor16_sum(b));
       if ((lane >> 4) == 0) bred[wave][o] = b;
       __syncthreads();
       if (tid < HEADS)

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void vtrace_kernel(const float* __restrict__ v
   const float aa = in ? g * (lam * fminf(1.f, rho)) : 0.f;
   const float e = seg_rev_scan(aa, td, t, L, S);
   const float tgt = e + v;
-  const float tgt_n = __shfl_down(tgt, 1, 64), v_n = __shfl_down(v, 1, 64);
+  const float tgt_n = shift_down1(tgt), v_n = shift_down1(v);
   const float boot = (t < L - 1) ? lam * tgt_n + (1.f - lam) * v_n : vt;
   const float qq = r + g * boot;
   if (in) {
@@ -148,13 +148,13 @@ __global__ __launch_bounds__(256) void loss_head_kernel(const LossArgs a, TO* __
     rho = expf(logpa - logmua);
   }
   // ---- V-trace over the first T-1 steps of each trajectory segment ----
-  const float v_n = __shfl_down(v, 1, 64);  // values[:, 1:]
+  const float v_n = shift_down1(v);  // values[:, 1:]
   const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
   const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
   const float e = seg_rev_scan(aa, td, t, L, S);
   const float tgt = e + v;
   const float err = tgt - v;
-  const float tgt_n = __shfl_down(tgt, 1, 64);
+  const float tgt_n = shift_down1(tgt);
   const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
   const float qq = r + g * boot;
   const float adv = fminf(a.cpg, rho) * (qq - v);
