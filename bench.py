@@ -159,6 +159,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    from impala_amd.distributed import compute_grads_allreduced
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
 
@@ -175,8 +176,7 @@ def main():
         if dist is None:
             eng.train_step(*batch)
         else:
-            eng.compute_grads(*batch)
-            dist.all_reduce(model.flat_grad)
+            compute_grads_allreduced(eng, batch, model.flat_grad)
             eng.apply_update()
 
     for _ in range(args.warmup):

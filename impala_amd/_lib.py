@@ -24,7 +24,8 @@ EXPORTS = (
     "impala_abi_version", "impala_last_error", "impala_config_default", "impala_param_count",
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
     "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
-    "impala_apply_update", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
+    "impala_apply_update", "impala_compute_grads_part", "impala_grad_bucket_offset",
+    "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
 )
 
@@ -65,6 +66,9 @@ def _declare(lib):
     lib.impala_train_step.argtypes = [_P, C.POINTER(ImpalaBatch), _P]
     lib.impala_compute_grads.argtypes = [_P, C.POINTER(ImpalaBatch), _P]
     lib.impala_apply_update.argtypes = [_P, _P]
+    lib.impala_compute_grads_part.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int, _P]
+    lib.impala_grad_bucket_offset.argtypes = [_P]
+    lib.impala_grad_bucket_offset.restype = C.c_size_t
     lib.impala_vtrace.argtypes = [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_float, C.c_float,
                                   C.c_float, _P, _P, _P, _P]
     lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,

@@ -232,8 +232,12 @@ int reduce_segments(impala_learner* h, int s_lo, int s_hi, hipStream_t st, int f
   return 0;
 }
 
+// part: -1 = the whole backward; 0 = through the conv3 weight gradient, ending with the
+// reduction of gradient bucket 1 (conv3 .. heads, canonical [cn.w3, total)); 1 = the rest
+// (conv2 weight gradient, conv2 dgrad + conv1 wgrad, bucket 0 = conv1 + conv2, loss metrics).
+// Data-parallel replicas all-reduce bucket 1 while part 1 runs.
 template <typename T>
-int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
+int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {
   using namespace net;
   const int N = h->N, B = h->cfg.batch_size, Tl = h->cfg.rollout_length;
   const T* sw = reinterpret_cast<const T*>(h->shadow);
@@ -250,6 +254,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     CK(hipStreamWaitEvent(ss, h->ev_fork[i], 0));
     return 0;
   };
+  if (part == 1) goto part1;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
   {
     HeadArgs ha{};
@@ -319,6 +324,14 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
     timer_end(h, K_CONV3_DGRAD, st);
     CK_LAUNCH("conv3_dgrad");
   }
+  if (part == 0) {  // bucket 1 complete
+    if (h->use_side) {
+      CK(hipEventRecord(h->ev_join, ss));
+      CK(hipStreamWaitEvent(st, h->ev_join, 0));
+    }
+    return reduce_segments(h, RS_CONV3, RS_END, st, 0);
+  }
+part1:
   if (int r = fork(3)) return r;  // dact2 ready
   {
     Conv2Wgrad<T> op{};
@@ -342,6 +355,13 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st) {
   CK_LAUNCH("conv2_dgrad_conv1_wgrad");
   // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were
   // reduced on the side stream right after their weight gradients ----
+  if (part == 1) {
+    if (h->use_side) {
+      CK(hipEventRecord(h->ev_join, ss));
+      CK(hipStreamWaitEvent(st, h->ev_join, 0));
+    }
+    return reduce_segments(h, RS_CONV1, RS_CONV3, st, 1);
+  }
   if (h->red_mode == 0) {
     if (h->use_side) {  // join
       CK(hipEventRecord(h->ev_join, ss));
@@ -692,11 +712,13 @@ int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, 
 
 extern "C++" {
 namespace {
-int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st) {
-  int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st, false)
-                  : launch_forward<float>(h, b->obs, h->N, st, false);
-  if (r) return r;
-  return h->bf16 ? launch_backward<__bf16>(h, b, st) : launch_backward<float>(h, b, st);
+int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {
+  if (part != 1) {
+    int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st, false)
+                    : launch_forward<float>(h, b->obs, h->N, st, false);
+    if (r) return r;
+  }
+  return h->bf16 ? launch_backward<__bf16>(h, b, st, part) : launch_backward<float>(h, b, st, part);
 }
 
 int enqueue_update(impala_learner* h, hipStream_t st) {
@@ -750,7 +772,7 @@ int run_graphed(impala_learner* h, int kind, const impala_batch* b, hipStream_t 
   CK(hipGraphLaunch(exec, st));
   return 0;
 }
-enum { G_GRADS = 0, G_UPDATE = 1, G_STEP = 2 };
+enum { G_GRADS = 0, G_UPDATE = 1, G_STEP = 2, G_GRADS0 = 3, G_GRADS1 = 4 };
 }  // namespace
 }  // extern "C++"
 
@@ -761,6 +783,17 @@ int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream)
   return run_graphed(h, G_GRADS, b, (hipStream_t)stream,
                      [&](hipStream_t s) { return enqueue_grads(h, b, s); });
 }
+
+int impala_compute_grads_part(impala_learner* h, const impala_batch* b, int part, void* stream) {
+  if (part != 0 && part != 1) return fail(IMPALA_E_INVALID, "part must be 0 or 1");
+  if (int r = check_bound(h)) return r;
+  if (int r = check_batch(b)) return r;
+  CK(hipSetDevice(h->device));
+  return run_graphed(h, part ? G_GRADS1 : G_GRADS0, b, (hipStream_t)stream,
+                     [&](hipStream_t s) { return enqueue_grads(h, b, s, part); });
+}
+
+size_t impala_grad_bucket_offset(const impala_learner* h) { return h ? h->cn.w3 : 0; }
 
 int impala_apply_update(impala_learner* h, void* stream) {
   if (int r = check_bound(h)) return r;

@@ -151,6 +151,21 @@ class Engine:
         check(_lib.lib().impala_compute_grads(self._h, C.byref(b), stream_ptr(stream)),
               "impala_compute_grads")
 
+    def compute_grads_part(self, part, obs, actions, rewards, discounts, mu, stream=None):
+        """Half of compute_grads: part 0 finishes grads[bucket_offset:] (conv3 .. heads),
+        part 1 (same batch) finishes grads[:bucket_offset] (conv1, conv2) and the metrics."""
+        b = self._batch(obs, actions, rewards, discounts, mu)
+        if part == 0:
+            self._sync_weights(stream)
+        check(_lib.lib().impala_compute_grads_part(self._h, C.byref(b), int(part),
+                                                   stream_ptr(stream)),
+              "impala_compute_grads_part")
+
+    @property
+    def bucket_offset(self) -> int:
+        """First flat-gradient index of bucket 1 (all-reduced while part 1 runs)."""
+        return int(_lib.lib().impala_grad_bucket_offset(self._h))
+
     def apply_update(self, stream=None):
         check(_lib.lib().impala_apply_update(self._h, stream_ptr(stream)), "impala_apply_update")
         self._updated()

@@ -135,9 +135,8 @@ class ImpalaLearner(Learner):
         if self._world_size == 1:
             e.train_step(*batch)
         else:
-            import torch.distributed as dist
-            e.compute_grads(*batch)
-            dist.all_reduce(self._model.flat_grad, group=self._pg)
+            from .distributed import compute_grads_allreduced
+            compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
             e.apply_update()
         m = e.metrics.clone()  # device scalars; float(v) synchronises lazily
         return {name: m[i] for i, name in enumerate(_lib.METRIC_NAMES)}

@@ -120,6 +120,14 @@ int impala_compute_grads(impala_learner* h, const impala_batch* batch, void* str
 /* ... caller all-reduces (sums) `grads` across replicas ... then: average (1/world_size),
  * global-norm clip and Adam. */
 int impala_apply_update(impala_learner* h, void* stream);
+/* The same gradients in two parts, so the all-reduce of the first bucket overlaps the rest of
+ * the backward (SURVEY.md §8(e) "2 buckets").  part 0: forward and backward through the conv3
+ * weight gradient; on return (stream order) grads[impala_grad_bucket_offset(h) ..] -- conv3,
+ * LayerNorm, FC and heads -- are final.  part 1 (same batch): the conv2 weight gradient and
+ * conv2 dgrad + conv1 wgrad; then grads[0 .. offset) -- conv1, conv2 -- and the metrics are
+ * final.  part 0 then part 1 give bit-identical grads to impala_compute_grads. */
+int impala_compute_grads_part(impala_learner* h, const impala_batch* batch, int part, void* stream);
+size_t impala_grad_bucket_offset(const impala_learner* h);
 
 /* Replay gather (agents/impala/builder.py:30-36 UniformSampler.sample + learning.py:121-123
  * collate/H2D, done in HBM): for each field f < nfields (<= 8), copy row idx[i] of src[f] to
