@@ -15,9 +15,16 @@ LIB_PATH = os.environ.get("IMPALA_HIP_LIB", os.path.join(_HERE, "libimpala_hip.s
 
 IMPALA_DTYPE_F32 = 0
 IMPALA_DTYPE_BF16 = 1
-NUM_METRICS = 8
+IMPALA_ALGO_IMPALA = 0
+IMPALA_ALGO_PPO = 1
+ABI_VERSION = 2
+NUM_METRICS = 9  # slots 0-6 METRIC_NAMES, 7 step, 8 PPO train/target
 METRIC_NAMES = ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl",
                 "train/ratio", "train/grad_norm")
+# PPOLearner metric keys (losses.py:147-155, agents/ppo/learning.py:136) -> metrics slot
+PPO_METRIC_SLOTS = (("train/loss", 0), ("train/entropy", 1), ("train/td", 2), ("train/pg", 3),
+                    ("train/target", 8), ("train/kl", 4), ("train/ratio", 5),
+                    ("train_step/grad_norm", 6))
 
 # every symbol declared in include/impala_hip.h
 EXPORTS = (
@@ -25,7 +32,7 @@ EXPORTS = (
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
     "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
     "impala_apply_update", "impala_compute_grads_part", "impala_grad_bucket_offset",
-    "impala_vtrace", "impala_loss_head", "impala_kernel_count",
+    "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
 )
 
@@ -37,13 +44,18 @@ class ImpalaConfig(C.Structure):
         ("adam_beta2", C.c_float), ("adam_eps", C.c_float), ("max_grad_norm", C.c_float),
         ("entropy_coeff", C.c_float), ("vtrace_lambda", C.c_float),
         ("clip_rho_threshold", C.c_float), ("clip_pg_rho_threshold", C.c_float),
-        ("world_size", C.c_int),
+        ("world_size", C.c_int), ("algo", C.c_int), ("ppo_clip", C.c_float),
     ]
 
 
 class ImpalaBatch(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("actions", C.c_void_p), ("rewards", C.c_void_p),
                 ("discounts", C.c_void_p), ("behaviour_logits", C.c_void_p)]
+
+
+class ImpalaPpoBatch(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("actions", C.c_void_p), ("targets", C.c_void_p),
+                ("behaviour_logits", C.c_void_p)]
 
 
 _lib = None
@@ -66,6 +78,9 @@ def _declare(lib):
     lib.impala_train_step.argtypes = [_P, C.POINTER(ImpalaBatch), _P]
     lib.impala_compute_grads.argtypes = [_P, C.POINTER(ImpalaBatch), _P]
     lib.impala_apply_update.argtypes = [_P, _P]
+    lib.impala_ppo_train_step.argtypes = [_P, C.POINTER(ImpalaPpoBatch), _P]
+    lib.impala_ppo_loss_head.argtypes = [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_float,
+                                         C.c_float, _P, _P, _P, _P]
     lib.impala_compute_grads_part.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int, _P]
     lib.impala_grad_bucket_offset.argtypes = [_P]
     lib.impala_grad_bucket_offset.restype = C.c_size_t

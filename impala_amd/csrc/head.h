@@ -31,6 +31,7 @@ struct HeadArgs {
   const int64_t* act; const float* rew; const float* disc; const float* mu;
   int B, T, A, S, TPW;  // TPW = trajectories per workgroup = 64 / S
   float lam, crho, cpg, ent_coef;
+  float clip_lo, clip_hi;  // PPO: ratio clamp bounds (1 -+ clip_coeff)
   // outputs
   void* dz;             // T [N][256]
   float* partials;      // [gridDim.x][8] loss partial sums
@@ -44,7 +45,9 @@ constexpr int HEAD_JC = HID / HEAD_SPLIT;  // 64 hidden columns per workgroup in
 
 // grid (groups, HEAD_SPLIT): all HEAD_SPLIT workgroups of a group redo phases 1-2 (cheap: h is an
 // L2 hit and the loss is one wavefront), then each takes a 64-column slice of dz / dWh.
-template <typename T>
+// PPO = true: the PPO clipped-surrogate loss (kernels.h::ppo_frame) on flat transitions (T = 1,
+// one lane per transition, targets in `rew`, `disc` unused) instead of V-trace.
+template <typename T, bool PPO = false>
 __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   using F = Frag<T>;
   typedef typename F::vec V;
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     for (int j = 0; j < MAX_A; ++j) mu[j] = mrow[j < A ? j : A - 1];
     act = (int)a.act[n];
     r = a.rew[n];
-    g = a.disc[n];
+    if constexpr (!PPO) g = a.disc[n];
   }
   // ---- every global load of the kernel is issued here, in one round trip: h rows, this
   // workgroup's z slice, the heads weights (both orientations) and bias ----
@@ -178,31 +181,50 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     }
     rho = fast_exp(logpa - logmua);
     if (!valid) { H = 0.f; kld = 0.f; rho = 0.f; v = 0.f; r = 0.f; g = 0.f; }
-    const float v_n = shift_down1(v);
-    const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
-    const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
-    const float e = seg_rev_scan(aa, td, t, L, S);
-    const float tgt = e + v;
-    const float err = tgt - v;
-    const float tgt_n = shift_down1(tgt);
-    const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
-    const float qq = r + g * boot;
-    const float adv = fminf(a.cpg, rho) * (qq - v);
-    if (valid) {
-      const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T_);
-      const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;
+    if constexpr (PPO) {
+      const PpoFrame pf = ppo_frame(rho, v, r, a.clip_lo, a.clip_hi);
+      if (valid) {
+        const float c = 1.f / (float)a.B, ke = a.ent_coef * c, kr = c * pf.dr * rho;
 #pragma unroll
-      for (int j = 0; j < MAX_A; ++j)
-        if (j < A) dHs[f * LDD + j] = (T)(ke * p[j] * (logp[j] + H) - kp * ((j == act ? 1.f : 0.f) - p[j]));
-      dHs[f * LDD + VCOL] = (T)(inL ? -2.f * c_pg * err : 0.f);
-    }
-    float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
-    s0 = wave_sum(s0); s1 = wave_sum(s1);
-    const float s2 = wave_sum(H), s3 = wave_sum(kld), s4 = wave_sum(rho);
-    if (lane == 0 && lead) {
-      float* pp = a.partials + blockIdx.x * 8;
-      pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
-    }
+        for (int j = 0; j < MAX_A; ++j)
+          if (j < A) dHs[f * LDD + j] = (T)(ke * p[j] * (logp[j] + H) + kr * ((j == act ? 1.f : 0.f) - p[j]));
+        dHs[f * LDD + VCOL] = (T)(-pf.adv * c);
+      }
+      float q[6] = {valid ? pf.pgl : 0.f, valid ? pf.adv * pf.adv : 0.f, H, kld, rho, r};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) q[k] = wave_sum(q[k]);
+      if (lane == 0 && lead) {
+        float* pp = a.partials + blockIdx.x * 8;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) pp[k] = q[k];
+      }
+    } else {
+      const float v_n = shift_down1(v);
+      const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
+      const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
+      const float e = seg_rev_scan(aa, td, t, L, S);
+      const float tgt = e + v;
+      const float err = tgt - v;
+      const float tgt_n = shift_down1(tgt);
+      const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
+      const float qq = r + g * boot;
+      const float adv = fminf(a.cpg, rho) * (qq - v);
+      if (valid) {
+        const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T_);
+        const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;
+#pragma unroll
+        for (int j = 0; j < MAX_A; ++j)
+          if (j < A) dHs[f * LDD + j] = (T)(ke * p[j] * (logp[j] + H) - kp * ((j == act ? 1.f : 0.f) - p[j]));
+        dHs[f * LDD + VCOL] = (T)(inL ? -2.f * c_pg * err : 0.f);
+      }
+      float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
+      s0 = wave_sum(s0); s1 = wave_sum(s1);
+      const float s2 = wave_sum(H), s3 = wave_sum(kld), s4 = wave_sum(rho);
+      if (lane == 0 && lead) {
+        float* pp = a.partials + blockIdx.x * 8;
+        pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
+      }
+    }  // V-trace loss
   }
   __syncthreads();
   // ---- phase 3: dz = gelu'(z) * (dH . Wh)   rows j (256: wave w -> 4 row tiles), cols f ----

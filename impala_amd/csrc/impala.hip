@@ -266,8 +266,14 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     ha.cpg = h->cfg.clip_pg_rho_threshold; ha.ent_coef = h->cfg.entropy_coeff;
     ha.dz = h->dz; ha.partials = h->loss_part; ha.slab_h = h->s_h; ha.slab_bh = h->s_bh;
     ha.heads_out = h->heads;
+    // torch.clamp(ratio, 1 - clip, 1 + clip): the bounds are python floats cast to fp32
+    ha.clip_lo = (float)(1.0 - (double)h->cfg.ppo_clip);
+    ha.clip_hi = (float)(1.0 + (double)h->cfg.ppo_clip);
     timer_begin(h, K_HEAD_STEP, st);
-    head_step_kernel<T><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
+    if (h->cfg.algo == IMPALA_ALGO_PPO)
+      head_step_kernel<T, true><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
+    else
+      head_step_kernel<T><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
     timer_end(h, K_HEAD_STEP, st);
     CK_LAUNCH("head_step");
   }
@@ -419,8 +425,9 @@ int check_bound(impala_learner* h, bool train = true) {
   return 0;
 }
 
-int check_batch(const impala_batch* b) {
-  if (!b || !b->obs || !b->actions || !b->rewards || !b->discounts || !b->behaviour_logits)
+int check_batch(const impala_batch* b, bool ppo = false) {
+  if (!b || !b->obs || !b->actions || !b->rewards || (!ppo && !b->discounts) ||
+      !b->behaviour_logits)
     return fail(IMPALA_E_INVALID, "null batch pointer");
   if (((uintptr_t)b->obs & 15) != 0) return fail(IMPALA_E_INVALID, "obs must be 16-byte aligned");
   return 0;
@@ -449,6 +456,8 @@ int impala_config_default(impala_config* c) {
   c->clip_rho_threshold = 1.f;
   c->clip_pg_rho_threshold = 1.f;
   c->world_size = 1;
+  c->algo = IMPALA_ALGO_IMPALA;
+  c->ppo_clip = 0.1f;
   return 0;
 }
 
@@ -459,8 +468,14 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   if (!cfg || !out) return fail(IMPALA_E_INVALID, "null argument");
   *out = nullptr;
   if (cfg->batch_size < 1) return fail(IMPALA_E_INVALID, "batch_size must be >= 1");
-  if (cfg->rollout_length < 2 || cfg->rollout_length > 64)
+  if (cfg->algo != IMPALA_ALGO_IMPALA && cfg->algo != IMPALA_ALGO_PPO)
+    return fail(IMPALA_E_INVALID, "unknown algo");
+  if (cfg->algo == IMPALA_ALGO_PPO && cfg->rollout_length != 1)
+    return fail(IMPALA_E_UNSUPPORTED, "PPO handles take flat transitions: rollout_length must be 1");
+  if (cfg->algo == IMPALA_ALGO_IMPALA && (cfg->rollout_length < 2 || cfg->rollout_length > 64))
     return fail(IMPALA_E_UNSUPPORTED, "rollout_length must be in [2, 64]");
+  if (!(cfg->ppo_clip >= 0.f && cfg->ppo_clip < 1.f))
+    return fail(IMPALA_E_INVALID, "ppo_clip must be in [0, 1)");
   if (cfg->num_actions < 1 || cfg->num_actions > MAX_A)
     return fail(IMPALA_E_UNSUPPORTED, "num_actions must be in [1, 15]");
   if (cfg->dtype != IMPALA_DTYPE_F32 && cfg->dtype != IMPALA_DTYPE_BF16)
@@ -633,6 +648,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     ra.T = cfg->rollout_length;
     ra.A = h->A;
     ra.ent_coef = cfg->entropy_coeff;
+    ra.algo = cfg->algo;
     ra.step = h->step;
     ra.lr = dec(cfg->lr); ra.b1 = dec(cfg->adam_beta1); ra.b2 = dec(cfg->adam_beta2);
     ra.adam_sc = h->adam_sc;
@@ -778,7 +794,7 @@ enum { G_GRADS = 0, G_UPDATE = 1, G_STEP = 2, G_GRADS0 = 3, G_GRADS1 = 4 };
 
 int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream) {
   if (int r = check_bound(h)) return r;
-  if (int r = check_batch(b)) return r;
+  if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));
   return run_graphed(h, G_GRADS, b, (hipStream_t)stream,
                      [&](hipStream_t s) { return enqueue_grads(h, b, s); });
@@ -787,7 +803,7 @@ int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream)
 int impala_compute_grads_part(impala_learner* h, const impala_batch* b, int part, void* stream) {
   if (part != 0 && part != 1) return fail(IMPALA_E_INVALID, "part must be 0 or 1");
   if (int r = check_bound(h)) return r;
-  if (int r = check_batch(b)) return r;
+  if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));
   return run_graphed(h, part ? G_GRADS1 : G_GRADS0, b, (hipStream_t)stream,
                      [&](hipStream_t s) { return enqueue_grads(h, b, s, part); });
@@ -802,12 +818,19 @@ int impala_apply_update(impala_learner* h, void* stream) {
                      [&](hipStream_t s) { return enqueue_update(h, s); });
 }
 
+int impala_ppo_train_step(impala_learner* h, const impala_ppo_batch* pb, void* stream) {
+  if (!h || !pb) return fail(IMPALA_E_INVALID, "null argument");
+  if (h->cfg.algo != IMPALA_ALGO_PPO) return fail(IMPALA_E_STATE, "not a PPO handle");
+  const impala_batch b{pb->obs, pb->actions, pb->targets, nullptr, pb->behaviour_logits};
+  return impala_train_step(h, &b, stream);
+}
+
 int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (h->cfg.world_size != 1)
     return fail(IMPALA_E_STATE, "world_size > 1: use compute_grads + all-reduce + apply_update");
   if (int r = check_bound(h)) return r;
-  if (int r = check_batch(b)) return r;
+  if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));
   return run_graphed(h, G_STEP, b, (hipStream_t)stream, [&](hipStream_t s) {
     if (int r = enqueue_grads(h, b, s)) return r;
@@ -923,6 +946,33 @@ int impala_loss_head(const float* logits, const float* values, const int64_t* ac
   finalize_loss_kernel<<<1, 64, 0, st>>>(part, wgs, B, T, entropy_coeff, metrics6);
   CK_LAUNCH("finalize_loss");
   CK(hipFreeAsync(part, st));
+  return 0;
+}
+
+int impala_ppo_loss_head(const float* logits, const float* values, const int64_t* actions,
+                         const float* targets, const float* behaviour_logits, int N, int A,
+                         float entropy_coeff, float clip_coeff, float* dlogits, float* dvalues,
+                         float* metrics7, void* stream) {
+  if (N < 1 || A < 1 || A > net::MAX_A) return fail(IMPALA_E_INVALID, "need N >= 1, 1 <= A <= 15");
+  if (!logits || !values || !actions || !targets || !behaviour_logits || !dlogits || !dvalues ||
+      !metrics7)
+    return fail(IMPALA_E_INVALID, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int wgs = cdiv(N, 256);
+  float *part = nullptr, *m9 = nullptr;
+  CK(hipMallocAsync((void**)&part, (size_t)wgs * 8 * 4, st));
+  CK(hipMallocAsync((void**)&m9, IMPALA_NUM_METRICS * 4, st));
+  ppo_loss_head_kernel<<<wgs, 256, 0, st>>>(logits, values, actions, targets, behaviour_logits, N,
+                                            A, entropy_coeff, (float)(1.0 - (double)clip_coeff),
+                                            (float)(1.0 + (double)clip_coeff), dlogits, dvalues,
+                                            part);
+  CK_LAUNCH("ppo_loss_head");
+  finalize_ppo_kernel<<<1, 64, 0, st>>>(part, wgs, N, entropy_coeff, m9);
+  CK_LAUNCH("finalize_ppo");
+  CK(hipMemcpyAsync(metrics7, m9, 6 * 4, hipMemcpyDeviceToDevice, st));
+  CK(hipMemcpyAsync(metrics7 + 6, m9 + IMPALA_M_TARGET, 4, hipMemcpyDeviceToDevice, st));
+  CK(hipFreeAsync(part, st));
+  CK(hipFreeAsync(m9, st));
   return 0;
 }
 

@@ -216,6 +216,121 @@ __global__ void finalize_loss_kernel(const float* part, int nparts, int B, int T
   if (threadIdx.x == 0) finalize_loss_metrics(part, nparts, B, T, ent_coef, metrics);
 }
 
+// =========================================================================================
+// PPO clipped surrogate (losses.py:131-155), per transition:
+//   ratio r = exp(log pi(a) - log pi_ref(a)),  adv = v_target - v
+//   pg_l = max(-adv r, -clamp(r, 1-eps, 1+eps) adv),  loss = mean(pg_l) + 0.5 mean(adv^2)
+//                                                           - c_ent mean(H(pi))
+// adv is detached in pg_l.  d pg_l / d r = -adv w, w = 1 where the unclipped term is the max,
+// clamp'(r) (1 inside [lo, hi], bounds included, else 0) where the clipped term is, and their
+// mean on a tie (torch.max splits the gradient evenly between equal inputs).
+// =========================================================================================
+struct PpoFrame {
+  float adv, pgl, dr;  // advantage, surrogate term, d pg_l / d r
+};
+DEV PpoFrame ppo_frame(float r, float v, float tgt, float lo, float hi) {
+  const float adv = tgt - v;
+  const float l1 = -adv * r, l2 = -fminf(fmaxf(r, lo), hi) * adv;
+  const float inside = (r >= lo && r <= hi) ? 1.f : 0.f;
+  const float w = l1 > l2 ? 1.f : (l1 < l2 ? inside : 0.5f * (1.f + inside));
+  return PpoFrame{adv, fmaxf(l1, l2), -adv * w};
+}
+
+// metrics from PPO partial sums (pg_l, adv^2, H, KL, r, target): slots 0..5 as IMPALA
+// (loss, entropy, td, pg, kl, ratio) and slot 8 = train/target; kl is clamp_min(0)'d
+DEV void finalize_ppo_metrics(const float* part, int nparts, int N, float ent_coef,
+                              float* metrics) {
+  float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < nparts; ++p)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s[k] += part[p * 8 + k];
+  const float c = 1.f / (float)N;
+  const float pg = s[0] * c, td = 0.5f * (s[1] * c), ent = s[2] * c;
+  metrics[0] = pg + td - ent_coef * ent;
+  metrics[1] = ent;
+  metrics[2] = td;
+  metrics[3] = pg;
+  metrics[4] = fmaxf(s[3] * c, 0.f);
+  metrics[5] = s[4] * c;
+  metrics[8] = s[5] * c;
+}
+
+// Standalone PPO loss head on given outputs, one lane per transition (test / reuse entry).
+__global__ __launch_bounds__(256) void ppo_loss_head_kernel(
+    const float* __restrict__ logits, const float* __restrict__ values,
+    const int64_t* __restrict__ act, const float* __restrict__ tgt,
+    const float* __restrict__ mu, int N, int A, float ent_coef, float lo, float hi,
+    float* __restrict__ dl, float* __restrict__ dv, float* __restrict__ partials) {
+  __shared__ float red[4][6];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 256 + threadIdx.x;
+  const bool valid = n0 < N;
+  const int n = valid ? n0 : 0;
+  float lg[MAX_A], mv[MAX_A], p[MAX_A], logp[MAX_A];
+#pragma unroll
+  for (int j = 0; j < MAX_A; ++j) {
+    const int jj = j < A ? j : A - 1;
+    lg[j] = logits[(size_t)n * A + jj];
+    mv[j] = mu[(size_t)n * A + jj];
+  }
+  const int a = (int)act[n];
+  const float v = values[n], t = tgt[n];
+  float m = -INFINITY, mm = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < MAX_A; ++j) {
+    lg[j] = j < A ? lg[j] : -INFINITY;
+    mv[j] = j < A ? mv[j] : -INFINITY;
+    m = fmaxf(m, lg[j]);
+    mm = fmaxf(mm, mv[j]);
+  }
+  float s = 0.f, sm = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAX_A; ++j) {
+    p[j] = j < A ? expf(lg[j] - m) : 0.f;
+    s += p[j];
+    sm += j < A ? expf(mv[j] - mm) : 0.f;
+  }
+  const float lse = m + logf(s), lse_mu = mm + logf(sm), inv_s = 1.f / s;
+  float H = 0.f, kl = 0.f, logpa = 0.f, logmua = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAX_A; ++j) {
+    const bool on = j < A;
+    logp[j] = on ? lg[j] - lse : 0.f;
+    p[j] *= inv_s;
+    const float lmu = on ? mv[j] - lse_mu : 0.f;
+    H -= p[j] * logp[j];
+    kl += p[j] * (logp[j] - lmu);
+    logpa = j == a ? logp[j] : logpa;
+    logmua = j == a ? lmu : logmua;
+  }
+  const float r = expf(logpa - logmua);
+  const PpoFrame pf = ppo_frame(r, v, t, lo, hi);
+  if (valid) {
+    const float c = 1.f / (float)N, ke = ent_coef * c, kr = c * pf.dr * r;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j)
+      if (j < A) dl[(size_t)n * A + j] = ke * p[j] * (logp[j] + H) + kr * ((j == a ? 1.f : 0.f) - p[j]);
+    dv[n] = -pf.adv * c;
+  }
+  float q[6] = {valid ? pf.pgl : 0.f, valid ? pf.adv * pf.adv : 0.f, valid ? H : 0.f,
+                valid ? kl : 0.f, valid ? r : 0.f, valid ? t : 0.f};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) q[k] = wave_sum(q[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) red[wave][k] = q[k];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int k = threadIdx.x;
+    partials[blockIdx.x * 8 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+__global__ void finalize_ppo_kernel(const float* part, int nparts, int N, float ent_coef,
+                                    float* metrics9) {
+  if (threadIdx.x == 0) finalize_ppo_metrics(part, nparts, N, ent_coef, metrics9);
+}
+
 
 // LayerNorm backward + conv3 ReLU mask; per-workgroup partials of d gamma, d beta.
 template <typename T>
@@ -383,6 +498,7 @@ struct RedArgs {
   float* sumsq_part;
   const float* loss_part;
   int n_loss_part, B, T, A;
+  int algo;  // IMPALA_ALGO_*: which loss the partial sums belong to
   float ent_coef;
   float* metrics;
   int64_t* step;
@@ -479,8 +595,12 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
   if (threadIdx.x == 0) a.sumsq_part[wg] = red[0] + red[1] + red[2] + red[3];
-  if (fin && blockIdx.x == 0 && threadIdx.x == 64)
-    finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
+  if (fin && blockIdx.x == 0 && threadIdx.x == 64) {
+    if (a.algo == 1)
+      finalize_ppo_metrics(a.loss_part, a.n_loss_part, a.B * a.T, a.ent_coef, a.metrics);
+    else
+      finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
+  }
   if (fin && blockIdx.x == 0 && threadIdx.x == 128) {  // step += 1 and its bias corrections
     const int64_t t = *a.step + 1;
     *a.step = t;

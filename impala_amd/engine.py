@@ -24,13 +24,18 @@ class Engine:
                  lr: float = 1e-4, eps: float = 1e-5, betas: Tuple[float, float] = (0.9, 0.999),
                  max_grad_norm: float = 0.5, entropy_coeff: float = 0.01, world_size: int = 1,
                  vtrace_lambda: float = 1.0, clip_rho_threshold: float = 1.0,
-                 clip_pg_rho_threshold: float = 1.0, inference_only: bool = False):
+                 clip_pg_rho_threshold: float = 1.0, inference_only: bool = False,
+                 algo: str = "impala", ppo_clip: float = 0.1):
         if model.flat.device.type != "cuda":
             raise RuntimeError("the IMPALA learner runs on the HIP path only (cuda device)")
         self.model = model
         self.device = model.flat.device
+        if algo not in ("impala", "ppo"):
+            raise ValueError(f"unknown algo {algo!r}")
+        self.algo = algo
         self.batch_size = int(batch_size)
-        self.rollout_length = int(rollout_length)
+        # PPO learns from flat transitions (agents/ppo/learning.py:132): N = batch_size
+        self.rollout_length = 1 if algo == "ppo" else int(rollout_length)
         self.num_actions = model.action_dim
         self.inference_only = inference_only
         dtype = dtype or model.compute_dtype
@@ -51,6 +56,8 @@ class Engine:
         cfg.clip_rho_threshold = clip_rho_threshold
         cfg.clip_pg_rho_threshold = clip_pg_rho_threshold
         cfg.world_size = int(world_size)
+        cfg.algo = _lib.IMPALA_ALGO_PPO if algo == "ppo" else _lib.IMPALA_ALGO_IMPALA
+        cfg.ppo_clip = float(ppo_clip)
         self.cfg = cfg
         h = C.c_void_p()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -122,39 +129,50 @@ class Engine:
                                    sp), "impala_forward")
         return logits, values
 
-    def _batch(self, obs, actions, rewards, discounts, mu) -> ImpalaBatch:
+    def _batch(self, *batch) -> ImpalaBatch:
+        """IMPALA: (obs u8 [B,T,3,64,64], actions i64 [B,T], rewards [B,T], discounts [B,T],
+        behaviour logits [B,T,A]).  PPO: (obs u8 [N,3,64,64], actions i64 [N], value targets
+        [N], behaviour logits [N,A]) -- passed to the library with rewards = targets."""
         B, T, A = self.batch_size, self.rollout_length, self.num_actions
-        exp = {"obs": ((B, T, 3, 64, 64), torch.uint8), "actions": ((B, T), torch.int64),
-               "rewards": ((B, T), torch.float32), "discounts": ((B, T), torch.float32),
-               "behaviour_logits": ((B, T, A), torch.float32)}
-        got = {"obs": obs, "actions": actions, "rewards": rewards, "discounts": discounts,
-               "behaviour_logits": mu}
-        for k, (shape, dt) in exp.items():
-            t = got[k]
+        if self.algo == "ppo":
+            names = ("obs", "actions", "targets", "behaviour_logits")
+            exp = (((B, 3, 64, 64), torch.uint8), ((B,), torch.int64), ((B,), torch.float32),
+                   ((B, A), torch.float32))
+        else:
+            names = ("obs", "actions", "rewards", "discounts", "behaviour_logits")
+            exp = (((B, T, 3, 64, 64), torch.uint8), ((B, T), torch.int64),
+                   ((B, T), torch.float32), ((B, T), torch.float32), ((B, T, A), torch.float32))
+        if len(batch) != len(names):
+            raise ValueError(f"{self.algo} batch is {names}, got {len(batch)} tensors")
+        for k, t, (shape, dt) in zip(names, batch, exp):
             if tuple(t.shape) != shape or t.dtype != dt:
                 raise ValueError(f"{k}: expected {dt} {shape}, got {t.dtype} {tuple(t.shape)}")
             if t.device != self.device or not t.is_contiguous():
                 raise ValueError(f"{k}: must be a contiguous tensor on {self.device}")
-        return ImpalaBatch(ptr(obs), ptr(actions), ptr(rewards), ptr(discounts), ptr(mu))
+        if self.algo == "ppo":
+            obs, actions, targets, mu = batch
+            return ImpalaBatch(ptr(obs), ptr(actions), ptr(targets), None, ptr(mu))
+        return ImpalaBatch(*[ptr(t) for t in batch])
 
-    def train_step(self, obs, actions, rewards, discounts, mu, stream=None):
-        """Full update (world_size 1): learning.py:140-177."""
-        b = self._batch(obs, actions, rewards, discounts, mu)
+    def train_step(self, *batch, stream=None):
+        """Full update (world_size 1): IMPALA learning.py:140-177, PPO
+        agents/ppo/learning.py:131-143 (the batch layout follows the handle's algo)."""
+        b = self._batch(*batch)
         self._sync_weights(stream)
         check(_lib.lib().impala_train_step(self._h, C.byref(b), stream_ptr(stream)),
               "impala_train_step")
         self._updated()
 
-    def compute_grads(self, obs, actions, rewards, discounts, mu, stream=None):
-        b = self._batch(obs, actions, rewards, discounts, mu)
+    def compute_grads(self, *batch, stream=None):
+        b = self._batch(*batch)
         self._sync_weights(stream)
         check(_lib.lib().impala_compute_grads(self._h, C.byref(b), stream_ptr(stream)),
               "impala_compute_grads")
 
-    def compute_grads_part(self, part, obs, actions, rewards, discounts, mu, stream=None):
+    def compute_grads_part(self, part, *batch, stream=None):
         """Half of compute_grads: part 0 finishes grads[bucket_offset:] (conv3 .. heads),
         part 1 (same batch) finishes grads[:bucket_offset] (conv1, conv2) and the metrics."""
-        b = self._batch(obs, actions, rewards, discounts, mu)
+        b = self._batch(*batch)
         if part == 0:
             self._sync_weights(stream)
         check(_lib.lib().impala_compute_grads_part(self._h, C.byref(b), int(part),
@@ -235,6 +253,23 @@ def loss_head(logits, values, actions, rewards, discounts, mu, entropy_coeff=0.0
                                       ptr(dv), ptr(met), ptr(adv), ptr(err), ptr(q), ptr(rho),
                                       stream_ptr(stream)), "impala_loss_head")
     return dict(dlogits=dl, dvalues=dv, metrics=met, adv=adv, err=err, q=q, rho=rho)
+
+
+def ppo_loss_head(logits, values, actions, targets, mu, entropy_coeff=0.01, clip_coeff=0.1,
+                  stream=None):
+    """PPO loss head (losses.py:131-155) on device tensors [N, A] / [N]; returns a dict with
+    dlogits, dvalues and metrics (loss, entropy, td, pg, kl, ratio, target)."""
+    N, A = logits.shape
+    f = lambda t: t.contiguous().to(torch.float32)  # noqa: E731
+    lg, v, t, m = f(logits), f(values).reshape(N), f(targets).reshape(N), f(mu)
+    a = actions.contiguous().to(torch.int64).reshape(N)
+    dl = torch.empty_like(lg)
+    dv = torch.empty_like(v)
+    met = torch.empty(7, dtype=torch.float32, device=lg.device)
+    check(_lib.lib().impala_ppo_loss_head(ptr(lg), ptr(v), ptr(a), ptr(t), ptr(m), N, A,
+                                          entropy_coeff, clip_coeff, ptr(dl), ptr(dv), ptr(met),
+                                          stream_ptr(stream)), "impala_ppo_loss_head")
+    return dict(dlogits=dl, dvalues=dv, metrics=met)
 
 
 def gather_rollouts(fields, idx, stream=None):

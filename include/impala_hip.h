@@ -7,6 +7,8 @@
  *                          (forward, Categorical log-prob / ratio, batched V-trace, pg/value/
  *                          entropy loss, backward, clip_grad_norm_(0.5), Adam.step)
  *   impala_compute_grads   learning.py:141-170 (zero_grad .. loss.backward + metrics)
+ *   impala_ppo_train_step  agents/ppo/learning.py:131-143  PPOLearner._train_step
+ *                          (losses.py:131-155 ppo_loss, backward, clip, Adam)
  *   impala_apply_update    learning.py:172-176 (clip_grad_norm_ + optimizer.step), after the
  *                          caller's gradient all-reduce in the data-parallel learner
  *   impala_forward         models/distributed_models.py:17-19 AtariPPOModel.forward
@@ -43,7 +45,7 @@
 extern "C" {
 #endif
 
-#define IMPALA_ABI_VERSION 1
+#define IMPALA_ABI_VERSION 2
 
 #define IMPALA_OK 0
 #define IMPALA_E_INVALID 1001   /* bad argument / shape */
@@ -62,7 +64,11 @@ extern "C" {
 #define IMPALA_M_RATIO 5
 #define IMPALA_M_GRAD_NORM 6
 #define IMPALA_M_STEP 7
-#define IMPALA_NUM_METRICS 8
+#define IMPALA_M_TARGET 8       /* PPO only: train/target (losses.py:150) */
+#define IMPALA_NUM_METRICS 9
+
+#define IMPALA_ALGO_IMPALA 0    /* V-trace actor-critic (agents/impala/learning.py:140-177) */
+#define IMPALA_ALGO_PPO 1       /* PPO clipped surrogate (agents/ppo/learning.py:131-143) */
 
 typedef struct impala_learner impala_learner;
 
@@ -78,6 +84,8 @@ typedef struct {
   float clip_rho_threshold;    /* rlego default 1.0                                          */
   float clip_pg_rho_threshold; /* rlego default 1.0                                          */
   int world_size;              /* data-parallel replicas (gradient average divisor)          */
+  int algo;                    /* IMPALA_ALGO_*; PPO needs rollout_length 1 (flat transitions) */
+  float ppo_clip;              /* losses.py:131 clip_coeff 0.1                               */
 } impala_config;
 
 typedef struct {
@@ -88,6 +96,15 @@ typedef struct {
   const float* behaviour_logits;
 } impala_batch;
 
+/* PPO transitions (agents/ppo/learning.py:132): obs [N][3][64][64], actions [N], value
+ * targets [N], behaviour (reference-policy) logits [N][A]; N = batch_size. */
+typedef struct {
+  const uint8_t* obs;
+  const int64_t* actions;
+  const float* targets;
+  const float* behaviour_logits;
+} impala_ppo_batch;
+
 int impala_abi_version(void);
 const char* impala_last_error(void);
 int impala_config_default(impala_config* cfg);
@@ -97,7 +114,8 @@ size_t impala_param_count(int num_actions);
 int impala_create(const impala_config* cfg, int device, impala_learner** out);
 int impala_destroy(impala_learner* h);
 
-/* Bind caller-owned device buffers (each impala_param_count() floats; metrics 8 floats).
+/* Bind caller-owned device buffers (each impala_param_count() floats; metrics
+ * IMPALA_NUM_METRICS floats).
  * Only `params` is required for impala_forward (inference-only handles); the training calls
  * need all five.
  * The library reads/writes them in place: params and Adam moments are updated by
@@ -115,6 +133,11 @@ int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, 
 
 /* Full learner update for one batch (world_size must be 1). */
 int impala_train_step(impala_learner* h, const impala_batch* batch, void* stream);
+/* PPOLearner._train_step (agents/ppo/learning.py:131-143) on an IMPALA_ALGO_PPO handle:
+ * forward, ppo_loss, backward, clip_grad_norm_, Adam; metrics slots 0-8 (slot 8 = target).
+ * The data-parallel calls (impala_compute_grads*, impala_apply_update) take the same batch
+ * as an impala_batch with rewards = targets and discounts unused. */
+int impala_ppo_train_step(impala_learner* h, const impala_ppo_batch* batch, void* stream);
 /* Data-parallel split: gradients of the local batch into `grads` (local mean) ... */
 int impala_compute_grads(impala_learner* h, const impala_batch* batch, void* stream);
 /* ... caller all-reduces (sums) `grads` across replicas ... then: average (1/world_size),
@@ -157,6 +180,13 @@ int impala_loss_head(const float* logits, const float* values, const int64_t* ac
                      int B, int T, int A, float entropy_coeff, float lambda_, float clip_rho,
                      float clip_pg_rho, float* dlogits, float* dvalues, float* metrics6,
                      float* adv, float* err, float* q, float* rho, void* stream);
+
+/* Standalone PPO loss head (losses.py:131-155) given outputs: logits [N][A], values [N].
+ * Writes dlogits [N][A], dvalues [N] and metrics7 (loss, entropy, td, pg, kl, ratio, target). */
+int impala_ppo_loss_head(const float* logits, const float* values, const int64_t* actions,
+                         const float* targets, const float* behaviour_logits, int N, int A,
+                         float entropy_coeff, float clip_coeff, float* dlogits, float* dvalues,
+                         float* metrics7, void* stream);
 
 #ifdef __cplusplus
 }

@@ -264,3 +264,84 @@ def loss_from_outputs(logits, values, act, rew, disc, mu, entropy_coeff=0.01,
                entropy=float(ent.detach()), kl=float(kl.detach()), ratio=float(rho.detach().mean()),
                dlogits=lg.grad.numpy().copy(), dvalues=v.grad.numpy().copy())
     return out
+
+
+# ------------------------------------------------------------------------------------- PPO
+# SURVEY.md §8(f) row 3.  PPOLearner._train_step (agents/ppo/learning.py:131-143) calls
+# losses.ppo_loss (losses.py:131-155) with entropy_cost = the learner's entropy_coeff (0.01:
+# PPOBuilder.make_learner passes no cfg, agents/ppo/builder.py:44-47), clip_coeff 0.1, then
+# backward, clip_grad_norm_(0.5), Adam.step, zero_grad.  Batch = flat transitions:
+# s u8 (N,3,64,64), a i64 (N,), v_target f32 (N,), pi_ref logits f32 (N,A).
+
+def ppo_loss(model: nn.Module, batch, entropy_cost: float = 0.01, clip_coeff: float = 0.1):
+    """losses.py:131-155 restated."""
+    s, a, v_target, pi_ref = batch
+    pi_tm1, v_tm1 = model(s)
+    pi_tm1 = torch.distributions.Categorical(logits=pi_tm1)
+    pi_ref = torch.distributions.Categorical(logits=pi_ref)
+    ratio = torch.exp(pi_tm1.log_prob(a) - pi_ref.log_prob(a))
+    adv = v_target - v_tm1.squeeze(-1)
+    td_loss = 0.5 * adv.pow(2).mean()
+    adv = adv.detach()
+    pg_loss_1 = -(adv * ratio)
+    pg_loss_2 = -torch.clamp(ratio, 1 - clip_coeff, 1 + clip_coeff) * adv
+    pg_loss = torch.max(pg_loss_1, pg_loss_2).mean()
+    kl = torch.distributions.kl_divergence(pi_tm1, pi_ref).mean().clamp_min(0.)
+    entropy = pi_tm1.entropy().mean()
+    loss = pg_loss + td_loss - entropy_cost * entropy
+    return loss, {
+        "train/loss": loss.detach(), "train/entropy": entropy.detach(),
+        "train/td": td_loss.detach(), "train/pg": pg_loss.detach(),
+        "train/target": v_target.mean().detach(), "train/kl": kl.detach(),
+        "train/ratio": ratio.mean().detach(),
+    }
+
+
+def ppo_train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
+                   max_grad_norm: float = 0.5, entropy_coeff: float = 0.01,
+                   clip_coeff: float = 0.1) -> Dict[str, torch.Tensor]:
+    """agents/ppo/learning.py:131-143 restated (the reference zeroes grads after the step)."""
+    loss, metrics = ppo_loss(model, batch, entropy_cost=entropy_coeff, clip_coeff=clip_coeff)
+    loss.backward()
+    metrics["train_step/grad_norm"] = torch.nn.utils.clip_grad_norm_(model.parameters(),
+                                                                     max_grad_norm)
+    optimizer.step()
+    optimizer.zero_grad()
+    return metrics
+
+
+class _Outputs(nn.Module):
+    """A 'model' returning fixed (logits, values) leaves, to run ppo_loss on given outputs."""
+
+    def __init__(self, logits, values):
+        super().__init__()
+        self.lg, self.v = logits, values
+
+    def forward(self, s):
+        return self.lg, self.v
+
+
+def ppo_loss_from_outputs(logits, values, act, target, pi_ref, entropy_coeff=0.01,
+                          clip_coeff=0.1):
+    """ppo_loss given the network outputs: metrics and d loss / d (logits, values)."""
+    lg = torch.tensor(logits, dtype=torch.float32, requires_grad=True)
+    v = torch.tensor(values, dtype=torch.float32, requires_grad=True)
+    batch = (None, torch.from_numpy(np.asarray(act, dtype=np.int64)),
+             torch.from_numpy(np.asarray(target, dtype=np.float32)),
+             torch.from_numpy(np.asarray(pi_ref, dtype=np.float32)))
+    loss, met = ppo_loss(_Outputs(lg, v), batch, entropy_cost=entropy_coeff,
+                         clip_coeff=clip_coeff)
+    loss.backward()
+    return {k.split("/")[1]: float(x) for k, x in met.items()}, lg.grad.numpy(), v.grad.numpy()
+
+
+def synthetic_ppo_batch(N: int, A: int = 15, seed: int = 4321, ratio_spread: float = 0.3):
+    """Flat PPO transitions: obs u8 uniform, a ~ U[0,A), v_target ~ N(0,1), pi_ref logits
+    ~ N(0,1).  (The reference actor's target computation, agents/ppo/learning.py:64-69,
+    cannot run: it references an undefined ``values``)"""
+    rng = np.random.default_rng(seed)
+    obs = rng.integers(0, 256, size=(N, 3, 64, 64), dtype=np.uint8)
+    act = rng.integers(0, A, size=(N,), dtype=np.int64)
+    tgt = rng.standard_normal(N).astype(np.float32)
+    mu = (ratio_spread * rng.standard_normal((N, A))).astype(np.float32)
+    return obs, act, tgt, mu

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     lib = _lib.lib()
-    assert lib.impala_abi_version() == 1
+    assert lib.impala_abi_version() == _lib.ABI_VERSION == 2
     assert _lib.param_count(15) == 344496
     assert _lib.param_count(6) == 344496 - 9 * 257
     cfg = _lib.default_config()
@@ -48,7 +48,8 @@ def test_host_only_entry_points():
 
 @pytest.mark.parametrize("field,value", [("batch_size", 0), ("rollout_length", 1),
                                          ("rollout_length", 65), ("num_actions", 16),
-                                         ("num_actions", 0), ("dtype", 7), ("world_size", 0)])
+                                         ("num_actions", 0), ("dtype", 7), ("world_size", 0),
+                                         ("algo", 5), ("ppo_clip", 1.5)])
 def test_create_rejects_bad_config_without_touching_the_device(field, value):
     lib = _lib.lib()
     cfg = _lib.default_config()

@@ -100,3 +100,45 @@ def test_vtrace_known_answers():
     # rho == 0  =>  err == 0 and adv == 0
     adv, err, q = ovt.vtrace_numpy(v_tm1, v_t, r, g, np.zeros((B, L)))
     assert np.all(err == 0) and np.all(adv == 0)
+
+
+# ------------------------------------------------------------------------------------- PPO
+PPO_KEYS = ("loss", "entropy", "td", "pg", "target", "kl", "ratio")
+
+
+def test_ppo_head_matches_reference():
+    """ppo_loss (losses.py:131-155) restated vs the reference on given outputs."""
+    d = _load("ppo_head.npz")
+    met, dl, dv = ref_cpu.ppo_loss_from_outputs(d["logits"], d["values"], d["act"],
+                                                d["target"], d["mu"])
+    np.testing.assert_allclose([met[k] for k in PPO_KEYS], d["scalars"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(dl, d["dlogits"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(dv, d["dvalues"], rtol=1e-5, atol=1e-9)
+    r = d["ratio"]
+    assert (r < 0.9).any() and (r > 1.1).any() and ((r >= 0.9) & (r <= 1.1)).any()
+
+
+def test_ppo_train_steps_match_reference():
+    """PPOLearner._train_step (agents/ppo/learning.py:131-143) restated, 3 steps."""
+    d = _load("ppo_train_step.npz")
+    m = ref_cpu.RefModel()
+    ref_cpu.load_flat(m, d["params0"])
+    opt = ref_cpu.make_optimizer(m)
+    snaps = []
+    orig = opt.step
+
+    def step(*a, **k):
+        snaps.append(ref_cpu.flat_grads(m))
+        return orig(*a, **k)
+
+    opt.step = step
+    for i in range(3):
+        b = [torch.from_numpy(d[f"{k}{i}"]) for k in ("obs", "act", "tgt", "mu")]
+        met = ref_cpu.ppo_train_step(m, opt, b)
+        got = [float(met[f"train/{k}"]) for k in PPO_KEYS] + [float(met["train_step/grad_norm"])]
+        exp = [float(d[k][i]) for k in PPO_KEYS + ("grad_norm",)]
+        np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-7, err_msg=f"step {i}")
+        if i == 0:
+            np.testing.assert_allclose(snaps[0], d["grads1"], rtol=1e-4, atol=1e-8)
+            np.testing.assert_allclose(ref_cpu.flat_params(m), d["params1"], rtol=0, atol=1e-7)
+    np.testing.assert_allclose(ref_cpu.flat_params(m), d["params3"], rtol=0, atol=1e-7)
