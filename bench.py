@@ -77,6 +77,37 @@ def synthetic_batch(B, T, A, seed, device):
     return [torch.from_numpy(x).to(device) for x in (obs, act, rew, disc, mu)]
 
 
+def synthetic_ppo_batch(N, A, seed, device):
+    """PPO transitions: obs u8 uniform, a ~ U[0,A), v_target ~ N(0,1), pi_ref ~ 0.3 N(0,1)."""
+    rng = np.random.default_rng(seed)
+    obs = rng.integers(0, 256, size=(N, 3, 64, 64), dtype=np.uint8)
+    act = rng.integers(0, A, size=(N,), dtype=np.int64)
+    tgt = rng.standard_normal(N).astype(np.float32)
+    mu = (0.3 * rng.standard_normal((N, A))).astype(np.float32)
+    return [torch.from_numpy(x).to(device) for x in (obs, act, tgt, mu)]
+
+
+def cpu_baseline_ppo(N, A, seconds):
+    """The reference PPO learner (oracle port of agents/ppo/learning.py:130-143)."""
+    from oracle import ref_cpu
+    threads = torch.get_num_threads()
+    batch = [torch.from_numpy(x) for x in ref_cpu.synthetic_ppo_batch(N, A, seed=4321)]
+    model = ref_cpu.make_model(0, A)
+    opt = ref_cpu.make_optimizer(model)
+    for _ in range(2):
+        ref_cpu.ppo_train_step(model, opt, batch)
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        ref_cpu.ppo_train_step(model, opt, batch)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": N / med, "unit": "env-frames/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} oracle PPO learner steps (N={N}, fp32 torch-CPU, "
+                      f"{threads} threads) after 2 warm-up; median step {med * 1e3:.1f} ms"}
+
+
 def cpu_baseline(B, T, A, seconds):
     """The reference CPU learner (oracle port of learning.py:140-177), timed on host cores."""
     from oracle import ref_cpu
@@ -145,7 +176,15 @@ def main():
     ap.add_argument("--roofline-kernel", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--algo", default="impala", choices=["impala", "ppo"],
+                    help="ppo: PPO learner step (BASELINE config 4) on --batch transitions "
+                         "(default 256, conf/agent/ppo.yaml)")
     args = ap.parse_args()
+    ppo = args.algo == "ppo"
+    if ppo:
+        if args.batch == 64:
+            args.batch = 256
+        args.rollout = 1
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -165,9 +204,13 @@ def main():
 
     B, T, A = args.batch, args.rollout, args.actions
     model = AtariPPOModel((3, 64, 64), A, device=dev, dtype=args.dtype, seed=0)
-    eng = Engine(model, batch_size=B, rollout_length=T, world_size=world)
+    eng = Engine(model, batch_size=B, rollout_length=T, world_size=world,
+                 algo=args.algo)
     model._train_engine = eng
-    batch = synthetic_batch(B, T, A, 1234 + rank, dev)
+    if ppo:
+        batch = synthetic_ppo_batch(B, A, 4321 + rank, dev)
+    else:
+        batch = synthetic_batch(B, T, A, 1234 + rank, dev)
     if dist is not None:  # identical initial weights on every replica
         dist.broadcast(model.flat, 0)
         model.params_changed()
@@ -233,15 +276,20 @@ def main():
     traffic, tsrc = profiled_traffic(rk, args.dtype)
     traffic_src = (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+WRITE_SIZE, "
                    "bytes per launch)") if tsrc else None
+    metric = "learner env-frames/sec (IMPALA procgen T=20 B=64) at 1/2/4/8 MI355X"
+    workload = f"IMPALA procgen learner step, NatureCNN actor-critic, B={B}/GPU T={T} A={A}, " \
+               f"global B={B * world}"
+    if ppo:
+        metric = "PPO learner transitions/sec (procgen, NatureCNN, BASELINE config 4)"
+        workload = f"PPO learner step (clip 0.1), NatureCNN actor-critic, N={B} transitions/GPU"
     out = {
-        "metric": "learner env-frames/sec (IMPALA procgen T=20 B=64) at 1/2/4/8 MI355X",
+        "metric": metric,
         "value": round(value, 1), "unit": "env-frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic rollouts resident in HBM (obs u8 uniform, BASELINE.md §3); "
                 "random-init weights (reference layer_init_truncated, seed 0)",
-        "config": {"workload": f"IMPALA procgen learner step, NatureCNN actor-critic, "
-                               f"B={B}/GPU T={T} A={A}, global B={B * world}",
+        "config": {"workload": workload,
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
         "roofline": {"bound": bound, "kernel": rk, "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
@@ -254,7 +302,8 @@ def main():
     if probe:
         out["kernel_probe_us"] = {k: round(v * 1e3, 2) for k, v in sorted(probe.items(), key=lambda kv: -kv[1])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(B, T, A, args.cpu_seconds)
+        out["cpu_baseline"] = (cpu_baseline_ppo(B, A, args.cpu_seconds) if ppo
+                               else cpu_baseline(B, T, A, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -140,3 +140,44 @@ class ImpalaBuilder(Builder):
         self._actor_model = actor_model
         model.downstream = actor_model  # push() publishes the learner weights here
         return model
+
+
+class PPOBuilder(Builder):
+    """agents/ppo/builder.py:24-53 on the HIP learner."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self._learner_model = None
+        self._actor_model = None
+
+    def make_replay(self):  # builder.py:30-36: CircularBuffer(size, torch.cat) + UniformSampler
+        return ReplayBuffer(self.cfg.agent.replay_buffer_size, seed=self.cfg.training.seed)
+
+    def make_actor(self, model, rb=None, deterministic: bool = False):  # builder.py:38-39
+        # PPOActorRemote._make_replay (agents/ppo/learning.py:65-69) references an undefined
+        # `values`; the actor side is out of scope here (SURVEY.md §2 rows 12-14)
+        raise NotImplementedError("PPO actors are not part of the MI355X learner path")
+
+    def make_learner(self, model, rb):  # builder.py:41-44: PPOLearner(model, rb, optimizer)
+        from impala_amd.ppo import PPOLearner
+        opt = ImpalaAdam(lr=float(self.cfg.agent.optimizer.lr),
+                         eps=float(self.cfg.agent.optimizer.eps))
+        dtype = None
+        lc = self.cfg.get("learner", {}) if isinstance(self.cfg, dict) else getattr(self.cfg, "learner", {})
+        if lc:
+            dtype = lc.get("dtype", None)
+        # the reference passes no cfg to the learner: constructor defaults (batch 256, clip 0.5,
+        # entropy 0.01, push period 8) apply, whatever conf/agent/ppo.yaml says
+        return PPOLearner(self._learner_model if model is None else model, rb, opt, dtype=dtype)
+
+    def make_network(self, env_spec=None):  # builder.py:46-53
+        obs_shape, n_act = (3, 64, 64), 15
+        if env_spec is not None:
+            obs_shape = tuple(env_spec.observation_space.shape)
+            n_act = int(env_spec.action_space.n)
+        model = AtariPPOModel(obs_shape, n_act, device=self.cfg.distributed.train_device,
+                              dtype="fp32")
+        self._learner_model = model
+        self._actor_model = model.clone_to(self.cfg.distributed.infer_device)
+        model.downstream = self._actor_model
+        return model

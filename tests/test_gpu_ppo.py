@@ -153,3 +153,37 @@ def test_ppo_grad_parts_match_whole():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(m2.flat_grad.cpu().numpy(), g)
     np.testing.assert_array_equal(e2.metrics.cpu().numpy(), met)
+
+
+def test_ppo_learner_interface_matches_reference():
+    """PPOLearner.train_step (agents/ppo/learning.py:110-143) through the host replay: same
+    metric keys, and the step equals the oracle's on the sampled transitions."""
+    from impala_amd.model import AtariPPOModel
+    from impala_amd.ppo import PPOLearner
+    from impala_amd.replay import ReplayBuffer
+    dev = _dev()
+    N = 32
+    obs, act, tgt, mu = ref_cpu.synthetic_ppo_batch(N, 15, seed=12)
+    rb = ReplayBuffer(100, seed=0)
+    for i in range(N):  # transition items as the reference actor stores them (leading dim 1)
+        rb.append([torch.from_numpy(obs[i:i + 1]), torch.from_numpy(act[i:i + 1]),
+                   torch.from_numpy(tgt[i:i + 1]), torch.from_numpy(mu[i:i + 1])])
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+    ref = ref_cpu.RefModel(15)
+    ref_cpu.load_flat(ref, m.flat.cpu().numpy())
+    learner = PPOLearner(m, rb, torch.optim.Adam(ref.parameters(), lr=1e-4, eps=1e-5),
+                         batch_size=N, learning_starts=N)
+    learner.prepare()
+    assert learner.can_train
+    out = learner.train_step()
+    keys = {"train/loss", "train/entropy", "train/td", "train/pg", "train/target", "train/kl",
+            "train/ratio", "train_step/grad_norm", "debug/replay_sample_per_second",
+            "debug/gradient_per_second", "debug/total_time", "debug/forward_dt",
+            "debug/update_time"}
+    assert set(out) == keys
+    # the oracle on the same (uniformly sampled, permuted) transitions: metrics are means, so
+    # any permutation of all N transitions gives the same values
+    opt = ref_cpu.make_optimizer(ref)
+    exp = ref_cpu.ppo_train_step(ref, opt, [torch.from_numpy(x) for x in (obs, act, tgt, mu)])
+    for k in keys - {k for k in keys if k.startswith("debug/")}:
+        np.testing.assert_allclose(float(out[k]), float(exp[k]), rtol=2e-4, atol=1e-6, err_msg=k)

@@ -131,3 +131,24 @@ def test_shard_range():
     assert shard_range(512, 8, 3) == (192, 256)
     with pytest.raises(ValueError):
         shard_range(10, 4, 0)
+
+
+def test_ppo_collate_transitions_matches_torch_cat():
+    """CircularBuffer(collate_fn=torch.cat) semantics (agents/ppo/builder.py:30-35)."""
+    import torch
+    from impala_amd.ppo import collate_transitions
+    rng = np.random.default_rng(0)
+    items = []
+    for i in range(5):
+        items.append([torch.from_numpy(rng.integers(0, 256, (1, 3, 64, 64), dtype=np.uint8)),
+                      torch.tensor([i % 3]), torch.tensor([0.5 * i]),
+                      torch.from_numpy(rng.standard_normal((1, 15)).astype(np.float32))])
+    s, a, t, mu = collate_transitions(items, torch.device("cpu"))
+    assert s.shape == (5, 3, 64, 64) and s.dtype == torch.uint8
+    assert a.tolist() == [0, 1, 2, 0, 1] and a.dtype == torch.int64
+    assert t.tolist() == [0.0, 0.5, 1.0, 1.5, 2.0]
+    assert torch.equal(mu, torch.cat([x[3] for x in items]))
+    # items without the leading dim collate the same way
+    s2, a2, t2, mu2 = collate_transitions([[x[0][0], x[1][0], x[2][0], x[3][0]] for x in items],
+                                          torch.device("cpu"))
+    assert torch.equal(s2, s) and torch.equal(a2, a) and torch.equal(t2, t) and torch.equal(mu2, mu)
