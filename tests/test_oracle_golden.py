@@ -142,3 +142,42 @@ def test_ppo_train_steps_match_reference():
             np.testing.assert_allclose(snaps[0], d["grads1"], rtol=1e-4, atol=1e-8)
             np.testing.assert_allclose(ref_cpu.flat_params(m), d["params1"], rtol=0, atol=1e-7)
     np.testing.assert_allclose(ref_cpu.flat_params(m), d["params3"], rtol=0, atol=1e-7)
+
+
+# ------------------------------------------------------------------------------------- SAC
+SAC_METRICS = ("qf1_loss", "qf2_loss", "qf1", "qf2", "qf_loss", "critic_grad_norm",
+               "actor_loss", "actor_std", "actor_grad_norm", "alpha_loss", "alpha")
+
+
+def _sac_batch(d, i):
+    return (torch.from_numpy(d[f"s{i}"]), torch.from_numpy(d[f"a{i}"]), torch.from_numpy(d[f"r{i}"]),
+            torch.from_numpy(d[f"s1{i}"]), torch.from_numpy(d[f"d{i}"]))
+
+
+def test_sac_train_steps_match_reference():
+    """SACLearner.train_step (agents/sac/learning.py:146-193) restated, 3 steps, with the
+    reference's recorded rsample noise."""
+    from oracle import sac_cpu
+    d = _load("sac_train_step.npz")
+    actor, critic = sac_cpu.make_models(17, 6, seed=0)
+    # seed-0 init is the reference's (critic then actor, layer_init_uniform)
+    np.testing.assert_array_equal(sac_cpu.flat(actor.parameters()), d["actor0"])
+    np.testing.assert_array_equal(sac_cpu.flat(critic.critic.parameters()), d["critic0"])
+    np.testing.assert_array_equal(sac_cpu.flat(critic.target_critic.parameters()), d["target0"])
+    st = sac_cpu.SACState(actor, critic)
+    for i in range(3):
+        eps = [torch.from_numpy(d[f"eps{i}"][j]) for j in range(3)]
+        met = sac_cpu.train_step(st, _sac_batch(d, i), torch.from_numpy(d[f"probs{i}"]), eps)
+        got = [float(met[f"train/{k}"].detach()) for k in SAC_METRICS]
+        np.testing.assert_allclose(got, [float(d[k][i]) for k in SAC_METRICS], rtol=1e-5,
+                                   atol=1e-6, err_msg=f"step {i}")
+        if i in (0, 2):
+            t = i + 1
+            np.testing.assert_allclose(sac_cpu.flat(actor.parameters()), d[f"actor{t}"], atol=1e-6)
+            np.testing.assert_allclose(sac_cpu.flat(critic.critic.parameters()), d[f"critic{t}"],
+                                       atol=1e-6)
+            np.testing.assert_allclose(sac_cpu.flat(critic.target_critic.parameters()),
+                                       d[f"target{t}"], atol=1e-6)
+            np.testing.assert_allclose(sac_cpu.flat(st.target_actor.parameters()), d[f"tactor{t}"],
+                                       atol=1e-6)
+            np.testing.assert_allclose(float(critic.log_alpha), float(d[f"log_alpha{t}"]), atol=1e-7)
