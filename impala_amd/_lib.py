@@ -35,6 +35,20 @@ EXPORTS = (
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
 )
+# every symbol declared in include/sac_hip.h
+SAC_EXPORTS = (
+    "sac_config_default", "sac_actor_param_count", "sac_critic_param_count", "sac_create",
+    "sac_destroy", "sac_bind_state", "sac_refresh_weights", "sac_set_steps", "sac_train_step",
+    "sac_act", "sac_policy", "sac_q_forward", "sac_phase_count", "sac_phase_name",
+    "sac_timer_start", "sac_timer_read", "sac_sample",
+)
+SAC_NUM_METRICS = 12
+# SACLearner metric keys (agents/sac/learning.py:206,220,243-265) -> metrics slot
+SAC_CRITIC_METRICS = (("train/qf1_loss", 0), ("train/qf2_loss", 1), ("train/qf1", 2),
+                      ("train/qf2", 3), ("train/qf_loss", 4), ("train/critic_grad_norm", 5))
+SAC_ACTOR_METRICS = (("train/actor_loss", 6), ("train/actor_std", 7),
+                     ("train/actor_grad_norm", 8))
+SAC_ALPHA_METRICS = (("train/alpha_loss", 9), ("train/alpha", 10))
 
 
 class ImpalaConfig(C.Structure):
@@ -56,6 +70,28 @@ class ImpalaBatch(C.Structure):
 class ImpalaPpoBatch(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("actions", C.c_void_p), ("targets", C.c_void_p),
                 ("behaviour_logits", C.c_void_p)]
+
+
+class SacConfig(C.Structure):
+    _fields_ = [
+        ("obs_dim", C.c_int), ("act_dim", C.c_int), ("batch_size", C.c_int), ("dtype", C.c_int),
+        ("critic_lr", C.c_float), ("actor_lr", C.c_float), ("adam_beta1", C.c_float),
+        ("adam_beta2", C.c_float), ("adam_eps", C.c_float), ("max_grad_norm", C.c_float),
+        ("tau", C.c_float), ("gamma", C.c_float), ("tune_alpha", C.c_int),
+        ("target_entropy", C.c_float), ("prio_exponent", C.c_float), ("seed", C.c_uint64),
+    ]
+
+
+class SacBatch(C.Structure):
+    _fields_ = [("s", C.c_void_p), ("a", C.c_void_p), ("r", C.c_void_p), ("s1", C.c_void_p),
+                ("done", C.c_void_p), ("probabilities", C.c_void_p), ("noise", C.c_void_p),
+                ("priorities", C.c_void_p)]
+
+
+class SacState(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "actor", "actor_grad", "actor_m", "actor_v", "target_actor", "critic", "critic_grad",
+        "critic_m", "critic_v", "target_critic", "log_alpha", "metrics")]
 
 
 _lib = None
@@ -97,6 +133,29 @@ def _declare(lib):
     lib.impala_timer_read.argtypes = [_P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     for name in EXPORTS:
         if name not in ("impala_last_error", "impala_param_count", "impala_kernel_name"):
+            getattr(lib, name).restype = C.c_int
+    lib.sac_config_default.argtypes = [C.POINTER(SacConfig)]
+    lib.sac_actor_param_count.argtypes = [C.c_int, C.c_int]
+    lib.sac_critic_param_count.argtypes = [C.c_int, C.c_int]
+    lib.sac_create.argtypes = [C.POINTER(SacConfig), C.c_int, C.POINTER(_P)]
+    lib.sac_destroy.argtypes = [_P]
+    lib.sac_bind_state.argtypes = [_P, C.POINTER(SacState), _P]
+    lib.sac_refresh_weights.argtypes = [_P, _P]
+    lib.sac_set_steps.argtypes = [_P, C.c_int64, C.c_int64, C.c_int64, _P]
+    lib.sac_train_step.argtypes = [_P, C.POINTER(SacBatch), _P]
+    lib.sac_act.argtypes = [_P, _P, C.c_int, _P, C.c_float, C.c_float, C.c_float, _P, _P]
+    lib.sac_policy.argtypes = [_P, _P, C.c_int, _P, _P, _P, _P, _P, _P, _P]
+    lib.sac_q_forward.argtypes = [_P, _P, _P, C.c_int, C.c_int, _P, _P, _P]
+    lib.sac_phase_name.argtypes = [C.c_int]
+    lib.sac_phase_name.restype = C.c_char_p
+    lib.sac_timer_start.argtypes = [_P, C.c_int, C.c_int]
+    lib.sac_timer_read.argtypes = [_P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    lib.sac_sample.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, C.c_int, _P, _P,
+                               C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_size_t), C.c_int, _P]
+    for name in SAC_EXPORTS:
+        if name in ("sac_actor_param_count", "sac_critic_param_count"):
+            getattr(lib, name).restype = C.c_size_t
+        elif name != "sac_phase_name":
             getattr(lib, name).restype = C.c_int
 
 

@@ -1,6 +1,6 @@
 """Build the HIP extension in-tree: ``python -m impala_amd.build``.
 
-Compiles ``impala_amd/csrc/impala.hip`` for gfx950 into ``impala_amd/libimpala_hip.so`` with
+Compiles ``impala_amd/csrc/{impala,sac}.hip`` for gfx950 into ``impala_amd/libimpala_hip.so`` with
 hipcc (cross-compiles without a GPU).  The .so is git-ignored and travels with the tree.
 """
 from __future__ import annotations
@@ -21,11 +21,18 @@ def sources():
                   if f.endswith((".hip", ".h")))
 
 
+def hip_units():
+    """The translation units linked into the one library (impala.hip: IMPALA / PPO learner,
+    sac.hip: SAC learner)."""
+    return [os.path.join(SRC_DIR, f) for f in ("impala.hip", "sac.hip")]
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = sources() + [os.path.join(os.path.dirname(HERE), "include", "impala_hip.h")]
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    deps = sources() + [os.path.join(inc, f) for f in os.listdir(inc)]
     return any(os.path.getmtime(s) > t for s in deps if os.path.exists(s))
 
 
@@ -35,7 +42,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     tmp = OUT + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-o", tmp, os.path.join(SRC_DIR, "impala.hip")]
+           "-Wall", "-Wno-unused-function", "-o", tmp] + hip_units()
     if verbose:
         print(" ".join(cmd), flush=True)
     if os.path.exists(tmp):

@@ -30,6 +30,15 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+// shared with the SAC translation unit (sac.hip): one last-error slot per thread for the library
+namespace impala_internal {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace impala_internal
+
+namespace {
+
 #define CK(x)                                                                          \
   do {                                                                                 \
     hipError_t e_ = (x);                                                               \
