@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Learner throughput bench: env-frames/s of the IMPALA learner step on MI355X.
+"""Learner throughput bench: env-frames/s of the IMPALA learner step on MI355X
+(``--algo ppo`` / ``--algo sac``: the PPO / SAC learner steps of BASELINE configs 4 / 5).
 
 ``python bench.py --gpus N --steps K --warmup W``  (N > 1: launched by torch.distributed.run).
 
@@ -164,6 +165,184 @@ def profiled_traffic(kernel, dtype):
     return best if best else (None, None)
 
 
+# ----------------------------------------------------------------------------- SAC
+def sac_phase_work(D, K, es, H=256):
+    """Algorithmic work of each SAC learner-step launch (sac.hip kPhase): (FLOPs/transition,
+    HBM bytes/transition, HBM bytes/launch), unpadded dims, each operand counted once."""
+    DK = D + K
+    act = H * es  # one hidden row
+    w2 = H * H * es
+    return {
+        "pack": (0, (2 * D + K) * 4 + (3 * D + 2 * DK) * es, 0),
+        "fwd_l1": (2 * H * (2 * D + 2 * DK), (2 * D + DK) * es + 4 * act + 3 * act,
+                   H * (2 * D + 2 * DK) * es),
+        "fwd_l2": (4 * 2 * H * H, 4 * act + 4 * act + 3 * act, 4 * w2),
+        "heads": (2 * 2 * H * 2 * K + 2 * 2 * H, 4 * act + 4 * K * 4 * 2, 0),
+        "target_critic_l1": (2 * 2 * H * DK, DK * es + 2 * act, 2 * H * DK * es),
+        "target_critic_l2": (2 * 2 * H * H, 4 * act, 2 * w2),
+        "critic_loss": (4 * 2 * H, 4 * act + 4 * act, 0),
+        "critic_bwd_l2": (2 * 2 * H * H + 2 * 2 * H * (H + 1) + 2 * 2 * (H + 1),
+                          2 * 3 * act + 2 * 2 * act + 2 * (act + es), 2 * w2 + 2 * (H * H + 2 * H + 1) * 4),
+        "critic_wgrad_l1": (2 * 2 * H * (DK + 1), 2 * act + (DK + 1) * es, 2 * H * (DK + 1) * 4),
+        "actor_q_l1": (2 * 2 * H * DK, DK * es + 2 * act, 2 * H * DK * es),
+        "actor_q_l2": (2 * 2 * H * H, 4 * act, 2 * w2),
+        "actor_loss": (2 * 2 * H, 4 * act, 0),
+        "actor_q_dgrad": (2 * 2 * H * H, 6 * act, 2 * w2),
+        "actor_head_bwd": (2 * 2 * H * K + 2 * H * 2 * K, 3 * act + 2 * act + 2 * K * es, 0),
+        "actor_bwd_l2": (2 * H * H + 2 * H * (H + 1) + 2 * 2 * K * (H + 1),
+                         3 * act + 2 * act + 2 * K * es + act, w2 + (H * H + H + 2 * K * (H + 1)) * 4),
+        "actor_wgrad_l1": (2 * H * (D + 1), act + (D + 1) * es, H * (D + 1) * 4),
+        "alpha_fwd_l1": (2 * H * D, D * es + act, H * D * es),
+        "alpha_fwd_l2": (2 * H * H, 2 * act, w2),
+        "alpha_head": (2 * H * 2 * K, act + K * 4, 0),
+        "critic_adam": (0, 0, 2 * (H * DK + H * H + 3 * H + 1) * (10 * 4 + 3 * es)),
+        "actor_adam": (0, 0, (H * D + H * H + 2 * H + 2 * K * (H + 1)) * (10 * 4 + 3 * es)),
+        "finalize": (0, 0, 0),
+    }
+
+
+def cpu_baseline_sac(N, D, K, seconds):
+    """The reference SAC learner step (oracle port of agents/sac/learning.py:146-265)."""
+    from oracle import sac_cpu
+    threads = torch.get_num_threads()
+    actor, critic = sac_cpu.make_models(D, K, seed=0)
+    st = sac_cpu.SACState(actor, critic)
+    s, a, r, s1, d = (torch.from_numpy(x) for x in sac_cpu.synthetic_batch(N, D, K, seed=99))
+    probs = torch.full((N,), 1.0 / 1000)
+    g = torch.Generator().manual_seed(0)
+
+    def one():
+        eps3 = [torch.randn(N, K, generator=g) for _ in range(3)]
+        sac_cpu.train_step(st, (s, a, r, s1, d), probs, eps3)
+
+    for _ in range(2):
+        one()
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        one()
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": N / med, "unit": "transitions/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} oracle SAC learner steps (N={N}, D={D}, K={K}, fp32 "
+                      f"torch-CPU, {threads} threads) after 2 warm-up; median step {med * 1e3:.2f} ms"}
+
+
+def run_sac(args):
+    """SAC learner step (BASELINE config 5): critic + actor + alpha updates and both Polyak
+    averages on N sampled transitions, sampled on the device from an HBM replay each step."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:  # independent replicas (the reference's SAC learner does not shard)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from impala_amd.sac import DeviceTransitionReplay, SACEngine, SoftActor, SoftCritic
+    N, D, K = args.batch, args.obs_dim, args.act_dim
+    torch.manual_seed(0)
+    critic = SoftCritic((D,), (K,), device=dev)
+    actor = SoftActor((D,), (K,), device=dev, dtype=args.dtype)
+    tactor = actor.clone_to(dev)
+    eng = SACEngine(actor, critic, tactor, batch_size=N, dtype=args.dtype, seed=rank)
+    actor._train_engine = eng
+    critic._engine = eng
+    # HBM replay of 1e6 transitions (conf/agent/sac.yaml replay_buffer_size), filled before timing
+    cap = args.replay
+    rb = DeviceTransitionReplay(cap, device=dev, seed=1000 + rank)
+    g = torch.Generator(device=dev).manual_seed(7 + rank)
+    rb.extend([torch.randn(cap, D, device=dev, generator=g),
+               torch.rand(cap, K, device=dev, generator=g) * 2 - 1,
+               torch.randn(cap, device=dev, generator=g),
+               torch.randn(cap, D, device=dev, generator=g),
+               torch.rand(cap, device=dev, generator=g) < 0.05])
+    prio = torch.zeros(N, dtype=torch.float32, device=dev)
+
+    def step():
+        _, (s, a, r, s1, d), p = rb.sample(N, copy=False)
+        eng.train_step(s, a, r, s1, d, probabilities=p, priorities=prio)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    work = sac_phase_work(D, K, 2 if args.dtype == "bf16" else 4)
+    names = eng.phase_names()
+    probe = {}
+    rk = args.roofline_kernel
+    if rk is None:
+        for i, kname in enumerate(names):
+            eng.timer_start(i, 3)
+            for _ in range(3):
+                step()
+            ms, n = eng.timer_read()
+            if n:
+                probe[kname] = ms / n
+        rk = max((k for k in probe if work[k][0]), key=probe.get)
+    torch.cuda.synchronize()
+    # timed region: the production mode (each step one hipGraph replay, sampling included)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # the dominant launch's duration: HIP events around it on its stream, over as many steps
+    # again (an armed timer launches directly -- a graph replay cannot carry per-launch events)
+    eng.timer_start(names.index(rk), args.steps)
+    for _ in range(args.steps):
+        step()
+    k_ms, k_n = eng.timer_read()
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    met = eng.metrics.cpu().numpy()
+    if not np.all(np.isfinite(met)):
+        raise RuntimeError(f"non-finite metrics {met}")
+    value = world * N * args.steps / elapsed
+    k_avg_ms = k_ms / max(k_n, 1)
+    fpt, bpt, bpl = work[rk]
+    flops, nbytes = fpt * N, bpt * N + bpl
+    t_s = k_avg_ms * 1e-3
+    if flops / (PEAK_TFLOPS[args.dtype] * 1e12) >= nbytes / (PEAK_HBM_GBS * 1e9):
+        bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
+    else:
+        bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
+    step_flops = sum(w[0] for w in work.values()) * N
+    out = {
+        "metric": "SAC learner transitions/sec (agents/sac, BASELINE config 5)",
+        "value": round(value, 1), "unit": "transitions/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": f"synthetic transitions (s, s1 ~ N(0,1), a ~ U(-1,1), r ~ N(0,1), 5% done) in a "
+                f"{cap}-transition HBM replay, sampled on the device each step; reference init (seed 0)",
+        "config": {"workload": f"SAC learner step (twin Q, tanh-Normal actor, alpha tuning, Polyak "
+                               f"0.005), obs {D}, action {K}, N={N} transitions/GPU",
+                   "global_batch": N * world, "parallelism": f"replicas{world}"},
+        "roofline": {"bound": bound, "kernel": rk, "achieved": round(achieved, 3), "peak": peak,
+                     "unit": unit, "frac": round(achieved / peak, 5), "traffic": None,
+                     "algorithmic": {"flops": flops, "bytes": nbytes},
+                     "avg_launch_us": round(k_avg_ms * 1e3, 2), "launches": k_n,
+                     "timing": "separate event-timed pass of --steps direct-launch steps"},
+        "step_gflop": round(step_flops / 1e9, 3),
+    }
+    if probe:
+        out["kernel_probe_us"] = {k: round(v * 1e3, 2) for k, v in sorted(probe.items(), key=lambda kv: -kv[1])}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_sac(N, D, K, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,10 +355,18 @@ def main():
     ap.add_argument("--roofline-kernel", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--algo", default="impala", choices=["impala", "ppo"],
+    ap.add_argument("--algo", default="impala", choices=["impala", "ppo", "sac"],
                     help="ppo: PPO learner step (BASELINE config 4) on --batch transitions "
-                         "(default 256, conf/agent/ppo.yaml)")
+                         "(default 256, conf/agent/ppo.yaml); sac: SAC learner step (config 5, "
+                         "--batch default 256 as conf/agent/sac.yaml, HalfCheetah dims 17/6)")
+    ap.add_argument("--obs-dim", type=int, default=17)
+    ap.add_argument("--act-dim", type=int, default=6)
+    ap.add_argument("--replay", type=int, default=1_000_000)
     args = ap.parse_args()
+    if args.algo == "sac":
+        if args.batch == 64:
+            args.batch = 256
+        return run_sac(args)
     ppo = args.algo == "ppo"
     if ppo:
         if args.batch == 64:

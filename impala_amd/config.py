@@ -57,13 +57,18 @@ def _num(x):
     return x
 
 
-def load_config(overrides: Optional[Dict[str, Any]] = None, deploy: Optional[str] = None) -> Cfg:
-    """Compose config.yaml + agent + task + deploy overlay (+ overrides), as main.py:39-53."""
+def load_config(overrides: Optional[Dict[str, Any]] = None, deploy: Optional[str] = None,
+                agent: Optional[str] = None, task: Optional[str] = None) -> Cfg:
+    """Compose config.yaml + agent + task + deploy overlay (+ overrides), as main.py:39-53.
+    ``agent`` / ``task`` select the group files as Hydra's ``agent=sac task=mujoco`` would
+    (agent=sac alone implies task=mujoco, the reference's SAC task)."""
     base = _load(os.path.join(CONF_DIR, "config.yaml"))
     defaults = base.pop("defaults", {})
     cfg = dict(base)
-    cfg["agent"] = _load(os.path.join(CONF_DIR, "agent", f"{defaults.get('agent', 'impala')}.yaml"))
-    cfg["task"] = _load(os.path.join(CONF_DIR, "task", f"{defaults.get('task', 'procgen')}.yaml"))
+    agent = agent or defaults.get("agent", "impala")
+    task = task or ("mujoco" if agent == "sac" else defaults.get("task", "procgen"))
+    cfg["agent"] = _load(os.path.join(CONF_DIR, "agent", f"{agent}.yaml"))
+    cfg["task"] = _load(os.path.join(CONF_DIR, "task", f"{task}.yaml"))
     dep = deploy or defaults.get("deploy", "local")
     if dep:
         cfg = _merge(cfg, _load(os.path.join(CONF_DIR, "deploy", f"{dep}.yaml")))

@@ -708,50 +708,74 @@ __global__ __launch_bounds__(256) void finalize_kernel(const FinArgs a) {
 // Uniform replay sampling (one workgroup): idx[i] = hash(seed, counter, i, round) % size,
 // redrawn while it collides with an earlier index (without replacement when n <= size).
 // =========================================================================================
-constexpr int SAMPLE_LDS = 4096;
+constexpr int SAMPLE_MAX_UNIQUE = 4096;  // n above this (or size >= 2^31): with replacement
+constexpr int SAMPLE_TS = 8192;          // LDS hash table slots (>= 2 n)
 DEV int64_t draw_index(uint64_t seed, uint64_t counter, int i, int round, int64_t size) {
   return (int64_t)(mix64(mix64(seed ^ mix64(counter)) + (uint64_t)i + ((uint64_t)round << 40)) %
                    (uint64_t)size);
 }
+// Every position draws a key; a round inserts all keys into an LDS hash table (linear probing,
+// atomicCAS on the key, atomicMin on the owning position), and every position whose key is
+// owned by an earlier position redraws.  atomicMin makes the winner order-independent, so the
+// result is deterministic; rounds repeat until no position redraws (bounded).
 __global__ __launch_bounds__(256) void sample_kernel(uint64_t seed, uint64_t counter, int64_t size,
                                                      int n, int64_t* idx, float* probs) {
-  __shared__ int64_t sidx[SAMPLE_LDS];
-  __shared__ int pending;
-  const bool unique = (int64_t)n <= size && n <= SAMPLE_LDS;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int64_t v = draw_index(seed, counter, i, 0, size);
-    if (unique) sidx[i] = v;
-    else idx[i] = v;
-    if (probs) probs[i] = __fdiv_rn(1.f, (float)size);
+  __shared__ uint32_t key[SAMPLE_TS];
+  __shared__ int owner[SAMPLE_TS];
+  constexpr int PER = SAMPLE_MAX_UNIQUE / 256;
+  const bool unique = (int64_t)n <= size && n <= SAMPLE_MAX_UNIQUE && size < (1LL << 31);
+  if (probs)
+    for (int i = threadIdx.x; i < n; i += 256) probs[i] = __fdiv_rn(1.f, (float)size);
+  if (!unique) {
+    for (int i = threadIdx.x; i < n; i += 256) idx[i] = draw_index(seed, counter, i, 0, size);
+    return;
   }
-  if (!unique) return;
-  for (int round = 1; round < 256; ++round) {
-    __syncthreads();
-    if (threadIdx.x == 0) pending = 0;
-    // mark collisions with an earlier position (read phase), then redraw (write phase)
-    int redraw[SAMPLE_LDS / 256];
-    int nr = 0;
+  uint32_t v[PER];
 #pragma unroll
-    for (int q = 0; q < SAMPLE_LDS / 256; ++q) {
-      const int i = threadIdx.x + 256 * q;
-      redraw[q] = -1;
-      if (i < n) {
-        const int64_t v = sidx[i];
-        bool dup = false;
-        for (int jj = 0; jj < i && !dup; ++jj) dup = sidx[jj] == v;
-        if (dup) { redraw[q] = i; ++nr; }
-      }
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + 256 * q;
+    v[q] = i < n ? (uint32_t)draw_index(seed, counter, i, 0, size) : 0u;
+  }
+  for (int round = 1; round < 64; ++round) {
+    for (int t = threadIdx.x; t < SAMPLE_TS; t += 256) {
+      key[t] = 0xFFFFFFFFu;
+      owner[t] = 0x7FFFFFFF;
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < SAMPLE_LDS / 256; ++q)
-      if (redraw[q] >= 0) sidx[redraw[q]] = draw_index(seed, counter, redraw[q], round, size);
-    if (nr) pending = 1;
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      if (i >= n) continue;
+      uint32_t h = (uint32_t)mix64(v[q]) & (SAMPLE_TS - 1);
+      for (int probe = 0; probe < SAMPLE_TS; ++probe) {
+        const uint32_t old = atomicCAS(&key[h], 0xFFFFFFFFu, v[q]);
+        if (old == 0xFFFFFFFFu || old == v[q]) {
+          atomicMin(&owner[h], i);
+          break;
+        }
+        h = (h + 1) & (SAMPLE_TS - 1);
+      }
+    }
     __syncthreads();
-    if (!pending) break;
+    int redraw = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      if (i >= n) continue;
+      uint32_t h = (uint32_t)mix64(v[q]) & (SAMPLE_TS - 1);
+      for (int probe = 0; probe < SAMPLE_TS && key[h] != v[q]; ++probe) h = (h + 1) & (SAMPLE_TS - 1);
+      if (owner[h] != i) {
+        v[q] = (uint32_t)draw_index(seed, counter, i, round, size);
+        redraw = 1;
+      }
+    }
+    if (!__syncthreads_or(redraw)) break;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += 256) idx[i] = sidx[i];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x + 256 * q;
+    if (i < n) idx[i] = (int64_t)v[q];
+  }
 }
 
 // row gather for sac_sample: dst_f[i] = src_f[idx[i]], any row size (4-byte copies when the

@@ -506,7 +506,11 @@ class SACLearner(Learner):
 
     def train_step(self) -> Dict[str, object]:  # learning.py:146-193
         t0 = time.perf_counter()
-        keys, batch, values = self._replay_buffer.sample(self._batch_size)
+        rb = self._replay_buffer
+        if isinstance(rb, DeviceTransitionReplay):  # consumed by this step before the next sample
+            keys, batch, values = rb.sample(self._batch_size, copy=False)
+        else:
+            keys, batch, values = rb.sample(self._batch_size)
         dev = self.device()
         s, a, r, s1, d = (torch.as_tensor(x).to(dev, non_blocking=True) for x in batch)
         s, a, r, s1, d = (x.squeeze(dim=-1) if x.dim() > 1 and x.shape[-1] == 1 else x
@@ -628,8 +632,10 @@ class DeviceTransitionReplay:
                     raise TimeoutError(f"replay warm_up: {self._size}/{need} after {timeout}s")
                 self._cv.wait(left)
 
-    def sample(self, batch_size: int):
-        """-> (keys [n] i64, [s, a, r, s1, done] device tensors, probabilities [n] f32)."""
+    def sample(self, batch_size: int, copy: bool = True):
+        """-> (keys [n] i64, [s, a, r, s1, done] device tensors, probabilities [n] f32).
+        copy=False returns the buffer's persistent output tensors (overwritten by the next
+        sample; the learner consumes them first), so a step's sampling is two launches."""
         with self._cv:
             if self._size == 0:
                 raise RuntimeError("sample from an empty replay buffer")
@@ -639,9 +645,9 @@ class DeviceTransitionReplay:
                 self._out = [torch.empty(n, *f.shape[1:], dtype=f.dtype, device=d) for f in self._fields]
                 self._idx = torch.empty(n, dtype=torch.int64, device=d)
                 self._probs = torch.empty(n, dtype=torch.float32, device=d)
-            out, idx, probs = self._out, self._idx, self._probs
+                self._keys_out = torch.empty(n, dtype=torch.int64, device=d)
+            out, idx, probs, keys_out = self._out, self._idx, self._probs, self._keys_out
             fields = self._fields + [self._keys]
-            keys_out = torch.empty(n, dtype=torch.int64, device=self.device)
             dsts = out + [keys_out]
             src = (C.c_void_p * 6)(*[f.data_ptr() for f in fields])
             dst = (C.c_void_p * 6)(*[t.data_ptr() for t in dsts])
@@ -651,7 +657,9 @@ class DeviceTransitionReplay:
             _lib.check(_lib.lib().sac_sample(self.seed, self._draws, self._size, n, idx.data_ptr(),
                                              probs.data_ptr(), src, dst, rb, 6,
                                              _lib.stream_ptr(None)), "sac_sample")
-        return keys_out, [t.clone() for t in out], probs.clone()
+        if not copy:
+            return keys_out, list(out), probs
+        return keys_out.clone(), [t.clone() for t in out], probs.clone()
 
 
 class SACActor(Actor):
