@@ -172,7 +172,7 @@ def sac_phase_work(D, K, es, H=256):
     DK = D + K
     act = H * es  # one hidden row
     w2 = H * H * es
-    return {
+    w = {
         "pack": (0, (2 * D + K) * 4 + (3 * D + 2 * DK) * es, 0),
         "fwd_l1": (2 * H * (2 * D + 2 * DK), (2 * D + DK) * es + 4 * act + 3 * act,
                    H * (2 * D + 2 * DK) * es),
@@ -199,6 +199,26 @@ def sac_phase_work(D, K, es, H=256):
         "actor_adam": (0, 0, (H * D + H * H + 2 * H + 2 * K * (H + 1)) * (10 * 4 + 3 * es)),
         "finalize": (0, 0, 0),
     }
+    # fused path (sac_fused.h): per-row-block chains; a chain's intermediate rows stay in LDS,
+    # so its bytes are the unfused phases' minus those hand-offs (approximated by their sum)
+    dgrad2 = 2 * H * H
+    w["critic_fwd_chain"] = sum_work(w, ("fwd_l1", "fwd_l2", "heads"))
+    w["critic_loss_chain"] = sum_work(w, ("target_critic_l1", "target_critic_l2", "critic_loss"),
+                                      (2 * dgrad2, 4 * act, 2 * w2))
+    w["critic_wgrad"] = sum_work(w, ("critic_wgrad_l1",),
+                                 (2 * 2 * H * (H + 1) + 2 * 2 * (H + 1), 4 * act + 2 * (act + es),
+                                  2 * (H * H + 2 * H + 1) * 4))
+    w["actor_chain"] = sum_work(w, ("actor_q_l1", "actor_q_l2", "actor_loss", "actor_q_dgrad",
+                                    "actor_head_bwd"), (dgrad2, 2 * act, w2))
+    w["actor_wgrad"] = sum_work(w, ("actor_wgrad_l1",),
+                                (2 * H * (H + 1) + 2 * 2 * K * (H + 1), 3 * act + 2 * K * es,
+                                 (H * H + H + 2 * K * (H + 1)) * 4))
+    w["alpha_chain"] = sum_work(w, ("alpha_fwd_l1", "alpha_fwd_l2", "alpha_head"))
+    return w
+
+
+def sum_work(w, names, extra=(0, 0, 0)):
+    return tuple(sum(w[n][i] for n in names) + extra[i] for i in range(3))
 
 
 def cpu_baseline_sac(N, D, K, seconds):
@@ -315,7 +335,7 @@ def run_sac(args):
         bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
-    step_flops = sum(w[0] for w in work.values()) * N
+    step_flops = sum(work[k][0] for k in probe) * N if probe else None
     out = {
         "metric": "SAC learner transitions/sec (agents/sac, BASELINE config 5)",
         "value": round(value, 1), "unit": "transitions/s", "n_gpus": world, "steps": args.steps,

@@ -272,20 +272,16 @@ struct HeadArgs {
   int N, K;
 };
 
+// one transition's head from its hidden-2 row (global or LDS), executed by one wave
 template <typename T>
-__global__ __launch_bounds__(256) void heads_kernel(const HeadArgs g) {
-  const int lane = threadIdx.x & 63;
-  const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-  if (n >= g.N) return;
-  const HeadJob& J = g.j[blockIdx.y];
+DEV void head_row(const HeadJob& J, const T* hrow, int n, int N, int K, int lane) {
   float h[4];
-  load_row<T>(J.h, J.ldh, n, lane, h);
+  load4(hrow + 4 * lane, h);
   if (J.kind == HK_Q) {
     const float q = dot_row(J.wm, lane, h) + J.bm[0];
     if (lane == 0) J.q[n] = q;
     return;
   }
-  const int K = g.K;
   float logp = 0.f, stdsum = 0.f;
   for (int k = 0; k < K; ++k) {
     const float mean = dot_row(J.wm + (size_t)k * H, lane, h) + J.bm[k];
@@ -316,7 +312,7 @@ __global__ __launch_bounds__(256) void heads_kernel(const HeadArgs g) {
       if (J.mean_out) J.mean_out[o] = mean;
       if (J.ls_out) J.ls_out[o] = ls;
       if (J.save) {
-        const size_t NK = (size_t)g.N * K;
+        const size_t NK = (size_t)N * K;
         J.save[o] = sd;
         J.save[NK + o] = y;
         J.save[2 * NK + o] = xm;
@@ -328,6 +324,15 @@ __global__ __launch_bounds__(256) void heads_kernel(const HeadArgs g) {
     if (J.logp) J.logp[n] = logp;
     if (J.stdrow) J.stdrow[n] = __fdiv_rn(stdsum, (float)K);
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void heads_kernel(const HeadArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (n >= g.N) return;
+  const HeadJob& J = g.j[blockIdx.y];
+  head_row<T>(J, (const T*)J.h + (size_t)n * J.ldh, n, g.N, g.K, lane);
 }
 
 // =========================================================================================
@@ -355,16 +360,12 @@ struct CLossArgs {
   float* rowm;        // [8][ldt]
 };
 
+// TD target, weights, losses and dQ of one transition (t1, t2 = target-critic Q values);
+// lane 0 writes the per-transition metric terms and priority when `emit`, and dQ into row 0
+// of both dq_t operands.
 template <typename T>
-__global__ __launch_bounds__(256) void critic_loss_kernel(const CLossArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-  if (n >= a.N) return;
-  float h[4];
-  load_row<T>(a.ht1, H, n, lane, h);
-  const float t1 = dot_row(a.w3t1, lane, h) + a.b3t1[0];
-  load_row<T>(a.ht2, H, n, lane, h);
-  const float t2 = dot_row(a.w3t2, lane, h) + a.b3t2[0];
+DEV void closs_row(const CLossArgs& a, float t1, float t2, int n, int lane, bool emit, float& dq1,
+                   float& dq2) {
   // importance weights: probabilities.pow(-0.4) / max (learning.py:197-199)
   float w = 1.f;
   if (a.probs) {
@@ -379,25 +380,46 @@ __global__ __launch_bounds__(256) void critic_loss_kernel(const CLossArgs a) {
   const float q1 = a.q1[n], q2 = a.q2[n];
   const float d1 = sub(y, q1), d2 = sub(y, q2);
   const float wn = mul(__fdiv_rn(1.f, (float)a.N), w);
-  const float dq1 = -mul(wn, mul(2.f, d1)), dq2 = -mul(wn, mul(2.f, d2));
+  dq1 = -mul(wn, mul(2.f, d1));
+  dq2 = -mul(wn, mul(2.f, d2));
   if (lane == 0) {
-    if (a.prio) a.prio[n] = fabsf(sub(y, fminf(q1, q2)));
-    a.rowm[0 * a.ldt + n] = mul(mul(d1, d1), w);
-    a.rowm[1 * a.ldt + n] = mul(mul(d2, d2), w);
-    a.rowm[2 * a.ldt + n] = q1;
-    a.rowm[3 * a.ldt + n] = q2;
+    if (emit) {
+      if (a.prio) a.prio[n] = fabsf(sub(y, fminf(q1, q2)));
+      a.rowm[0 * a.ldt + n] = mul(mul(d1, d1), w);
+      a.rowm[1 * a.ldt + n] = mul(mul(d2, d2), w);
+      a.rowm[2 * a.ldt + n] = q1;
+      a.rowm[3 * a.ldt + n] = q2;
+    }
     ((T*)a.dq1t)[n] = to_t<T>(dq1);
     ((T*)a.dq2t)[n] = to_t<T>(dq2);
   }
+}
+// dh2 = dq * W3 (.) [h2 > 0] for the lane's 4 features of one row
+template <typename T>
+DEV void dq_to_dh(float dq, const float* w3, const T* h2row, int lane, float d[4]) {
+  float h[4];
+  load4(h2row + 4 * lane, h);
+  const f32x4 wv = load4f(w3 + 4 * lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = h[i] > 0.f ? dq * wv[i] : 0.f;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void critic_loss_kernel(const CLossArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (n >= a.N) return;
+  float h[4];
+  load_row<T>(a.ht1, H, n, lane, h);
+  const float t1 = dot_row(a.w3t1, lane, h) + a.b3t1[0];
+  load_row<T>(a.ht2, H, n, lane, h);
+  const float t2 = dot_row(a.w3t2, lane, h) + a.b3t2[0];
+  float dq[2];
+  closs_row<T>(a, t1, t2, n, lane, true, dq[0], dq[1]);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const float dq = q ? dq2 : dq1;
-    const float* w3 = q ? a.w3c2 : a.w3c1;
-    load_row<T>(q ? a.hc2 : a.hc1, H, n, lane, h);
-    const f32x4 wv = load4f(w3 + 4 * lane);
     float d[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) d[i] = h[i] > 0.f ? dq * wv[i] : 0.f;
+    dq_to_dh<T>(dq[q], q ? a.w3c2 : a.w3c1, (const T*)(q ? a.hc2 : a.hc1) + (size_t)n * H, lane, d);
     store4((T*)(q ? a.dh2 : a.dh1) + (size_t)n * H + 4 * lane, d);
     T* dt = (T*)(q ? a.dh2t : a.dh1t);
 #pragma unroll
@@ -420,6 +442,15 @@ struct ALossArgs {
   float* rowm;      // row 4: loss term
 };
 
+// actor loss term and the dQ of both networks for one transition (q1, q2 on (s, pi))
+DEV void aloss_row(const ALossArgs& a, float q1, float q2, int n, int lane, float& dq1, float& dq2) {
+  const float alpha = expf(a.log_alpha[0]);
+  const float g = -__fdiv_rn(1.f, (float)a.N);
+  dq1 = q1 < q2 ? g : (q1 == q2 ? 0.5f * g : 0.f);
+  dq2 = q2 < q1 ? g : (q1 == q2 ? 0.5f * g : 0.f);
+  if (lane == 0) a.rowm[4 * a.ldt + n] = sub(mul(alpha, a.logp[n]), fminf(q1, q2));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void actor_loss_kernel(const ALossArgs a) {
   const int lane = threadIdx.x & 63;
@@ -430,19 +461,12 @@ __global__ __launch_bounds__(256) void actor_loss_kernel(const ALossArgs a) {
   load_row<T>(a.hp2, H, n, lane, h2);
   const float q1 = dot_row(a.w3c1, lane, h1) + a.b3c1[0];
   const float q2 = dot_row(a.w3c2, lane, h2) + a.b3c2[0];
-  const float alpha = expf(a.log_alpha[0]);
-  const float g = -__fdiv_rn(1.f, (float)a.N);
-  const float dq1 = q1 < q2 ? g : (q1 == q2 ? 0.5f * g : 0.f);
-  const float dq2 = q2 < q1 ? g : (q1 == q2 ? 0.5f * g : 0.f);
-  if (lane == 0) a.rowm[4 * a.ldt + n] = sub(mul(alpha, a.logp[n]), fminf(q1, q2));
+  float dq[2];
+  aloss_row(a, q1, q2, n, lane, dq[0], dq[1]);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const float dq = q ? dq2 : dq1;
-    const float* hh = q ? h2 : h1;
-    const f32x4 wv = load4f((q ? a.w3c2 : a.w3c1) + 4 * lane);
     float d[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) d[i] = hh[i] > 0.f ? dq * wv[i] : 0.f;
+    dq_to_dh<T>(dq[q], q ? a.w3c2 : a.w3c1, (const T*)(q ? a.hp2 : a.hp1) + (size_t)n * H, lane, d);
     store4((T*)(q ? a.dh2 : a.dh1) + (size_t)n * H + 4 * lane, d);
   }
 }
@@ -473,15 +497,15 @@ struct ABwdArgs {
   void *gmt, *gut;              // [16][ldt] (T): g_mean, g_u transposed
 };
 
+// one transition: d1/d2 = its ReLU-masked critic dh1 rows on (s, pi), ha2 = its actor hidden-2
+// row; writes dha2 (row-major when dha2_row, transposed into a.dha2t) and g_mean / g_u.
 template <typename T>
-__global__ __launch_bounds__(256) void actor_head_bwd_kernel(const ABwdArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-  if (n >= a.N) return;
+DEV void ahead_row(const ABwdArgs& a, const T* d1row, const T* d2row, const T* ha2row, T* dha2_row,
+                   int n, int lane) {
   const int K = a.K, DK = a.D + a.K;
   float d1[4], d2[4];
-  load_row<T>(a.dhp1, H, n, lane, d1);
-  load_row<T>(a.dhp2, H, n, lane, d2);
+  load4(d1row + 4 * lane, d1);
+  load4(d2row + 4 * lane, d2);
   const float c = mul(__fdiv_rn(1.f, (float)a.N), expf(a.log_alpha[0]));
   const size_t NK = (size_t)a.N * K;
   float gm[MAXK], gu[MAXK];  // static indices only (fully unrolled, k < K uniform)
@@ -508,7 +532,7 @@ __global__ __launch_bounds__(256) void actor_head_bwd_kernel(const ABwdArgs a) {
     gu[k] = gs * sd * (3.5f * (1.f - tu * tu));
   }
   float hv[4];
-  load_row<T>(a.ha2, H, n, lane, hv);
+  load4(ha2row + 4 * lane, hv);
   float d[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -519,7 +543,7 @@ __global__ __launch_bounds__(256) void actor_head_bwd_kernel(const ABwdArgs a) {
       if (k < K) s += gm[k] * a.wm[(size_t)k * H + hcol] + gu[k] * a.wl[(size_t)k * H + hcol];
     d[i] = hv[i] > 0.f ? s : 0.f;
   }
-  store4((T*)a.dha2 + (size_t)n * H + 4 * lane, d);
+  if (dha2_row) store4(dha2_row + 4 * lane, d);
 #pragma unroll
   for (int i = 0; i < 4; ++i) ((T*)a.dha2t)[(size_t)(4 * lane + i) * a.ldt + n] = to_t<T>(d[i]);
   if (lane < K) {
@@ -530,6 +554,15 @@ __global__ __launch_bounds__(256) void actor_head_bwd_kernel(const ABwdArgs a) {
     ((T*)a.gmt)[(size_t)lane * a.ldt + n] = to_t<T>(g1);
     ((T*)a.gut)[(size_t)lane * a.ldt + n] = to_t<T>(g2);
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void actor_head_bwd_kernel(const ABwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (n >= a.N) return;
+  ahead_row<T>(a, (const T*)a.dhp1 + (size_t)n * H, (const T*)a.dhp2 + (size_t)n * H,
+               (const T*)a.ha2 + (size_t)n * H, (T*)a.dha2 + (size_t)n * H, n, lane);
 }
 
 // =========================================================================================

@@ -7,11 +7,12 @@
 // the kernel-layout weight copies (T, padded, and transposed where a dgrad reads them), which
 // the Adam kernels re-emit every step.
 //
-// One train step is a fixed chain of 22 launches (phase names in kPhase): the critic step
+// One train step is a fixed chain of launches (phase names in kPhase): the critic step
 // (learning.py:195-211), the actor step (:213-223), the alpha step (:225-230), Polyak (:174-180)
-// folded into the two Adam launches.  The chain is replayed from a hipGraph (SAC_GRAPH=0
-// disables it): every launch is a few microseconds, so the host enqueue of 22 launches would
-// otherwise bound the step.
+// folded into the two Adam launches.  Default: 10 launches of per-row-block chain kernels
+// (sac_fused.h); SAC_FUSED=0: 22 launches of one kernel per layer (bitwise-equal results).
+// The chain is replayed from a hipGraph (SAC_GRAPH=0 disables it): every launch is a few
+// microseconds, so host enqueue would otherwise bound the step.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,6 +25,7 @@
 
 #include "../../include/sac_hip.h"
 #include "sac.h"
+#include "sac_fused.h"
 
 namespace impala_internal {
 int set_error(int code, const std::string& msg);
@@ -45,7 +47,7 @@ int fail(int code, const std::string& msg) { return impala_internal::set_error(c
   do {                                                                                 \
     hipError_t e_ = hipGetLastError();                                                 \
     if (e_ != hipSuccess)                                                              \
-      return fail((int)e_, std::string("launch ") + name + ": " + hipGetErrorString(e_)); \
+      return fail((int)e_, std::string("launch ") + (name) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
 inline int rup(int x, int m) { return (x + m - 1) / m * m; }
@@ -60,13 +62,18 @@ inline double dec(float x) {  // the decimal constant a float config value was w
 enum Phase {
   P_PACK = 0, P_FWD1, P_FWD2, P_HEADS, P_TFWD1, P_TFWD2, P_CLOSS, P_CBWD2, P_CBWD1, P_CADAM,
   P_AFWD1, P_AFWD2, P_ALOSS, P_ABWD2, P_AHEAD, P_ABWD1, P_AW1, P_AADAM, P_LFWD1, P_LFWD2,
-  P_LHEAD, P_FIN, P_COUNT
+  P_LHEAD, P_FIN,
+  // fused path (sac_fused.h)
+  P_CFWD, P_CCHAIN, P_CWGRAD, P_ACHAIN, P_AWGRAD, P_LCHAIN, P_COUNT
 };
 const char* kPhase[P_COUNT] = {
     "pack", "fwd_l1", "fwd_l2", "heads", "target_critic_l1", "target_critic_l2", "critic_loss",
     "critic_bwd_l2", "critic_wgrad_l1", "critic_adam", "actor_q_l1", "actor_q_l2", "actor_loss",
     "actor_q_dgrad", "actor_head_bwd", "actor_bwd_l2", "actor_wgrad_l1", "actor_adam",
-    "alpha_fwd_l1", "alpha_fwd_l2", "alpha_head", "finalize"};
+    "alpha_fwd_l1", "alpha_fwd_l2", "alpha_head", "finalize", "critic_fwd_chain",
+    "critic_loss_chain", "critic_wgrad", "actor_chain", "actor_wgrad", "alpha_chain"};
+
+inline const char* pname(int ph) { return ph >= 0 && ph < P_COUNT ? kPhase[ph] : "sac_forward"; }
 
 struct Offs {  // canonical flat offsets
   long long a_w1, a_b1, a_w2, a_b2, a_wm, a_bm, a_wl, a_bl, a_total;
@@ -129,6 +136,7 @@ struct sac_learner {
   int nsq_c = 0, nsq_a = 0;
   int64_t* steps = nullptr;  // critic, actor, alpha, learner
   MlpK ka{}, kta{}, kq[2]{}, ktq[2]{};
+  bool fused = true;  // per-row-block chain kernels (SAC_FUSED=0: one launch per layer)
   // graph cache
   bool use_graph = true;
   hipStream_t cap = nullptr;
@@ -284,7 +292,7 @@ int launch_gemm(sac_learner* h, int ph, std::initializer_list<GJob> jobs, hipStr
   timer_begin(h, ph, st);
   gemm_jobs<T><<<cdiv(t, 4), 256, 0, st>>>(g);
   timer_end(h, ph, st);
-  SCK_LAUNCH(kPhase[ph]);
+  SCK_LAUNCH(pname(ph));
   return 0;
 }
 
@@ -315,7 +323,7 @@ int launch_heads(sac_learner* h, int ph, std::initializer_list<HeadJob> jobs, in
   timer_begin(h, ph, st);
   heads_kernel<T><<<dim3(cdiv(n, 4), nj), 256, 0, st>>>(a);
   timer_end(h, ph, st);
-  SCK_LAUNCH(kPhase[ph]);
+  SCK_LAUNCH(pname(ph));
   return 0;
 }
 
@@ -365,7 +373,7 @@ int launch_adam(sac_learner* h, bool critic, int update, hipStream_t st) {
   timer_begin(h, ph, st);
   adam_net_kernel<T><<<cdiv(a.n, 256), 256, 0, st>>>(a);
   timer_end(h, ph, st);
-  SCK_LAUNCH(kPhase[ph]);
+  SCK_LAUNCH(pname(ph));
   return 0;
 }
 
@@ -547,12 +555,178 @@ int enqueue_step(sac_learner* h, const sac_batch* b, hipStream_t st) {
   return 0;
 }
 
+ChainJob chain_job(const void* x, int ldx, int K1, const MlpK& k, const float* b1, const float* b2,
+                   HeadJob head) {
+  ChainJob c{};
+  c.x = x; c.ldx = ldx; c.K1 = K1;
+  c.w1 = k.w1; c.b1 = b1; c.w2 = k.w2; c.b2 = b2;
+  c.head = head;
+  return c;
+}
+
+template <typename T>
+int launch_chain(sac_learner* h, int ph, std::initializer_list<ChainJob> jobs, int n, hipStream_t st) {
+  ChainArgs a{};
+  int nj = 0;
+  for (const ChainJob& j : jobs) a.j[nj++] = j;
+  a.N = n;
+  a.K = h->K;
+  a.ldt = h->Np;
+  timer_begin(h, ph, st);
+  chain_fwd_kernel<T><<<dim3(cdiv(n, 16), nj), 256, 0, st>>>(a);
+  timer_end(h, ph, st);
+  SCK_LAUNCH(pname(ph));
+  return 0;
+}
+
+// the fused learner step: 12 launches (sac_fused.h), bitwise equal to enqueue_step
+template <typename T>
+int enqueue_step_fused(sac_learner* h, const sac_batch* b, hipStream_t st) {
+  const sac_state& S = h->st;
+  const Offs& o = h->off;
+  const int N = h->N, Np = h->Np, D = h->D, K = h->K;
+  const long long NK = (long long)N * K;
+  const long long qb[2] = {0, o.q_per};
+  const float* eps = b->noise ? b->noise : h->eps;
+  const float *eps0 = eps, *eps1 = eps + NK, *eps2 = eps + 2 * NK;
+  int r;
+  {  // operand rows (+ device noise)
+    PackArgs p{};
+    p.s = b->s; p.a = b->a; p.s1 = b->s1;
+    p.N = N; p.D = D; p.K = K; p.ldd = h->Dp; p.ldc = h->Cp; p.ldt = Np;
+    p.xs = h->xs; p.xs1 = h->xs1; p.xc = h->xc; p.xt = h->xt; p.xp = h->xp;
+    p.xst = h->xst; p.xct = h->xct;
+    p.eps = b->noise ? nullptr : h->eps;
+    p.seed = h->cfg.seed;
+    p.counter = h->steps + 3;
+    timer_begin(h, P_PACK, st);
+    pack_kernel<T><<<std::max(1, std::min(256, cdiv(std::max((long long)N * h->DK, 3 * NK), 256))), 256, 0, st>>>(p);
+    timer_end(h, P_PACK, st);
+    SCK_LAUNCH("pack");
+  }
+  // critic step: forward chains (target actor -> a1, Q1, Q2, actor -> pi) ...
+  {
+    HeadJob tj = policy_job(nullptr, S.target_actor, o, eps0);
+    tj.xout = h->xt; tj.ldx = h->Cp; tj.xoff = D; tj.logp = h->logp1;
+    HeadJob aj = policy_job(nullptr, S.actor, o, eps1);
+    aj.xout = h->xp; aj.ldx = h->Cp; aj.xoff = D; aj.logp = h->logp; aj.save = h->save;
+    aj.stdrow = h->rowm + 5 * Np;
+    ChainJob j0 = chain_job(h->xs1, h->Dp, h->Dp, h->kta, S.target_actor + o.a_b1, S.target_actor + o.a_b2, tj);
+    ChainJob jq[2];
+    for (int q = 0; q < 2; ++q) {
+      jq[q] = chain_job(h->xc, h->Cp, h->Cp, h->kq[q], S.critic + qb[q] + o.q_b1, S.critic + qb[q] + o.q_b2,
+                        q_job(nullptr, S.critic, qb[q], o, q ? h->q2 : h->q1));
+      jq[q].h1 = h->hc1[q]; jq[q].h1t = h->hc1t[q]; jq[q].h2 = h->hc2[q]; jq[q].h2t = h->hc2t[q];
+    }
+    ChainJob j3 = chain_job(h->xs, h->Dp, h->Dp, h->ka, S.actor + o.a_b1, S.actor + o.a_b2, aj);
+    j3.h1 = h->ha1; j3.h1t = h->ha1t; j3.h2 = h->ha2; j3.h2t = h->ha2t;
+    if ((r = launch_chain<T>(h, P_CFWD, {j0, jq[0], jq[1], j3}, N, st))) return r;
+  }
+  {  // ... target critic chains, critic loss, row-local critic backward ...
+    CChainArgs c{};
+    CLossArgs& a = c.L;
+    a.w3t1 = S.target_critic + qb[0] + o.q_w3; a.b3t1 = S.target_critic + qb[0] + o.q_b3;
+    a.w3t2 = S.target_critic + qb[1] + o.q_w3; a.b3t2 = S.target_critic + qb[1] + o.q_b3;
+    a.hc1 = h->hc2[0]; a.hc2 = h->hc2[1];
+    a.w3c1 = S.critic + qb[0] + o.q_w3; a.w3c2 = S.critic + qb[1] + o.q_w3;
+    a.q1 = h->q1; a.q2 = h->q2; a.logp1 = h->logp1;
+    a.r = b->r; a.done = b->done; a.probs = b->probabilities; a.log_alpha = S.log_alpha;
+    a.gamma = h->cfg.gamma; a.prio_exp = -h->cfg.prio_exponent;
+    a.N = N; a.ldh = H; a.ldt = Np;
+    a.prio = b->priorities;
+    a.dh1t = h->dh2t[0]; a.dh2t = h->dh2t[1];
+    a.dq1t = h->dqt[0]; a.dq2t = h->dqt[1];
+    a.rowm = h->rowm;
+    c.xt = h->xt; c.ldx = h->Cp; c.K1 = h->Cp;
+    for (int q = 0; q < 2; ++q) {
+      c.tw1[q] = h->ktq[q].w1; c.tw2[q] = h->ktq[q].w2;
+      c.tb1[q] = S.target_critic + qb[q] + o.q_b1; c.tb2[q] = S.target_critic + qb[q] + o.q_b2;
+      c.w2t[q] = h->kq[q].w2t; c.h1[q] = h->hc1[q]; c.dh1t[q] = h->dhc1t[q];
+    }
+    timer_begin(h, P_CCHAIN, st);
+    critic_chain_kernel<T><<<dim3(cdiv(N, 16), 2), 256, 0, st>>>(c);
+    timer_end(h, P_CCHAIN, st);
+    SCK_LAUNCH("critic_loss_chain");
+  }
+  float* cg = S.critic_grad;
+  {  // ... every critic weight gradient, clip + Adam + Polyak
+    const int t2 = cdiv(H + 1, 16);
+    float* sq1 = h->sq_c + 34 * t2;
+    const int t1 = 16 * cdiv(h->DK + 1, 16);
+    if ((r = launch_gemm<T>(h, P_CWGRAD, {
+             wgrad_job(h->dh2t[0], H, h->hc1t[0], H, Np, cg + qb[0] + o.q_w2, cg + qb[0] + o.q_b2, h->sq_c),
+             wgrad_job(h->dh2t[1], H, h->hc1t[1], H, Np, cg + qb[1] + o.q_w2, cg + qb[1] + o.q_b2, h->sq_c + 16 * t2),
+             wgrad_job(h->dqt[0], 1, h->hc2t[0], H, Np, cg + qb[0] + o.q_w3, cg + qb[0] + o.q_b3, h->sq_c + 32 * t2),
+             wgrad_job(h->dqt[1], 1, h->hc2t[1], H, Np, cg + qb[1] + o.q_w3, cg + qb[1] + o.q_b3, h->sq_c + 33 * t2),
+             wgrad_job(h->dhc1t[0], H, h->xct, h->DK, Np, cg + qb[0] + o.q_w1, cg + qb[0] + o.q_b1, sq1),
+             wgrad_job(h->dhc1t[1], H, h->xct, h->DK, Np, cg + qb[1] + o.q_w1, cg + qb[1] + o.q_b1, sq1 + t1)}, st)))
+      return r;
+  }
+  if ((r = launch_adam<T>(h, true, 1, st))) return r;
+  {  // actor step: Q chains on (s, pi) with the updated critic, actor loss, row-local backward
+    AChainArgs c{};
+    ALossArgs& a = c.L;
+    a.logp = h->logp; a.log_alpha = S.log_alpha; a.N = N; a.ldt = Np; a.rowm = h->rowm;
+    ABwdArgs& bb = c.B;
+    bb.w1c1 = S.critic + qb[0] + o.q_w1; bb.w1c2 = S.critic + qb[1] + o.q_w1;
+    bb.save = h->save; bb.eps = eps1; bb.log_alpha = S.log_alpha;
+    bb.wm = S.actor + o.a_wm; bb.wl = S.actor + o.a_wl;
+    bb.ha2 = h->ha2;
+    bb.D = D; bb.K = K; bb.N = N; bb.ldt = Np;
+    bb.dha2t = h->dha2t; bb.gmt = h->gmt; bb.gut = h->gut;
+    c.xp = h->xp; c.ldx = h->Cp; c.K1 = h->Cp;
+    for (int q = 0; q < 2; ++q) {
+      c.w1[q] = h->kq[q].w1; c.w2[q] = h->kq[q].w2; c.w2t[q] = h->kq[q].w2t;
+      c.b1[q] = S.critic + qb[q] + o.q_b1; c.b2[q] = S.critic + qb[q] + o.q_b2;
+      c.w3[q] = S.critic + qb[q] + o.q_w3; c.b3[q] = S.critic + qb[q] + o.q_b3;
+    }
+    c.aw2t = h->ka.w2t; c.ha1 = h->ha1; c.dha1t = h->dha1t;
+    timer_begin(h, P_ACHAIN, st);
+    actor_chain_kernel<T><<<cdiv(N, 16), 256, 0, st>>>(c);
+    timer_end(h, P_ACHAIN, st);
+    SCK_LAUNCH("actor_chain");
+  }
+  float* ag = S.actor_grad;
+  {
+    const int t_w2 = 16 * cdiv(H + 1, 16), t_head = cdiv(K, 16) * cdiv(H + 1, 16);
+    if ((r = launch_gemm<T>(h, P_AWGRAD, {
+             wgrad_job(h->dha2t, H, h->ha1t, H, Np, ag + o.a_w2, ag + o.a_b2, h->sq_a),
+             wgrad_job(h->gmt, K, h->ha2t, H, Np, ag + o.a_wm, ag + o.a_bm, h->sq_a + t_w2),
+             wgrad_job(h->gut, K, h->ha2t, H, Np, ag + o.a_wl, ag + o.a_bl, h->sq_a + t_w2 + t_head),
+             wgrad_job(h->dha1t, H, h->xst, D, Np, ag + o.a_w1, ag + o.a_b1, h->sq_a + t_w2 + 2 * t_head)}, st)))
+      return r;
+  }
+  if ((r = launch_adam<T>(h, false, 1, st))) return r;
+  if (h->cfg.tune_alpha) {  // alpha step: a fresh sample from the updated actor
+    HeadJob lj = policy_job(nullptr, S.actor, o, eps2);
+    lj.logp = h->logp2;
+    if ((r = launch_chain<T>(h, P_LCHAIN, {chain_job(h->xs, h->Dp, h->Dp, h->ka, S.actor + o.a_b1,
+                                                     S.actor + o.a_b2, lj)}, N, st)))
+      return r;
+  }
+  {
+    FinArgs f{};
+    f.rowm = h->rowm; f.ldt = Np; f.N = N; f.tune_alpha = h->cfg.tune_alpha;
+    f.logp2 = h->logp2; f.la = S.log_alpha; f.metrics = S.metrics; f.steps = h->steps;
+    f.lr = dec(h->cfg.critic_lr); f.b1 = dec(h->cfg.adam_beta1); f.b2 = dec(h->cfg.adam_beta2);
+    f.eps = h->cfg.adam_eps; f.target_entropy = h->cfg.target_entropy;
+    timer_begin(h, P_FIN, st);
+    finalize_kernel<<<1, 256, 0, st>>>(f);
+    timer_end(h, P_FIN, st);
+    SCK_LAUNCH("finalize");
+  }
+  return 0;
+}
+
 template <typename T>
 int enqueue_forward(sac_learner* h, const float* obs, int n, hipStream_t st, HeadJob job) {
   const Offs& o = h->off;
   pack_obs_kernel<T><<<std::max(1, std::min(256, cdiv((long long)n * h->D, 256))), 256, 0, st>>>(
       obs, n, h->D, h->Dp, (T*)h->xi);
   SCK_LAUNCH("pack_obs");
+  if (h->fused)
+    return launch_chain<T>(h, -1, {chain_job(h->xi, h->Dp, h->Dp, h->ka, h->st.actor + o.a_b1,
+                                             h->st.actor + o.a_b2, job)}, n, st);
   int r;
   if ((r = launch_gemm<T>(h, -1, {fwd_job(h->ka.w1, h->Dp, h->xi, h->Dp, h->Dp, h->st.actor + o.a_b1,
                                            h->hb1, nullptr, h->Np, n)}, st)))
@@ -574,6 +748,11 @@ int enqueue_q_forward(sac_learner* h, const float* obs, const float* act, int n,
   pack_sa_kernel<T><<<std::max(1, std::min(256, cdiv((long long)n * h->DK, 256))), 256, 0, st>>>(
       obs, act, n, h->D, h->K, h->Cp, (T*)h->xi2);
   SCK_LAUNCH("pack_sa");
+  if (h->fused)
+    return launch_chain<T>(h, -1, {
+        chain_job(h->xi2, h->Cp, h->Cp, k[0], P + o.q_b1, P + o.q_b2, q_job(nullptr, P, 0, o, q1)),
+        chain_job(h->xi2, h->Cp, h->Cp, k[1], P + o.q_per + o.q_b1, P + o.q_per + o.q_b2,
+                  q_job(nullptr, P, o.q_per, o, q2))}, n, st);
   int r;
   if ((r = launch_gemm<T>(h, -1, {
            fwd_job(k[0].w1, h->Cp, h->xi2, h->Cp, h->Cp, P + o.q_b1, h->hp1[0], nullptr, h->Np, n),
@@ -590,6 +769,8 @@ bool same_batch(const sac_batch& a, const sac_batch& b) { return std::memcmp(&a,
 
 int run_step(sac_learner* h, const sac_batch* b, hipStream_t st) {
   auto body = [&](hipStream_t s) {
+    if (h->fused)
+      return h->bf16 ? enqueue_step_fused<__bf16>(h, b, s) : enqueue_step_fused<float>(h, b, s);
     return h->bf16 ? enqueue_step<__bf16>(h, b, s) : enqueue_step<float>(h, b, s);
   };
   if (!h->use_graph || h->timer_phase >= 0) return body(st);
@@ -694,6 +875,8 @@ int sac_create(const sac_config* cfg, int device, sac_learner** out) {
   h->off = offsets(h->D, h->K);
   const char* g = std::getenv("SAC_GRAPH");
   h->use_graph = !(g && g[0] == '0');
+  const char* fz = std::getenv("SAC_FUSED");
+  h->fused = !(fz && fz[0] == '0') && h->Cp <= H;  // the chain kernels stage K1 <= 256
   auto cleanup = [&](int code) {
     if (h->arena) (void)hipFree(h->arena);
     if (h->cap) (void)hipStreamDestroy(h->cap);

@@ -212,6 +212,36 @@ def test_sac_graph_replay_and_determinism_bitwise():
             np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("dtype,N,K", [("fp32", 256, 6), ("bf16", 256, 6), ("fp32", 37, 16),
+                                         ("bf16", 100, 1)])
+def test_sac_fused_chains_match_per_layer_bitwise(dtype, N, K):
+    """The per-row-block chain kernels (sac_fused.h, default) and the one-launch-per-layer
+    path (SAC_FUSED=0) give bitwise-identical parameters, gradients, metrics, priorities."""
+    dev = _dev()
+    D = 17
+    a0 = sac_cpu.flat(sac_cpu.make_models(D, K, seed=3)[0].parameters())
+    c0 = sac_cpu.flat(sac_cpu.make_models(D, K, seed=4)[1].critic.parameters())
+    outs = []
+    for fused in ("1", "0"):
+        os.environ["SAC_FUSED"] = fused
+        try:
+            actor, critic, tactor, eng = _setup(dev, D, K, N, dtype=dtype, actor0=a0, critic0=c0)
+        finally:
+            os.environ.pop("SAC_FUSED", None)
+        prios = []
+        for step in range(3):
+            batch, p, eps = _batch(N, D, K, 40 + step)
+            prios.append(_run(eng, batch, p, eps, dev))
+        q1, q2 = critic(torch.from_numpy(batch[0]).to(dev), torch.from_numpy(batch[1]).to(dev))
+        pol = actor.policy(torch.from_numpy(batch[0]).to(dev), noise=torch.from_numpy(eps[0]).to(dev))
+        outs.append([actor.flat, actor.flat_grad, critic.flat, critic.flat_grad, critic.target_flat,
+                     tactor.flat, critic.la_buf, eng.metrics, q1, q2, *pol])
+        outs[-1] = [t.cpu().numpy() for t in outs[-1]] + prios
+        eng.close()
+    for x, y in zip(*outs):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_sac_device_noise_seeded():
     """noise=None: the three rsample blocks come from the device generator keyed by (seed,
     learner step): same seed -> bitwise-equal runs, another seed -> different updates."""
