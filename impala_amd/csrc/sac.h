@@ -273,23 +273,27 @@ struct HeadArgs {
 };
 
 // one transition's head from its hidden-2 row (global or LDS), executed by one wave
+// (operands wm / bm / wl / bl / eps passed separately so they can live in LDS; eps row `er`
+// holds this transition's noise)
 template <typename T>
-DEV void head_row(const HeadJob& J, const T* hrow, int n, int N, int K, int lane) {
+DEV void head_row(const HeadJob& J, const float* wm, const float* bm, const float* wl,
+                  const float* bl, const float* eps_, const T* hrow, int n, int N, int K, int lane,
+                  int er) {
   float h[4];
   load4(hrow + 4 * lane, h);
   if (J.kind == HK_Q) {
-    const float q = dot_row(J.wm, lane, h) + J.bm[0];
+    const float q = dot_row(wm, lane, h) + bm[0];
     if (lane == 0) J.q[n] = q;
     return;
   }
   float logp = 0.f, stdsum = 0.f;
   for (int k = 0; k < K; ++k) {
-    const float mean = dot_row(J.wm + (size_t)k * H, lane, h) + J.bm[k];
-    const float u = dot_row(J.wl + (size_t)k * H, lane, h) + J.bl[k];
+    const float mean = dot_row(wm + (size_t)k * H, lane, h) + bm[k];
+    const float u = dot_row(wl + (size_t)k * H, lane, h) + bl[k];
     const float tu = tanhf(u);
     const float ls = add(-5.f, mul(3.5f, add(tu, 1.f)));  // LOG_STD_MIN + 0.5*(MAX-MIN)*(t+1)
     const float sd = expf(ls);
-    const float e = J.eps ? J.eps[(size_t)n * K + k] : 0.f;
+    const float e = eps_ ? eps_[(size_t)er * K + k] : 0.f;
     if (J.kind == HK_ACT) {
       const float x = add(mean, mul(mul(sd, e), J.noise_scale));
       const float y = add(mul(tanhf(x), J.act_scale), J.act_bias);
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(256) void heads_kernel(const HeadArgs g) {
   const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
   if (n >= g.N) return;
   const HeadJob& J = g.j[blockIdx.y];
-  head_row<T>(J, (const T*)J.h + (size_t)n * J.ldh, n, g.N, g.K, lane);
+  head_row<T>(J, J.wm, J.bm, J.wl, J.bl, J.eps, (const T*)J.h + (size_t)n * J.ldh, n, g.N, g.K, lane, n);
 }
 
 // =========================================================================================
@@ -360,45 +364,65 @@ struct CLossArgs {
   float* rowm;        // [8][ldt]
 };
 
-// TD target, weights, losses and dQ of one transition (t1, t2 = target-critic Q values);
-// lane 0 writes the per-transition metric terms and priority when `emit`, and dQ into row 0
-// of both dq_t operands.
-template <typename T>
-DEV void closs_row(const CLossArgs& a, float t1, float t2, int n, int lane, bool emit, float& dq1,
-                   float& dq2) {
-  // importance weights: probabilities.pow(-0.4) / max (learning.py:197-199)
-  float w = 1.f;
-  if (a.probs) {
-    float mx = 0.f;
-    for (int i = lane; i < a.N; i += 64) mx = fmaxf(mx, powf(a.probs[i], a.prio_exp));
-    w = __fdiv_rn(powf(a.probs[n], a.prio_exp), wave_max(mx));
+// one transition's inputs to critic_loss (loaded together: one memory round trip)
+struct CRow {
+  float p, lp1, r, q1, q2;
+  int done;
+};
+DEV CRow load_crow(const CLossArgs& a, int n) {
+  CRow c;
+  c.p = a.probs ? a.probs[n] : 1.f;
+  c.lp1 = a.logp1[n];
+  c.r = a.r[n];
+  c.q1 = a.q1[n];
+  c.q2 = a.q2[n];
+  c.done = a.done[n];
+  return c;
+}
+// importance-weight normaliser max_i probabilities[i]^-0.4 (learning.py:197-199), by one wave
+DEV float weight_max(const CLossArgs& a, int lane) {
+  float mx = 0.f;
+  for (int base = 0; base < a.N; base += 8 * 64) {  // 8 loads in flight per lane per round
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + lane + 64 * j;
+      v[j] = i < a.N ? a.probs[i] : -1.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (v[j] >= 0.f) mx = fmaxf(mx, powf(v[j], a.prio_exp));
   }
-  const float alpha = expf(a.log_alpha[0]);
-  const float mn = sub(fminf(t1, t2), mul(alpha, a.logp1[n]));
-  const float notd = a.done[n] ? 0.f : a.gamma;
-  const float y = add(a.r[n], mul(notd, mn));
-  const float q1 = a.q1[n], q2 = a.q2[n];
-  const float d1 = sub(y, q1), d2 = sub(y, q2);
+  return wave_max(mx);
+}
+// TD target, weights, losses and dQ of one transition (t1, t2 = target-critic Q values,
+// alpha = exp(log_alpha)); lane 0 writes the per-transition metric terms and priority when
+// `emit`, and dQ into row 0 of both dq_t operands.
+template <typename T>
+DEV void closs_row(const CLossArgs& a, const CRow& c, float alpha, float wmax, float t1, float t2,
+                   int n, int lane, bool emit, float& dq1, float& dq2) {
+  const float w = a.probs ? __fdiv_rn(powf(c.p, a.prio_exp), wmax) : 1.f;
+  const float mn = sub(fminf(t1, t2), mul(alpha, c.lp1));
+  const float notd = c.done ? 0.f : a.gamma;
+  const float y = add(c.r, mul(notd, mn));
+  const float d1 = sub(y, c.q1), d2 = sub(y, c.q2);
   const float wn = mul(__fdiv_rn(1.f, (float)a.N), w);
   dq1 = -mul(wn, mul(2.f, d1));
   dq2 = -mul(wn, mul(2.f, d2));
   if (lane == 0) {
     if (emit) {
-      if (a.prio) a.prio[n] = fabsf(sub(y, fminf(q1, q2)));
+      if (a.prio) a.prio[n] = fabsf(sub(y, fminf(c.q1, c.q2)));
       a.rowm[0 * a.ldt + n] = mul(mul(d1, d1), w);
       a.rowm[1 * a.ldt + n] = mul(mul(d2, d2), w);
-      a.rowm[2 * a.ldt + n] = q1;
-      a.rowm[3 * a.ldt + n] = q2;
+      a.rowm[2 * a.ldt + n] = c.q1;
+      a.rowm[3 * a.ldt + n] = c.q2;
     }
     ((T*)a.dq1t)[n] = to_t<T>(dq1);
     ((T*)a.dq2t)[n] = to_t<T>(dq2);
   }
 }
-// dh2 = dq * W3 (.) [h2 > 0] for the lane's 4 features of one row
-template <typename T>
-DEV void dq_to_dh(float dq, const float* w3, const T* h2row, int lane, float d[4]) {
-  float h[4];
-  load4(h2row + 4 * lane, h);
+// dh2 = dq * W3 (.) [h2 > 0] for the lane's 4 features of one row (h = those h2 values)
+DEV void dq_to_dh(float dq, const float* w3, const float h[4], int lane, float d[4]) {
   const f32x4 wv = load4f(w3 + 4 * lane);
 #pragma unroll
   for (int i = 0; i < 4; ++i) d[i] = h[i] > 0.f ? dq * wv[i] : 0.f;
@@ -415,11 +439,14 @@ __global__ __launch_bounds__(256) void critic_loss_kernel(const CLossArgs a) {
   load_row<T>(a.ht2, H, n, lane, h);
   const float t2 = dot_row(a.w3t2, lane, h) + a.b3t2[0];
   float dq[2];
-  closs_row<T>(a, t1, t2, n, lane, true, dq[0], dq[1]);
+  const CRow c = load_crow(a, n);
+  closs_row<T>(a, c, expf(a.log_alpha[0]), a.probs ? weight_max(a, lane) : 1.f, t1, t2, n, lane,
+               true, dq[0], dq[1]);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     float d[4];
-    dq_to_dh<T>(dq[q], q ? a.w3c2 : a.w3c1, (const T*)(q ? a.hc2 : a.hc1) + (size_t)n * H, lane, d);
+    load_row<T>(q ? a.hc2 : a.hc1, H, n, lane, h);
+    dq_to_dh(dq[q], q ? a.w3c2 : a.w3c1, h, lane, d);
     store4((T*)(q ? a.dh2 : a.dh1) + (size_t)n * H + 4 * lane, d);
     T* dt = (T*)(q ? a.dh2t : a.dh1t);
 #pragma unroll
@@ -443,12 +470,12 @@ struct ALossArgs {
 };
 
 // actor loss term and the dQ of both networks for one transition (q1, q2 on (s, pi))
-DEV void aloss_row(const ALossArgs& a, float q1, float q2, int n, int lane, float& dq1, float& dq2) {
-  const float alpha = expf(a.log_alpha[0]);
+DEV void aloss_row(const ALossArgs& a, float q1, float q2, float logp, float alpha, int n, int lane,
+                   float& dq1, float& dq2) {
   const float g = -__fdiv_rn(1.f, (float)a.N);
   dq1 = q1 < q2 ? g : (q1 == q2 ? 0.5f * g : 0.f);
   dq2 = q2 < q1 ? g : (q1 == q2 ? 0.5f * g : 0.f);
-  if (lane == 0) a.rowm[4 * a.ldt + n] = sub(mul(alpha, a.logp[n]), fminf(q1, q2));
+  if (lane == 0) a.rowm[4 * a.ldt + n] = sub(mul(alpha, logp), fminf(q1, q2));
 }
 
 template <typename T>
@@ -462,11 +489,11 @@ __global__ __launch_bounds__(256) void actor_loss_kernel(const ALossArgs a) {
   const float q1 = dot_row(a.w3c1, lane, h1) + a.b3c1[0];
   const float q2 = dot_row(a.w3c2, lane, h2) + a.b3c2[0];
   float dq[2];
-  aloss_row(a, q1, q2, n, lane, dq[0], dq[1]);
+  aloss_row(a, q1, q2, a.logp[n], expf(a.log_alpha[0]), n, lane, dq[0], dq[1]);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     float d[4];
-    dq_to_dh<T>(dq[q], q ? a.w3c2 : a.w3c1, (const T*)(q ? a.hp2 : a.hp1) + (size_t)n * H, lane, d);
+    dq_to_dh(dq[q], q ? a.w3c2 : a.w3c1, q ? h2 : h1, lane, d);
     store4((T*)(q ? a.dh2 : a.dh1) + (size_t)n * H + 4 * lane, d);
   }
 }
@@ -492,6 +519,7 @@ struct ABwdArgs {
   const float *wm, *wl;         // actor fc_mean / fc_logstd weights [K][256]
   const void* ha2;              // actor hidden-2 rows (T)
   int D, K, N, ldt;
+  int w1_so, w1_sk, w1_off;     // action column k of w1c at [o * w1_so + k * w1_sk + w1_off]
   void* dha2;                   // [N][256] (T)
   void* dha2t;                  // [256][ldt] (T)
   void *gmt, *gut;              // [16][ldt] (T): g_mean, g_u transposed
@@ -499,70 +527,72 @@ struct ABwdArgs {
 
 // one transition: d1/d2 = its ReLU-masked critic dh1 rows on (s, pi), ha2 = its actor hidden-2
 // row; writes dha2 (row-major when dha2_row, transposed into a.dha2t) and g_mean / g_u.
+// save / eps: row `si` of [4][NKs/K][K] / [.][K] blocks (global, or a row block staged in LDS).
+// sg: this wave's 2*MAXK floats of LDS for g_mean / g_u (every lane holds the same values; the
+// k loops stay rolled, so register use does not grow with MAXK).
+// hv: the lane's 4 actor hidden-2 values of the row (dha2 mask); alpha = exp(log_alpha)
 template <typename T>
-DEV void ahead_row(const ABwdArgs& a, const T* d1row, const T* d2row, const T* ha2row, T* dha2_row,
-                   int n, int lane) {
-  const int K = a.K, DK = a.D + a.K;
+DEV void ahead_row(const ABwdArgs& a, const T* d1row, const T* d2row, const float hv[4], T* dha2_row,
+                   int n, int lane, const float* save, const float* eps, int si, size_t NKs,
+                   float* sg, float alpha) {
+  const int K = a.K;
   float d1[4], d2[4];
   load4(d1row + 4 * lane, d1);
   load4(d2row + 4 * lane, d2);
-  const float c = mul(__fdiv_rn(1.f, (float)a.N), expf(a.log_alpha[0]));
-  const size_t NK = (size_t)a.N * K;
-  float gm[MAXK], gu[MAXK];  // static indices only (fully unrolled, k < K uniform)
-#pragma unroll
-  for (int k = 0; k < MAXK; ++k) {
-    gm[k] = gu[k] = 0.f;
-    if (k >= K) continue;
+  const float c = mul(__fdiv_rn(1.f, (float)a.N), alpha);
+#pragma unroll 1
+  for (int k = 0; k < K; ++k) {
     float p1 = 0.f, p2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int o = 4 * lane + i;
-      p1 += d1[i] * a.w1c1[(size_t)o * DK + a.D + k];
-      p2 += d2[i] * a.w1c2[(size_t)o * DK + a.D + k];
+      const size_t w = (size_t)(4 * lane + i) * a.w1_so + (size_t)k * a.w1_sk + a.w1_off;
+      p1 += d1[i] * a.w1c1[w];
+      p2 += d2[i] * a.w1c2[w];
     }
     const float dpi = wave_sum(p1) + wave_sum(p2);
-    const size_t o = (size_t)n * K + k;
-    const float sd = a.save[o], y = a.save[NK + o], xm = a.save[2 * NK + o], tu = a.save[3 * NK + o];
-    const float e = a.eps[o];
+    const size_t o = (size_t)si * K + k;
+    const float sd = save[o], y = save[NKs + o], xm = save[2 * NKs + o], tu = save[3 * NKs + o];
+    const float e = eps[o];
     const float var = sd * sd, omy = 1.f - y * y;
     const float gy = dpi + c * (2.f * y / (omy + 1e-6f));
     const float gx = gy * omy - c * xm / var;
-    gm[k] = gx + c * xm / var;
     const float gs = gx * e + c * (xm * xm) / (var * sd) - c / sd;
-    gu[k] = gs * sd * (3.5f * (1.f - tu * tu));
+    sg[k] = gx + c * xm / var;
+    sg[MAXK + k] = gs * sd * (3.5f * (1.f - tu * tu));
   }
-  float hv[4];
-  load4(ha2row + 4 * lane, hv);
+  float sacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int k = 0; k < K; ++k) {
+    const float gm = sg[k], gu = sg[MAXK + k];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hcol = 4 * lane + i;
+      sacc[i] += gm * a.wm[(size_t)k * H + hcol] + gu * a.wl[(size_t)k * H + hcol];
+    }
+  }
   float d[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int hcol = 4 * lane + i;
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k)
-      if (k < K) s += gm[k] * a.wm[(size_t)k * H + hcol] + gu[k] * a.wl[(size_t)k * H + hcol];
-    d[i] = hv[i] > 0.f ? s : 0.f;
-  }
+  for (int i = 0; i < 4; ++i) d[i] = hv[i] > 0.f ? sacc[i] : 0.f;
   if (dha2_row) store4(dha2_row + 4 * lane, d);
 #pragma unroll
   for (int i = 0; i < 4; ++i) ((T*)a.dha2t)[(size_t)(4 * lane + i) * a.ldt + n] = to_t<T>(d[i]);
   if (lane < K) {
-    float g1 = 0.f, g2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k)
-      if (k == lane) { g1 = gm[k]; g2 = gu[k]; }
-    ((T*)a.gmt)[(size_t)lane * a.ldt + n] = to_t<T>(g1);
-    ((T*)a.gut)[(size_t)lane * a.ldt + n] = to_t<T>(g2);
+    ((T*)a.gmt)[(size_t)lane * a.ldt + n] = to_t<T>(sg[lane]);
+    ((T*)a.gut)[(size_t)lane * a.ldt + n] = to_t<T>(sg[MAXK + lane]);
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void actor_head_bwd_kernel(const ABwdArgs a) {
+  __shared__ float sg[4][2 * MAXK];
   const int lane = threadIdx.x & 63;
   const int n = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
   if (n >= a.N) return;
-  ahead_row<T>(a, (const T*)a.dhp1 + (size_t)n * H, (const T*)a.dhp2 + (size_t)n * H,
-               (const T*)a.ha2 + (size_t)n * H, (T*)a.dha2 + (size_t)n * H, n, lane);
+  float hv[4];
+  load_row<T>(a.ha2, H, n, lane, hv);
+  ahead_row<T>(a, (const T*)a.dhp1 + (size_t)n * H, (const T*)a.dhp2 + (size_t)n * H, hv,
+               (T*)a.dha2 + (size_t)n * H, n, lane, a.save, a.eps, n, (size_t)a.N * a.K,
+               sg[threadIdx.x >> 6], expf(a.log_alpha[0]));
 }
 
 // =========================================================================================

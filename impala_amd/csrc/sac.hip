@@ -509,6 +509,7 @@ int enqueue_step(sac_learner* h, const sac_batch* b, hipStream_t st) {
     a.wm = S.actor + o.a_wm; a.wl = S.actor + o.a_wl;
     a.ha2 = h->ha2;
     a.D = D; a.K = K; a.N = N; a.ldt = Np;
+    a.w1_so = h->DK; a.w1_sk = 1; a.w1_off = D;
     a.dha2 = h->dha2; a.dha2t = h->dha2t; a.gmt = h->gmt; a.gut = h->gut;
     timer_begin(h, P_AHEAD, st);
     actor_head_bwd_kernel<T><<<cdiv(N, 4), 256, 0, st>>>(a);
@@ -573,7 +574,7 @@ int launch_chain(sac_learner* h, int ph, std::initializer_list<ChainJob> jobs, i
   a.K = h->K;
   a.ldt = h->Np;
   timer_begin(h, ph, st);
-  chain_fwd_kernel<T><<<dim3(cdiv(n, 16), nj), 256, 0, st>>>(a);
+  chain_fwd_kernel<T><<<dim3(cdiv(n, 16), nj), 64 * FW, 0, st>>>(a);
   timer_end(h, ph, st);
   SCK_LAUNCH(pname(ph));
   return 0;
@@ -644,7 +645,7 @@ int enqueue_step_fused(sac_learner* h, const sac_batch* b, hipStream_t st) {
       c.w2t[q] = h->kq[q].w2t; c.h1[q] = h->hc1[q]; c.dh1t[q] = h->dhc1t[q];
     }
     timer_begin(h, P_CCHAIN, st);
-    critic_chain_kernel<T><<<dim3(cdiv(N, 16), 2), 256, 0, st>>>(c);
+    critic_chain_kernel<T><<<dim3(cdiv(N, 16), 2), 64 * FW, 0, st>>>(c);
     timer_end(h, P_CCHAIN, st);
     SCK_LAUNCH("critic_loss_chain");
   }
@@ -673,6 +674,7 @@ int enqueue_step_fused(sac_learner* h, const sac_batch* b, hipStream_t st) {
     bb.wm = S.actor + o.a_wm; bb.wl = S.actor + o.a_wl;
     bb.ha2 = h->ha2;
     bb.D = D; bb.K = K; bb.N = N; bb.ldt = Np;
+    bb.w1_so = h->DK; bb.w1_sk = 1; bb.w1_off = D;  // the chain kernel restages them in LDS
     bb.dha2t = h->dha2t; bb.gmt = h->gmt; bb.gut = h->gut;
     c.xp = h->xp; c.ldx = h->Cp; c.K1 = h->Cp;
     for (int q = 0; q < 2; ++q) {
@@ -682,7 +684,7 @@ int enqueue_step_fused(sac_learner* h, const sac_batch* b, hipStream_t st) {
     }
     c.aw2t = h->ka.w2t; c.ha1 = h->ha1; c.dha1t = h->dha1t;
     timer_begin(h, P_ACHAIN, st);
-    actor_chain_kernel<T><<<cdiv(N, 16), 256, 0, st>>>(c);
+    actor_chain_kernel<T><<<cdiv(N, 16), 64 * FW, 0, st>>>(c);
     timer_end(h, P_ACHAIN, st);
     SCK_LAUNCH("actor_chain");
   }

@@ -9,10 +9,14 @@
 // Inside one workgroup the layer's weight rows stream from L2 (every row block reads the same
 // weights) and the activation operand comes from LDS.
 //
-// layer16: out[n][o] = epilogue(sum_k W[o][k] * in[n][k]) for the tile's 16 rows and all 256
-// outputs; 4 waves, wave w owns o in [64w, 64w + 64) as four 16x16 MFMA tiles.  The operand
-// roles, k order and epilogue arithmetic are those of gemm_jobs, so the fused and unfused
-// steps produce bitwise-identical results (tests/test_gpu_sac.py).
+// Workgroups are 16 waves (1024 threads): in a layer wave w owns the 16x16 output tile
+// o in [16w, 16w + 16); in a row phase wave w owns transition row w.  The small per-row
+// operands (head weights, W3, the critic's action columns, noise, saved head values) are staged
+// into LDS at kernel entry, so no row phase waits on a dependent global load.
+//
+// A layer: out[n][o] = epilogue(sum_k W[o][k] * in[n][k]) for the tile's 16 rows and all 256
+// outputs (mma_wf + epi16).  The operand roles, k order and epilogue arithmetic are those of
+// gemm_jobs, so the fused and unfused steps give bitwise-identical results (test_gpu_sac.py).
 #pragma once
 #include "sac.h"
 
@@ -25,82 +29,144 @@ template <typename T> struct Tile {
   static constexpr int SZ = 16 * LD;
 };
 
-// 16 rows (row0 .. row0 + 15, zero beyond nrows) of a [rows][ld] T matrix, K elements each
-// (K a multiple of 16 bytes), into an LDS tile of stride Tile<T>::LD
-template <typename T>
-DEV void load_tile(const T* __restrict__ src, int ld, int K, int row0, int nrows, T* dst) {
-  constexpr int VE = 16 / (int)sizeof(T);
-  const int vpr = K / VE;
-  for (int v = threadIdx.x; v < 16 * vpr; v += 256) {
-    const int r = v / vpr, c = (v - r * vpr) * VE;
-    f32x4 x = {0.f, 0.f, 0.f, 0.f};
-    if (row0 + r < nrows) x = *reinterpret_cast<const f32x4*>(src + (size_t)(row0 + r) * ld + c);
-    *reinterpret_cast<f32x4*>(dst + r * Tile<T>::LD + c) = x;
-  }
-}
+constexpr int FW = 16;  // waves per fused workgroup
 
-// MODE 0: relu(acc + bias);  MODE 1: acc masked by M[n][o] > 0 (ReLU backward).
-// out (LDS tile, nullable), g_rm (row-major [N][256], nullable), g_t (transposed [.][ldt]).
-template <typename T, int MODE>
-DEV void layer16(const T* __restrict__ W, int ldw, int K, const float* __restrict__ bias,
-                 const T* in, T* out, const T* M, int ldm, T* g_rm, T* g_t, int ldt, int row0,
-                 int nrows) {
+// This wave's A fragments (weight rows [16w, 16w + 16)) for k-steps [0, NS * KSTEP) of a layer,
+// loaded ahead of the layer that consumes them (one layer of look-ahead hides the L2/HBM
+// latency of the next weights behind the current layer's epilogue and row phase).
+template <typename T, int NS> struct WF {
+  typename Frag<T>::vec a[NS];
+};
+template <typename T> struct WFN {  // 256-deep layers / first layers with K1 <= 64
+  static constexpr int BIG = H / Frag<T>::KSTEP, SMALL = 64 / Frag<T>::KSTEP;
+};
+template <typename T, int NS>
+DEV WF<T, NS> load_wf(const T* __restrict__ W, int ldw, int K) {
+  using F = Frag<T>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const T* wp = W + (size_t)(16 * wave + (lane & 15)) * ldw + F::KPL * (lane >> 4);
+  WF<T, NS> w;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) w.a[s] = s * F::KSTEP < K ? F::load(wp + s * F::KSTEP) : F::zero();
+  return w;
+}
+// acc = sum_k W[o][k] in[n][k] from prefetched fragments (same k order as gemm_jobs)
+template <typename T, int NS>
+DEV f32x4 mma_wf(const WF<T, NS>& w, int K, const T* in) {
   using F = Frag<T>;
   typedef typename F::vec V;
+  const int lane = threadIdx.x & 63;
+  const T* ip = in + (lane & 15) * Tile<T>::LD + F::KPL * (lane >> 4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s * F::KSTEP < K) acc = F::mma(w.a[s], *reinterpret_cast<const V*>(ip + s * F::KSTEP), acc);
+  return acc;
+}
+// epilogue of a 16-row layer tile: MODE 0 relu(acc + bias) (bias in LDS), MODE 1 acc masked by
+// m (the lane's 4 mask values) > 0; stores to the LDS tile / row-major / transposed copies
+template <typename T, int MODE>
+DEV void epi16(f32x4 acc, const float* bias, const float m[4], T* out, T* g_rm, T* g_t, int ldt,
+               int row0, int nrows) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, c = lane & 15;
-  const int kl = F::KPL * g;
-  const T* wp = W + (size_t)(64 * wave + c) * ldw + kl;
-  const T* ip = in + c * Tile<T>::LD + kl;
-  f32x4 acc[4];
+  const int c = lane & 15, o = 16 * wave + 4 * (lane >> 4), n = row0 + c;
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int CH = 4;
-#pragma unroll 1
-  for (int k0 = 0; k0 < K; k0 += CH * F::KSTEP) {
-    V a[CH][4], b[CH];
+  for (int i = 0; i < 4; ++i) v[i] = MODE == 0 ? fmaxf(v[i] + bias[o + i], 0.f) : (m[i] > 0.f ? v[i] : 0.f);
+  if (out) store4(out + c * Tile<T>::LD + o, v);
+  if (n < nrows) {
+    if (g_rm) store4(g_rm + (size_t)n * H + o, v);
+    if (g_t) {
 #pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      const int k = k0 + s * F::KSTEP;
-      if (k < K) {
-        b[s] = *reinterpret_cast<const V*>(ip + k);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[s][j] = F::load(wp + (size_t)16 * j * ldw + k);
-      } else {
-        b[s] = F::zero();
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[s][j] = F::zero();
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < CH; ++s)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = F::mma(a[s][j], b[s], acc[j]);
-  }
-  const int n = row0 + c;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int o = 64 * wave + 16 * j + 4 * g;
-    float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-    if (MODE == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i] + bias[o + i], 0.f);
-    } else {
-      float m[4];
-      load4(M + (size_t)c * ldm + o, m);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] : 0.f;
-    }
-    if (out) store4(out + c * Tile<T>::LD + o, v);
-    if (n < nrows) {
-      if (g_rm) store4(g_rm + (size_t)n * H + o, v);
-      if (g_t) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) g_t[(size_t)(o + i) * ldt + n] = to_t<T>(v[i]);
-      }
+      for (int i = 0; i < 4; ++i) g_t[(size_t)(o + i) * ldt + n] = to_t<T>(v[i]);
     }
   }
 }
+// the lane's 4 mask values of a layer tile from LDS (row c, features o..o+3)
+template <typename T>
+DEV void tile_mask(const T* tile, float m[4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  load4(tile + (lane & 15) * Tile<T>::LD + 16 * wave + 4 * (lane >> 4), m);
+}
+// ... or from a global row-major [rows][256] matrix (zero beyond nrows)
+template <typename T>
+DEV void rows_mask(const T* rm, int row0, int nrows, float m[4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = row0 + (lane & 15);
+  m[0] = m[1] = m[2] = m[3] = 0.f;
+  if (n < nrows) load4(rm + (size_t)n * H + 16 * wave + 4 * (lane >> 4), m);
+}
+// Prologue staging in two passes -- every global load of the prologue is issued first (into
+// registers), then the LDS stores -- so the prologue costs one memory round trip, not one per
+// staged array.  M = elements per thread (n <= M * 1024).
+template <int M> struct Reg {
+  float v[M];
+  DEV void load(const float* __restrict__ src, int n) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int i = (int)threadIdx.x + j * FW * 64;
+      v[j] = i < n ? src[i] : 0.f;
+    }
+  }
+  DEV void store(float* dst, int n) const {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int i = (int)threadIdx.x + j * FW * 64;
+      if (i < n) dst[i] = v[j];
+    }
+  }
+};
+// one 16-byte vector per thread of a 16-row operand tile (16 x K elements, K*sizeof(T) <= 1 KB)
+template <typename T> struct TileReg {
+  f32x4 x;
+  int r, c;
+  bool ok;
+  DEV void load(const T* __restrict__ src, int ld, int K, int row0, int nrows) {
+    constexpr int VE = 16 / (int)sizeof(T);
+    const int vpr = K / VE, v = (int)threadIdx.x;
+    ok = v < 16 * vpr;
+    r = ok ? v / vpr : 0;
+    c = ok ? (v - r * vpr) * VE : 0;
+    x = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ok && row0 + r < nrows) x = *reinterpret_cast<const f32x4*>(src + (size_t)(row0 + r) * ld + c);
+  }
+  DEV void store(T* dst) const {
+    if (ok) *reinterpret_cast<f32x4*>(dst + r * Tile<T>::LD + c) = x;
+  }
+};
+
+// head operands staged into LDS (policy: fc_mean rows then fc_logstd rows, biases, the row
+// block's noise; Q: W3 and b3), loaded in the prologue's single round trip
+struct HeadStage {
+  Reg<MAXK * H / (FW * 64)> wm, wl;
+  Reg<1> b, e;
+  DEV void load(const HeadJob& J, int K, int row0, int N) {
+    if (J.kind == HK_Q) {
+      wm.load(J.wm, H);
+      b.load(J.bm, 1);
+      return;
+    }
+    wm.load(J.wm, K * H);
+    wl.load(J.wl, K * H);
+    // biases: thread t < K loads bm[t], K <= t < 2K loads bl[t - K]
+    const int t = threadIdx.x;
+    b.v[0] = t < K ? J.bm[t] : (t < 2 * K ? J.bl[t - K] : 0.f);
+    const int rows = min(16, N - row0);
+    e.load(J.eps ? J.eps + (size_t)row0 * K : nullptr, J.eps ? rows * K : 0);
+  }
+  // LDS copies: weights [2K][256] in sW (Q: W3 in row 0), biases in sB, noise rows in sE
+  DEV void store(const HeadJob& J, int K, float* sW, float* sB, float* sE) const {
+    if (J.kind == HK_Q) {
+      wm.store(sW, H);
+      b.store(sB, 1);
+      return;
+    }
+    wm.store(sW, K * H);
+    wl.store(sW + K * H, K * H);
+    b.store(sB, 2 * K);
+    e.store(sE, 16 * K);
+  }
+};
 
 // ---------------------------------------------------------------------------------------
 // chain_fwd_kernel: per row block and job, X -> Linear+ReLU -> Linear+ReLU -> head (policy
@@ -124,25 +190,45 @@ struct ChainArgs {
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void chain_fwd_kernel(const ChainArgs g) {
+__global__ __launch_bounds__(1024) void chain_fwd_kernel(const ChainArgs g) {
   __shared__ __attribute__((aligned(16))) T sX[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH1[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH2[Tile<T>::SZ];
+  __shared__ float sW[2 * MAXK * H], sB[2 * MAXK], sE[16 * MAXK], sBias[2][H];
   const ChainJob& J = g.j[blockIdx.y];
   const int row0 = blockIdx.x * 16;
-  load_tile<T>((const T*)J.x, J.ldx, J.K1, row0, g.N, sX);
+  constexpr int NB = WFN<T>::BIG, NS = WFN<T>::SMALL;
+  const bool small = J.K1 <= 64;
+  // issue order = use order (vmcnt retires loads in order): staged operands, W1, then W2,
+  // whose stream overlaps the LDS staging and the first layer
+  HeadStage hs;
+  hs.load(J.head, g.K, row0, g.N);
+  Reg<1> b1, b2;
+  b1.load(J.b1, H);
+  b2.load(J.b2, H);
+  TileReg<T> xt;
+  xt.load((const T*)J.x, J.ldx, J.K1, row0, g.N);
+  WF<T, NS> w1 = load_wf<T, NS>((const T*)J.w1, J.K1, small ? J.K1 : 0);
+  WF<T, NB> w2 = load_wf<T, NB>((const T*)J.w2, H, H);
+  hs.store(J.head, g.K, sW, sB, sE);
+  b1.store(sBias[0], H);
+  b2.store(sBias[1], H);
+  xt.store(sX);
   __syncthreads();
-  layer16<T, 0>((const T*)J.w1, J.K1, J.K1, J.b1, sX, sH1, nullptr, 0, (T*)J.h1, (T*)J.h1t, g.ldt,
-                row0, g.N);
-  __syncthreads();
-  layer16<T, 0>((const T*)J.w2, H, H, J.b2, sH1, sH2, nullptr, 0, (T*)J.h2, (T*)J.h2t, g.ldt,
-                row0, g.N);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int r = wave; r < 16; r += 4) {
-    const int n = row0 + r;
-    if (n < g.N) head_row<T>(J.head, sH2 + r * Tile<T>::LD, n, g.N, g.K, lane);
+  const float nom[4] = {0.f, 0.f, 0.f, 0.f};
+  if (small) {
+    epi16<T, 0>(mma_wf<T, NS>(w1, J.K1, sX), sBias[0], nom, sH1, (T*)J.h1, (T*)J.h1t, g.ldt, row0, g.N);
+  } else {  // wide first layer (64 < K1 <= 256): its fragments are fetched here
+    const WF<T, NB> wk = load_wf<T, NB>((const T*)J.w1, J.K1, J.K1);
+    epi16<T, 0>(mma_wf<T, NB>(wk, J.K1, sX), sBias[0], nom, sH1, (T*)J.h1, (T*)J.h1t, g.ldt, row0, g.N);
   }
+  __syncthreads();
+  epi16<T, 0>(mma_wf<T, NB>(w2, H, sH1), sBias[1], nom, sH2, (T*)J.h2, (T*)J.h2t, g.ldt, row0, g.N);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
+  if (row0 + r < g.N)
+    head_row<T>(J.head, sW, sB, sW + g.K * H, sB + g.K, J.head.eps ? sE : nullptr,
+                sH2 + r * Tile<T>::LD, row0 + r, g.N, g.K, lane, r);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -164,43 +250,77 @@ struct CChainArgs {
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void critic_chain_kernel(const CChainArgs g) {
+__global__ __launch_bounds__(1024) void critic_chain_kernel(const CChainArgs g) {
   __shared__ __attribute__((aligned(16))) T sX[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH1[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH2[Tile<T>::SZ];
-  __shared__ float st[2][16];
+  __shared__ float st[2][16], sW3[4][H], sB3[2], sBias[4][H], sWmax;
+  constexpr int NB = WFN<T>::BIG, NS = WFN<T>::SMALL;
   const CLossArgs& a = g.L;
   const int q = blockIdx.y;
   const int row0 = blockIdx.x * 16;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  load_tile<T>((const T*)g.xt, g.ldx, g.K1, row0, a.N, sX);
+  const int lane = threadIdx.x & 63, r = threadIdx.x >> 6, n = row0 + r;
+  const bool small = g.K1 <= 64;
+  // everything this block reads from memory is requested up front, in use order
+  CRow crow{};
+  const float la = a.log_alpha[0];
+  float h2m[4] = {0.f, 0.f, 0.f, 0.f}, h1m[4];
+  if (n < a.N) {
+    crow = load_crow(a, n);
+    load_row<T>(q ? a.hc2 : a.hc1, H, n, lane, h2m);
+  }
+  rows_mask<T>((const T*)g.h1[q], row0, a.N, h1m);
+  Reg<1> w3[4], bs[4];
+  w3[0].load(a.w3t1, H);
+  w3[1].load(a.w3t2, H);
+  w3[2].load(a.w3c1, H);
+  w3[3].load(a.w3c2, H);
+  bs[0].load(g.tb1[0], H);
+  bs[1].load(g.tb2[0], H);
+  bs[2].load(g.tb1[1], H);
+  bs[3].load(g.tb2[1], H);
+  const float b3v = threadIdx.x == 0 ? a.b3t1[0] : (threadIdx.x == 1 ? a.b3t2[0] : 0.f);
+  TileReg<T> xr;
+  xr.load((const T*)g.xt, g.ldx, g.K1, row0, a.N);
+  WF<T, NS> w1 = load_wf<T, NS>((const T*)g.tw1[0], g.K1, small ? g.K1 : 0);
+  WF<T, NB> w2 = load_wf<T, NB>((const T*)g.tw2[0], H, H);
+  float wm = 1.f;
+  if (r == 0 && a.probs) wm = weight_max(a, lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w3[i].store(sW3[i], H);
+    bs[i].store(sBias[i], H);
+  }
+  if (threadIdx.x < 2) sB3[threadIdx.x] = b3v;
+  if (threadIdx.x == 0) sWmax = wm;
+  xr.store(sX);
   __syncthreads();
-#pragma unroll 1
+  const float nom[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
   for (int c = 0; c < 2; ++c) {
-    layer16<T, 0>((const T*)g.tw1[c], g.K1, g.K1, g.tb1[c], sX, sH1, nullptr, 0, nullptr, nullptr,
-                  0, row0, a.N);
+    f32x4 acc = small ? mma_wf<T, NS>(w1, g.K1, sX)
+                      : mma_wf<T, NB>(load_wf<T, NB>((const T*)g.tw1[c], g.K1, g.K1), g.K1, sX);
+    if (c == 0) w1 = load_wf<T, NS>((const T*)g.tw1[1], g.K1, small ? g.K1 : 0);
+    epi16<T, 0>(acc, sBias[2 * c], nom, sH1, nullptr, nullptr, 0, row0, a.N);
     __syncthreads();
-    layer16<T, 0>((const T*)g.tw2[c], H, H, g.tb2[c], sH1, sH2, nullptr, 0, nullptr, nullptr, 0,
-                  row0, a.N);
+    acc = mma_wf<T, NB>(w2, H, sH1);
+    w2 = load_wf<T, NB>((const T*)(c == 0 ? g.tw2[1] : g.w2t[q]), H, H);  // next big layer
+    epi16<T, 0>(acc, sBias[2 * c + 1], nom, sH2, nullptr, nullptr, 0, row0, a.N);
     __syncthreads();
-    const float* w3 = c ? a.w3t2 : a.w3t1;
-    const float* b3 = c ? a.b3t2 : a.b3t1;
-    for (int r = wave; r < 16; r += 4) {
-      float h[4];
-      load4(sH2 + r * Tile<T>::LD + 4 * lane, h);
-      const float t = dot_row(w3, lane, h) + b3[0];
-      if (lane == 0) st[c][r] = t;
-    }
+    float h[4];
+    load4(sH2 + r * Tile<T>::LD + 4 * lane, h);
+    const float t = dot_row(sW3[c], lane, h) + sB3[c];
+    if (lane == 0) st[c][r] = t;
     __syncthreads();
   }
-  // TD target and dQ; dh2 of network q into the sH2 tile (rows beyond N stay zero)
-  for (int r = wave; r < 16; r += 4) {
-    const int n = row0 + r;
+  // TD target and dQ; dh2 of network q into the sH2 tile (rows beyond N zero)
+  {
     float d[4] = {0.f, 0.f, 0.f, 0.f};
     if (n < a.N) {
       float dq[2];
-      closs_row<T>(a, st[0][r], st[1][r], n, lane, q == 0, dq[0], dq[1]);
-      dq_to_dh<T>(dq[q], q ? a.w3c2 : a.w3c1, (const T*)(q ? a.hc2 : a.hc1) + (size_t)n * H, lane, d);
+      closs_row<T>(a, crow, expf(la), a.probs ? sWmax : 1.f, st[0][r], st[1][r], n, lane, q == 0,
+                   dq[0], dq[1]);
+      dq_to_dh(dq[q], sW3[2 + q], h2m, lane, d);
       T* dt = (T*)(q ? a.dh2t : a.dh1t);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dt[(size_t)(4 * lane + i) * a.ldt + n] = to_t<T>(d[i]);
@@ -208,8 +328,7 @@ __global__ __launch_bounds__(256) void critic_chain_kernel(const CChainArgs g) {
     store4(sH2 + r * Tile<T>::LD + 4 * lane, d);
   }
   __syncthreads();
-  layer16<T, 1>((const T*)g.w2t[q], H, H, nullptr, sH2, nullptr, (const T*)g.h1[q] + (size_t)row0 * H,
-                H, nullptr, (T*)g.dh1t[q], a.ldt, row0, a.N);
+  epi16<T, 1>(mma_wf<T, NB>(w2, H, sH2), nullptr, h1m, nullptr, nullptr, (T*)g.dh1t[q], a.ldt, row0, a.N);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -232,65 +351,136 @@ struct AChainArgs {
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void actor_chain_kernel(const AChainArgs g) {
+__global__ __launch_bounds__(1024) void actor_chain_kernel(const AChainArgs g) {
   __shared__ __attribute__((aligned(16))) T sX[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH1[2][Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH2[2][Tile<T>::SZ];
-  __shared__ float sq[2][16];
+  __shared__ float sq[2][16], sW3[2][H], sB3[2], sBias[4][H];
+  __shared__ float sA[2][MAXK * H];   // critic action columns, [k][o]
+  __shared__ float sWh[2][MAXK * H];  // actor fc_mean / fc_logstd rows
+  __shared__ float sS[4 * 16 * MAXK], sE[16 * MAXK], sG[16][2 * MAXK];
+  constexpr int NB = WFN<T>::BIG, NS = WFN<T>::SMALL;
   const ALossArgs& a = g.L;
-  const int N = a.N;
+  ABwdArgs bb = g.B;  // operands redirected into LDS
+  const int N = a.N, K = bb.K, DK = bb.D + bb.K;
   const int row0 = blockIdx.x * 16;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  load_tile<T>((const T*)g.xp, g.ldx, g.K1, row0, N, sX);
-  __syncthreads();
-#pragma unroll 1
+  const int lane = threadIdx.x & 63, r = threadIdx.x >> 6, n = row0 + r;
+  const bool small = g.K1 <= 64;
+  const float la = a.log_alpha[0];
+  float logp = 0.f, hv[4] = {0.f, 0.f, 0.f, 0.f}, ha1m[4];
+  if (n < N) {
+    logp = a.logp[n];
+    load_row<T>(bb.ha2, H, n, lane, hv);
+  }
+  rows_mask<T>((const T*)g.ha1, row0, N, ha1m);
+  constexpr int MK = MAXK * H / (FW * 64);
+  Reg<1> w3[2], bs[4];
+  w3[0].load(g.w3[0], H);
+  w3[1].load(g.w3[1], H);
+#pragma unroll
   for (int q = 0; q < 2; ++q) {
-    layer16<T, 0>((const T*)g.w1[q], g.K1, g.K1, g.b1[q], sX, sH1[q], nullptr, 0, nullptr, nullptr,
-                  0, row0, N);
-    __syncthreads();
-    layer16<T, 0>((const T*)g.w2[q], H, H, g.b2[q], sH1[q], sH2[q], nullptr, 0, nullptr, nullptr, 0,
-                  row0, N);
-    __syncthreads();
-    for (int r = wave; r < 16; r += 4) {
-      float h[4];
-      load4(sH2[q] + r * Tile<T>::LD + 4 * lane, h);
-      const float v = dot_row(g.w3[q], lane, h) + g.b3[q][0];
-      if (lane == 0) sq[q][r] = v;
+    bs[2 * q].load(g.b1[q], H);
+    bs[2 * q + 1].load(g.b2[q], H);
+  }
+  const float b3v = threadIdx.x < 2 ? g.b3[threadIdx.x][0] : 0.f;
+  float ca[2][MK];  // critic action columns, gathered [k][o] from [o][D + k]
+#pragma unroll
+  for (int j = 0; j < MK; ++j) {
+    const int i = (int)threadIdx.x + j * FW * 64, k = i / H, o = i - k * H;
+    const bool ok = i < K * H;
+    ca[0][j] = ok ? bb.w1c1[(size_t)o * DK + bb.D + k] : 0.f;
+    ca[1][j] = ok ? bb.w1c2[(size_t)o * DK + bb.D + k] : 0.f;
+  }
+  Reg<MK> whm, whl;
+  whm.load(bb.wm, K * H);
+  whl.load(bb.wl, K * H);
+  const size_t NK = (size_t)N * K;
+  const int rows = min(16, N - row0);
+  Reg<1> sv[4], ev;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sv[j].load(bb.save + j * NK + (size_t)row0 * K, rows * K);
+  ev.load(bb.eps + (size_t)row0 * K, rows * K);
+  TileReg<T> xr;
+  xr.load((const T*)g.xp, g.ldx, g.K1, row0, N);
+  WF<T, NS> w1 = load_wf<T, NS>((const T*)g.w1[0], g.K1, small ? g.K1 : 0);
+  WF<T, NB> w2 = load_wf<T, NB>((const T*)g.w2[0], H, H);
+  // ---- LDS stores (one round trip after the loads above were issued)
+  w3[0].store(sW3[0], H);
+  w3[1].store(sW3[1], H);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bs[i].store(sBias[i], H);
+  if (threadIdx.x < 2) sB3[threadIdx.x] = b3v;
+#pragma unroll
+  for (int j = 0; j < MK; ++j) {
+    const int i = (int)threadIdx.x + j * FW * 64;
+    if (i < K * H) {
+      sA[0][i] = ca[0][j];
+      sA[1][i] = ca[1][j];
     }
   }
+  whm.store(sWh[0], K * H);
+  whl.store(sWh[1], K * H);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sv[j].store(sS + j * 16 * K, 16 * K);
+  ev.store(sE, 16 * K);
+  xr.store(sX);
+  bb.w1c1 = sA[0]; bb.w1c2 = sA[1];
+  bb.w1_so = 1; bb.w1_sk = H; bb.w1_off = 0;
+  bb.wm = sWh[0]; bb.wl = sWh[1];
   __syncthreads();
-  for (int r = wave; r < 16; r += 4) {
-    const int n = row0 + r;
+  const float nom[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    f32x4 acc = small ? mma_wf<T, NS>(w1, g.K1, sX)
+                      : mma_wf<T, NB>(load_wf<T, NB>((const T*)g.w1[q], g.K1, g.K1), g.K1, sX);
+    if (q == 0) w1 = load_wf<T, NS>((const T*)g.w1[1], g.K1, small ? g.K1 : 0);
+    epi16<T, 0>(acc, sBias[2 * q], nom, sH1[q], nullptr, nullptr, 0, row0, N);
+    __syncthreads();
+    acc = mma_wf<T, NB>(w2, H, sH1[q]);
+    w2 = load_wf<T, NB>((const T*)(q == 0 ? g.w2[1] : g.w2t[0]), H, H);  // next big layer
+    epi16<T, 0>(acc, sBias[2 * q + 1], nom, sH2[q], nullptr, nullptr, 0, row0, N);
+    __syncthreads();
+    float h[4];
+    load4(sH2[q] + r * Tile<T>::LD + 4 * lane, h);
+    const float v = dot_row(sW3[q], lane, h) + sB3[q];
+    if (lane == 0) sq[q][r] = v;
+  }
+  __syncthreads();
+  {
+    const float alpha = expf(la);
     float dq[2] = {0.f, 0.f};
-    if (n < N) aloss_row(a, sq[0][r], sq[1][r], n, lane, dq[0], dq[1]);
+    if (n < N) aloss_row(a, sq[0][r], sq[1][r], logp, alpha, n, lane, dq[0], dq[1]);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       T* row = sH2[q] + r * Tile<T>::LD;
-      float d[4];
-      dq_to_dh<T>(dq[q], g.w3[q], row, lane, d);
+      float h[4], d[4];
+      load4(row + 4 * lane, h);
+      dq_to_dh(dq[q], sW3[q], h, lane, d);
       store4(row + 4 * lane, d);
     }
   }
   __syncthreads();
-#pragma unroll 1
-  for (int q = 0; q < 2; ++q)  // dh1_q in place of h1_q (each element read then written by one lane)
-    layer16<T, 1>((const T*)g.w2t[q], H, H, nullptr, sH2[q], sH1[q], sH1[q], Tile<T>::LD, nullptr,
-                  nullptr, 0, row0, N);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // dh1_q in place of h1_q (each element read then written by one lane)
+    const f32x4 acc = mma_wf<T, NB>(w2, H, sH2[q]);
+    w2 = load_wf<T, NB>((const T*)(q == 0 ? g.w2t[1] : g.aw2t), H, H);
+    float m[4];
+    tile_mask<T>(sH1[q], m);
+    epi16<T, 1>(acc, nullptr, m, sH1[q], nullptr, nullptr, 0, row0, N);
+  }
   __syncthreads();
-  for (int r = wave; r < 16; r += 4) {
-    const int n = row0 + r;
+  {
     T* dst = sH2[0] + r * Tile<T>::LD;  // dha2 tile (dh2 no longer needed)
     if (n < N) {
-      ahead_row<T>(g.B, sH1[0] + r * Tile<T>::LD, sH1[1] + r * Tile<T>::LD,
-                   (const T*)g.B.ha2 + (size_t)n * H, dst, n, lane);
+      ahead_row<T>(bb, sH1[0] + r * Tile<T>::LD, sH1[1] + r * Tile<T>::LD, hv, dst, n, lane, sS, sE,
+                   r, (size_t)16 * K, sG[r], expf(la));
     } else {
       float z[4] = {0.f, 0.f, 0.f, 0.f};
       store4(dst + 4 * lane, z);
     }
   }
   __syncthreads();
-  layer16<T, 1>((const T*)g.aw2t, H, H, nullptr, sH2[0], nullptr, (const T*)g.ha1 + (size_t)row0 * H,
-                H, nullptr, (T*)g.dha1t, a.ldt, row0, N);
+  epi16<T, 1>(mma_wf<T, NB>(w2, H, sH2[0]), nullptr, ha1m, nullptr, nullptr, (T*)g.dha1t, a.ldt, row0, N);
 }
 
 }  // namespace sac

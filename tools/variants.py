@@ -22,7 +22,8 @@ def build(name, edits):
     os.makedirs(OUT, exist_ok=True)
     out = os.path.join(OUT, name + ".so")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", out, os.path.join(src, "impala.hip")]
+           "-I", os.path.join(ROOT, "include"), "-o", out, os.path.join(src, "impala.hip"),
+           os.path.join(src, "sac.hip")]
     subprocess.run(cmd, check=True)
     shutil.rmtree(tmp)
     return out
