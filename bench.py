@@ -335,7 +335,10 @@ def run_sac(args):
         bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
-    step_flops = sum(work[k][0] for k in probe) * N if probe else None
+    # per-step algorithmic flops: the phases that ran (probe), else the fused step's phases
+    ran = probe or ("critic_fwd_chain", "critic_loss_chain", "critic_wgrad", "actor_chain",
+                    "actor_wgrad", "alpha_chain")
+    step_flops = sum(work[k][0] for k in ran) * N
     out = {
         "metric": "SAC learner transitions/sec (agents/sac, BASELINE config 5)",
         "value": round(value, 1), "unit": "transitions/s", "n_gpus": world, "steps": args.steps,
