@@ -134,6 +134,51 @@ def cpu_baseline(B, T, A, seconds):
                       f"{threads} threads, {cpu}) after 2 warm-up; median step {med * 1e3:.1f} ms"}
 
 
+def run_host_staged(eng, batch, args, dist, model, world):
+    """The PCIe-inclusive rate (SURVEY.md §8(d) secondary bound; never `value`): every step's
+    batch comes from page-locked host memory through the library's staging ring
+    (impala_stage, 2 slots), the H2D copies of step k+1 overlapping the update on step k."""
+    from impala_amd.distributed import compute_grads_allreduced
+    hosts = [[t.cpu().pin_memory() for t in batch] for _ in range(2)]
+    eng.stage_init(2)
+
+    def run(n):
+        eng.stage(0, *hosts[0])
+        for k in range(n):
+            s = k % 2
+            if k + 1 < n:
+                eng.stage(1 - s, *hosts[1 - s])
+            b = eng.slot_batch(s)
+            if dist is None:
+                eng.train_step(b)
+            else:
+                compute_grads_allreduced(eng, (b,), model.flat_grad)
+                eng.apply_update()
+            eng.slot_release(s)
+
+    run(max(args.warmup, 2))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=model.flat.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    nbytes = sum(t.numel() * t.element_size() for t in hosts[0])
+    return {"value": round(world * eng.frames * args.steps / elapsed, 1), "unit": "env-frames/s",
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "h2d_bytes_per_step": nbytes,
+            "h2d_GBps_per_gpu": round(nbytes * args.steps / elapsed / 1e9, 2),
+            "note": "rollouts staged from page-locked host memory every step (impala_stage ring, "
+                    "2 slots, H2D overlapped with the previous update); not `value`"}
+
+
 PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
                  "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "head_step": "head_step",
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
@@ -378,6 +423,8 @@ def main():
     ap.add_argument("--roofline-kernel", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-staged", action="store_true",
+                    help="skip the PCIe-inclusive pass (host batches through impala_stage)")
     ap.add_argument("--algo", default="impala", choices=["impala", "ppo", "sac"],
                     help="ppo: PPO learner step (BASELINE config 4) on --batch transitions "
                          "(default 256, conf/agent/ppo.yaml); sac: SAC learner step (config 5, "
@@ -511,6 +558,8 @@ def main():
     }
     if probe:
         out["kernel_probe_us"] = {k: round(v * 1e3, 2) for k, v in sorted(probe.items(), key=lambda kv: -kv[1])}
+    if not args.no_host_staged:
+        out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = (cpu_baseline_ppo(B, A, args.cpu_seconds) if ppo
                                else cpu_baseline(B, T, A, args.cpu_seconds))

@@ -34,6 +34,8 @@ EXPORTS = (
     "impala_apply_update", "impala_compute_grads_part", "impala_grad_bucket_offset",
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
+    "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
+    "impala_slot_release",
 )
 # every symbol declared in include/sac_hip.h
 SAC_EXPORTS = (
@@ -127,6 +129,11 @@ def _declare(lib):
                                      _P, _P, _P, _P, _P]
     lib.impala_gather_rows.argtypes = [C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_size_t),
                                        C.c_int, _P, C.c_int, _P]
+    lib.impala_stage_init.argtypes = [_P, C.c_int]
+    lib.impala_stage.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int]
+    lib.impala_stage_wait.argtypes = [_P, C.c_int]
+    lib.impala_slot_batch.argtypes = [_P, C.c_int, _P, C.POINTER(ImpalaBatch)]
+    lib.impala_slot_release.argtypes = [_P, C.c_int, _P]
     lib.impala_kernel_name.argtypes = [C.c_int]
     lib.impala_kernel_name.restype = C.c_char_p
     lib.impala_timer_start.argtypes = [_P, C.c_int, C.c_int]

@@ -41,14 +41,27 @@ def build(force: bool = False, verbose: bool = True) -> str:
         return OUT
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     tmp = OUT + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-o", tmp] + hip_units()
-    if verbose:
-        print(" ".join(cmd), flush=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             "-Wno-unused-function"]
+    # the units compile in parallel (sac.hip dominates), then one link
+    objs, procs = [], []
+    for src in hip_units():
+        obj = os.path.join(HERE, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmd = [hipcc] + flags + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((cmd, subprocess.Popen(cmd)))
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     if os.path.exists(tmp):
         os.remove(tmp)
-    subprocess.run(cmd, check=True)
+    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
+                   check=True)
     os.replace(tmp, OUT)
+    for obj in objs:
+        os.remove(obj)
     return OUT
 
 

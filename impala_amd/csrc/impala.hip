@@ -146,6 +146,17 @@ struct impala_learner {
   hipStream_t cap = nullptr;
   bool use_graph = false;
   uint64_t graph_tick = 0;
+  // host staging ring (impala_stage*): device batch slots filled by H2D copies on `h2d`;
+  // `ready` = the slot's copies are done, `done` = the steps that read it are done
+  struct StageSlot {
+    char* mem = nullptr;
+    impala_batch dev{};
+    hipEvent_t ready = nullptr, done = nullptr;
+  };
+  static constexpr int kMaxStageSlots = 8;
+  StageSlot ring[kMaxStageSlots];
+  int n_slots = 0;
+  hipStream_t h2d = nullptr;
 };
 
 namespace {
@@ -426,6 +437,18 @@ void drop_graphs(impala_learner* h) {
   }
 }
 
+void free_ring(impala_learner* h) {
+  if (h->h2d) (void)hipStreamSynchronize(h->h2d);
+  for (auto& s : h->ring) {
+    if (s.done) (void)hipEventSynchronize(s.done);
+    if (s.ready) (void)hipEventDestroy(s.ready);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.mem) (void)hipFree(s.mem);
+    s = impala_learner::StageSlot{};
+  }
+  h->n_slots = 0;
+}
+
 int check_bound(impala_learner* h, bool train = true) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (!h->params) return fail(IMPALA_E_STATE, "impala_bind_state() not called");
@@ -671,6 +694,8 @@ int impala_destroy(impala_learner* h) {
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();  // replays may still be in flight on the caller's streams
   drop_graphs(h);
+  free_ring(h);
+  if (h->h2d) (void)hipStreamDestroy(h->h2d);
   if (h->timer_ev) {
     for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
     delete[] h->timer_ev;
@@ -865,6 +890,89 @@ int impala_gather_rows(const void* const* src, void* const* dst, const size_t* r
   ga.n = n;
   gather_rows_kernel<<<dim3(n, nfields), 256, 0, (hipStream_t)stream>>>(ga);
   CK_LAUNCH("gather_rows");
+  return 0;
+}
+
+int impala_stage_init(impala_learner* h, int nslots) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (nslots < 1 || nslots > impala_learner::kMaxStageSlots)
+    return fail(IMPALA_E_INVALID, "nslots must be in [1, 8]");
+  CK(hipSetDevice(h->device));
+  free_ring(h);
+  if (!h->h2d) CK(hipStreamCreateWithFlags(&h->h2d, hipStreamNonBlocking));
+  const size_t N = (size_t)h->N;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_obs = take(N * 3 * 64 * 64), o_act = take(N * 8), o_rew = take(N * 4),
+               o_disc = take(N * 4), o_mu = take(N * (size_t)h->A * 4);
+  for (int i = 0; i < nslots; ++i) {
+    auto& s = h->ring[i];
+    hipError_t e = hipMalloc(&s.mem, off);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    // both events start recorded (complete), so the first stage / slot_batch never waits
+    if (e == hipSuccess) e = hipEventRecord(s.ready, h->h2d);
+    if (e == hipSuccess) e = hipEventRecord(s.done, h->h2d);
+    if (e != hipSuccess) {
+      free_ring(h);
+      return fail((int)e, std::string("impala_stage_init: ") + hipGetErrorString(e));
+    }
+    s.dev = impala_batch{(const uint8_t*)(s.mem + o_obs), (const int64_t*)(s.mem + o_act),
+                         (const float*)(s.mem + o_rew), (const float*)(s.mem + o_disc),
+                         (const float*)(s.mem + o_mu)};
+  }
+  h->n_slots = nslots;
+  return 0;
+}
+
+int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (slot < 0 || slot >= h->n_slots)
+    return fail(IMPALA_E_INVALID, "slot out of range (impala_stage_init not called?)");
+  const bool ppo = h->cfg.algo == IMPALA_ALGO_PPO;
+  if (!b || !b->obs || !b->actions || !b->rewards || (!ppo && !b->discounts) ||
+      !b->behaviour_logits)
+    return fail(IMPALA_E_INVALID, "null batch pointer");
+  CK(hipSetDevice(h->device));
+  auto& s = h->ring[slot];
+  const size_t N = (size_t)h->N;
+  CK(hipStreamWaitEvent(h->h2d, s.done, 0));  // the steps that read the slot have run
+  CK(hipMemcpyAsync((void*)s.dev.obs, b->obs, N * 3 * 64 * 64, hipMemcpyDefault, h->h2d));
+  CK(hipMemcpyAsync((void*)s.dev.actions, b->actions, N * 8, hipMemcpyDefault, h->h2d));
+  CK(hipMemcpyAsync((void*)s.dev.rewards, b->rewards, N * 4, hipMemcpyDefault, h->h2d));
+  if (b->discounts)
+    CK(hipMemcpyAsync((void*)s.dev.discounts, b->discounts, N * 4, hipMemcpyDefault, h->h2d));
+  CK(hipMemcpyAsync((void*)s.dev.behaviour_logits, b->behaviour_logits, N * (size_t)h->A * 4,
+                    hipMemcpyDefault, h->h2d));
+  CK(hipEventRecord(s.ready, h->h2d));
+  return 0;
+}
+
+int impala_stage_wait(impala_learner* h, int slot) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (slot < 0 || slot >= h->n_slots) return fail(IMPALA_E_INVALID, "slot out of range");
+  CK(hipEventSynchronize(h->ring[slot].ready));
+  return 0;
+}
+
+int impala_slot_batch(impala_learner* h, int slot, void* stream, impala_batch* out) {
+  if (!h || !out) return fail(IMPALA_E_INVALID, "null argument");
+  if (slot < 0 || slot >= h->n_slots) return fail(IMPALA_E_INVALID, "slot out of range");
+  CK(hipSetDevice(h->device));
+  CK(hipStreamWaitEvent((hipStream_t)stream, h->ring[slot].ready, 0));
+  *out = h->ring[slot].dev;
+  return 0;
+}
+
+int impala_slot_release(impala_learner* h, int slot, void* stream) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (slot < 0 || slot >= h->n_slots) return fail(IMPALA_E_INVALID, "slot out of range");
+  CK(hipSetDevice(h->device));
+  CK(hipEventRecord(h->ring[slot].done, (hipStream_t)stream));
   return 0;
 }
 

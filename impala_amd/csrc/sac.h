@@ -186,10 +186,19 @@ struct PackArgs {
   float* eps;                     // [3][N][K] when generated
   uint64_t seed;
   const int64_t* counter;
+  const float* probs;  // sampler probabilities (nullable) -> *wmax = max probs^prio_exp (1 if none)
+  float prio_exp;
+  float* wmax;         // nullable
 };
+
+DEV float probs_pow_max(const float* probs, int N, float e, int lane);
 
 template <typename T>
 __global__ __launch_bounds__(256) void pack_kernel(const PackArgs p) {
+  if (p.wmax && blockIdx.x == 0 && threadIdx.x < 64) {  // the IS-weight normaliser, once per step
+    const float m = p.probs ? probs_pow_max(p.probs, p.N, p.prio_exp, threadIdx.x) : 1.f;
+    if (threadIdx.x == 0) *p.wmax = m;
+  }
   const int DK = p.D + p.K;
   const long long tot = (long long)p.N * DK;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot; i += (long long)gridDim.x * 256) {
@@ -362,6 +371,7 @@ struct CLossArgs {
   void *dh1t, *dh2t;  // [256][ldt] (T)
   void *dq1t, *dq2t;  // [16][ldt] (T), row 0
   float* rowm;        // [8][ldt]
+  const float* wmax;  // fused path: the normaliser, computed by pack_kernel
 };
 
 // one transition's inputs to critic_loss (loaded together: one memory round trip)
@@ -371,7 +381,9 @@ struct CRow {
 };
 DEV CRow load_crow(const CLossArgs& a, int n) {
   CRow c;
-  c.p = a.probs ? a.probs[n] : 1.f;
+  // pointer select, not value select (closs_row ignores p without probabilities): a "load or
+  // constant" select becomes a branch with a full vmcnt wait
+  c.p = (a.probs ? a.probs : a.r)[n];
   c.lp1 = a.logp1[n];
   c.r = a.r[n];
   c.q1 = a.q1[n];
@@ -380,21 +392,20 @@ DEV CRow load_crow(const CLossArgs& a, int n) {
   return c;
 }
 // importance-weight normaliser max_i probabilities[i]^-0.4 (learning.py:197-199), by one wave
-DEV float weight_max(const CLossArgs& a, int lane) {
+DEV float probs_pow_max(const float* probs, int N, float e, int lane) {
   float mx = 0.f;
-  for (int base = 0; base < a.N; base += 8 * 64) {  // 8 loads in flight per lane per round
+  for (int base = 0; base < N; base += 8 * 64) {  // 8 loads in flight per lane per round
+    // unconditional loads (indices past N re-read element N - 1), the range test at use
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = base + lane + 64 * j;
-      v[j] = i < a.N ? a.probs[i] : -1.f;
-    }
+    for (int j = 0; j < 8; ++j) v[j] = probs[min(base + lane + 64 * j, N - 1)];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (v[j] >= 0.f) mx = fmaxf(mx, powf(v[j], a.prio_exp));
+      if (base + lane + 64 * j < N) mx = fmaxf(mx, powf(v[j], e));
   }
   return wave_max(mx);
 }
+DEV float weight_max(const CLossArgs& a, int lane) { return probs_pow_max(a.probs, a.N, a.prio_exp, lane); }
 // TD target, weights, losses and dQ of one transition (t1, t2 = target-critic Q values,
 // alpha = exp(log_alpha)); lane 0 writes the per-transition metric terms and priority when
 // `emit`, and dQ into row 0 of both dq_t operands.

@@ -132,7 +132,7 @@ struct sac_learner {
   void *dha2 = nullptr, *dha2t = nullptr, *dha1t = nullptr, *gmt = nullptr, *gut = nullptr;
   // fp32 scratch
   float *q1 = nullptr, *q2 = nullptr, *logp1 = nullptr, *logp = nullptr, *logp2 = nullptr;
-  float *save = nullptr, *rowm = nullptr, *eps = nullptr, *sq_c = nullptr, *sq_a = nullptr;
+  float *save = nullptr, *rowm = nullptr, *eps = nullptr, *sq_c = nullptr, *sq_a = nullptr, *wmax = nullptr;
   int nsq_c = 0, nsq_a = 0;
   int64_t* steps = nullptr;  // critic, actor, alpha, learner
   MlpK ka{}, kta{}, kq[2]{}, ktq[2]{};
@@ -212,6 +212,7 @@ void carve(sac_learner* h) {
   h->save = F(4 * NK);
   h->rowm = F(8LL * Np);
   h->eps = F(3 * NK);
+  h->wmax = F(4);
   // norm slots: one per weight-gradient tile
   const int t_w2 = 16 * cdiv(H + 1, 16), t_w3 = cdiv(H + 1, 16);
   const int t_w1c = 16 * cdiv(h->DK + 1, 16), t_w1a = 16 * cdiv(h->D + 1, 16);
@@ -600,6 +601,7 @@ int enqueue_step_fused(sac_learner* h, const sac_batch* b, hipStream_t st) {
     p.eps = b->noise ? nullptr : h->eps;
     p.seed = h->cfg.seed;
     p.counter = h->steps + 3;
+    p.probs = b->probabilities; p.prio_exp = -h->cfg.prio_exponent; p.wmax = h->wmax;
     timer_begin(h, P_PACK, st);
     pack_kernel<T><<<std::max(1, std::min(256, cdiv(std::max((long long)N * h->DK, 3 * NK), 256))), 256, 0, st>>>(p);
     timer_end(h, P_PACK, st);
@@ -638,6 +640,7 @@ int enqueue_step_fused(sac_learner* h, const sac_batch* b, hipStream_t st) {
     a.dh1t = h->dh2t[0]; a.dh2t = h->dh2t[1];
     a.dq1t = h->dqt[0]; a.dq2t = h->dqt[1];
     a.rowm = h->rowm;
+    a.wmax = h->wmax;
     c.xt = h->xt; c.ldx = h->Cp; c.K1 = h->Cp;
     for (int q = 0; q < 2; ++q) {
       c.tw1[q] = h->ktq[q].w1; c.tw2[q] = h->ktq[q].w2;

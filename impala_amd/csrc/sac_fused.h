@@ -46,8 +46,15 @@ DEV WF<T, NS> load_wf(const T* __restrict__ W, int ldw, int K) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const T* wp = W + (size_t)(16 * wave + (lane & 15)) * ldw + F::KPL * (lane >> 4);
   WF<T, NS> w;
+  // k-steps at or beyond K load the last real k-step again (mma_wf skips them): a per-element
+  // "load or zero" select compiles to a branch and a vmcnt(0) wait per fragment
+  if (K > 0) {
 #pragma unroll
-  for (int s = 0; s < NS; ++s) w.a[s] = s * F::KSTEP < K ? F::load(wp + s * F::KSTEP) : F::zero();
+    for (int s = 0; s < NS; ++s) w.a[s] = F::load(wp + min(s * F::KSTEP, K - F::KSTEP));
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) w.a[s] = F::zero();
+  }
   return w;
 }
 // acc = sum_k W[o][k] in[n][k] from prefetched fragments (same k order as gemm_jobs)
@@ -88,25 +95,29 @@ DEV void tile_mask(const T* tile, float m[4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   load4(tile + (lane & 15) * Tile<T>::LD + 16 * wave + 4 * (lane >> 4), m);
 }
-// ... or from a global row-major [rows][256] matrix (zero beyond nrows)
+// ... or from a global row-major [rows][256] matrix.  Rows beyond nrows read the last row (an
+// unconditional load; see Reg): they only reach tile rows that are never stored.
 template <typename T>
 DEV void rows_mask(const T* rm, int row0, int nrows, float m[4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n = row0 + (lane & 15);
-  m[0] = m[1] = m[2] = m[3] = 0.f;
-  if (n < nrows) load4(rm + (size_t)n * H + 16 * wave + 4 * (lane >> 4), m);
+  const int n = min(row0 + (lane & 15), nrows - 1);
+  load4(rm + (size_t)n * H + 16 * wave + 4 * (lane >> 4), m);
 }
 // Prologue staging in two passes -- every global load of the prologue is issued first (into
 // registers), then the LDS stores -- so the prologue costs one memory round trip, not one per
-// staged array.  M = elements per thread (n <= M * 1024).
+// staged array.  M = elements per thread (n <= M * 1024).  The loads are unconditional (index
+// clamped to n - 1; store() writes only i < n): a per-element "load or 0" select makes hipcc
+// branch around each load with a vmcnt(0) wait, which serialises the prologue.
 template <int M> struct Reg {
   float v[M];
   DEV void load(const float* __restrict__ src, int n) {
+    if (n <= 0) {  // wave-uniform
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-      const int i = (int)threadIdx.x + j * FW * 64;
-      v[j] = i < n ? src[i] : 0.f;
+      for (int j = 0; j < M; ++j) v[j] = 0.f;
+      return;
     }
+#pragma unroll
+    for (int j = 0; j < M; ++j) v[j] = src[min((int)threadIdx.x + j * FW * 64, n - 1)];
   }
   DEV void store(float* dst, int n) const {
 #pragma unroll
@@ -139,7 +150,7 @@ template <typename T> struct TileReg {
 // block's noise; Q: W3 and b3), loaded in the prologue's single round trip
 struct HeadStage {
   Reg<MAXK * H / (FW * 64)> wm, wl;
-  Reg<1> b, e;
+  Reg<1> b, b2, e;
   DEV void load(const HeadJob& J, int K, int row0, int N) {
     if (J.kind == HK_Q) {
       wm.load(J.wm, H);
@@ -148,9 +159,8 @@ struct HeadStage {
     }
     wm.load(J.wm, K * H);
     wl.load(J.wl, K * H);
-    // biases: thread t < K loads bm[t], K <= t < 2K loads bl[t - K]
-    const int t = threadIdx.x;
-    b.v[0] = t < K ? J.bm[t] : (t < 2 * K ? J.bl[t - K] : 0.f);
+    b.load(J.bm, K);   // fc_mean bias (thread t < K) ...
+    b2.load(J.bl, K);  // ... and fc_logstd bias, merged at store time
     const int rows = min(16, N - row0);
     e.load(J.eps ? J.eps + (size_t)row0 * K : nullptr, J.eps ? rows * K : 0);
   }
@@ -163,7 +173,8 @@ struct HeadStage {
     }
     wm.store(sW, K * H);
     wl.store(sW + K * H, K * H);
-    b.store(sB, 2 * K);
+    b.store(sB, K);
+    b2.store(sB + K, K);
     e.store(sE, 16 * K);
   }
 };
@@ -254,7 +265,7 @@ __global__ __launch_bounds__(1024) void critic_chain_kernel(const CChainArgs g) 
   __shared__ __attribute__((aligned(16))) T sX[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH1[Tile<T>::SZ];
   __shared__ __attribute__((aligned(16))) T sH2[Tile<T>::SZ];
-  __shared__ float st[2][16], sW3[4][H], sB3[2], sBias[4][H], sWmax;
+  __shared__ float st[2][16], sW3[4][H], sB3[2], sBias[4][H];
   constexpr int NB = WFN<T>::BIG, NS = WFN<T>::SMALL;
   const CLossArgs& a = g.L;
   const int q = blockIdx.y;
@@ -262,13 +273,12 @@ __global__ __launch_bounds__(1024) void critic_chain_kernel(const CChainArgs g) 
   const int lane = threadIdx.x & 63, r = threadIdx.x >> 6, n = row0 + r;
   const bool small = g.K1 <= 64;
   // everything this block reads from memory is requested up front, in use order
-  CRow crow{};
+  // (rows beyond N load row N - 1 -- no branch around the loads -- and are never used)
+  const int nc = min(n, a.N - 1);
+  const CRow crow = load_crow(a, nc);
   const float la = a.log_alpha[0];
-  float h2m[4] = {0.f, 0.f, 0.f, 0.f}, h1m[4];
-  if (n < a.N) {
-    crow = load_crow(a, n);
-    load_row<T>(q ? a.hc2 : a.hc1, H, n, lane, h2m);
-  }
+  float h2m[4], h1m[4];
+  load_row<T>(q ? a.hc2 : a.hc1, H, nc, lane, h2m);
   rows_mask<T>((const T*)g.h1[q], row0, a.N, h1m);
   Reg<1> w3[4], bs[4];
   w3[0].load(a.w3t1, H);
@@ -279,20 +289,18 @@ __global__ __launch_bounds__(1024) void critic_chain_kernel(const CChainArgs g) 
   bs[1].load(g.tb2[0], H);
   bs[2].load(g.tb1[1], H);
   bs[3].load(g.tb2[1], H);
-  const float b3v = threadIdx.x == 0 ? a.b3t1[0] : (threadIdx.x == 1 ? a.b3t2[0] : 0.f);
+  const float b3a = a.b3t1[0], b3b = a.b3t2[0];
   TileReg<T> xr;
   xr.load((const T*)g.xt, g.ldx, g.K1, row0, a.N);
   WF<T, NS> w1 = load_wf<T, NS>((const T*)g.tw1[0], g.K1, small ? g.K1 : 0);
   WF<T, NB> w2 = load_wf<T, NB>((const T*)g.tw2[0], H, H);
-  float wm = 1.f;
-  if (r == 0 && a.probs) wm = weight_max(a, lane);
+  const float wm = a.wmax[0];  // IS-weight normaliser (pack_kernel; 1 without probabilities)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     w3[i].store(sW3[i], H);
     bs[i].store(sBias[i], H);
   }
-  if (threadIdx.x < 2) sB3[threadIdx.x] = b3v;
-  if (threadIdx.x == 0) sWmax = wm;
+  if (threadIdx.x < 2) sB3[threadIdx.x] = threadIdx.x ? b3b : b3a;
   xr.store(sX);
   __syncthreads();
   const float nom[4] = {0.f, 0.f, 0.f, 0.f};
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(1024) void critic_chain_kernel(const CChainArgs g) 
     float d[4] = {0.f, 0.f, 0.f, 0.f};
     if (n < a.N) {
       float dq[2];
-      closs_row<T>(a, crow, expf(la), a.probs ? sWmax : 1.f, st[0][r], st[1][r], n, lane, q == 0,
+      closs_row<T>(a, crow, expf(la), wm, st[0][r], st[1][r], n, lane, q == 0,
                    dq[0], dq[1]);
       dq_to_dh(dq[q], sW3[2 + q], h2m, lane, d);
       T* dt = (T*)(q ? a.dh2t : a.dh1t);
@@ -367,11 +375,11 @@ __global__ __launch_bounds__(1024) void actor_chain_kernel(const AChainArgs g) {
   const int lane = threadIdx.x & 63, r = threadIdx.x >> 6, n = row0 + r;
   const bool small = g.K1 <= 64;
   const float la = a.log_alpha[0];
-  float logp = 0.f, hv[4] = {0.f, 0.f, 0.f, 0.f}, ha1m[4];
-  if (n < N) {
-    logp = a.logp[n];
-    load_row<T>(bb.ha2, H, n, lane, hv);
-  }
+  // (rows beyond N load row N - 1 -- no branch around the loads -- and are never used)
+  const int nc = min(n, N - 1);
+  const float logp = a.logp[nc];
+  float hv[4], ha1m[4];
+  load_row<T>(bb.ha2, H, nc, lane, hv);
   rows_mask<T>((const T*)g.ha1, row0, N, ha1m);
   constexpr int MK = MAXK * H / (FW * 64);
   Reg<1> w3[2], bs[4];
@@ -382,14 +390,14 @@ __global__ __launch_bounds__(1024) void actor_chain_kernel(const AChainArgs g) {
     bs[2 * q].load(g.b1[q], H);
     bs[2 * q + 1].load(g.b2[q], H);
   }
-  const float b3v = threadIdx.x < 2 ? g.b3[threadIdx.x][0] : 0.f;
-  float ca[2][MK];  // critic action columns, gathered [k][o] from [o][D + k]
+  const float b3a = g.b3[0][0], b3b = g.b3[1][0];
+  float ca[2][MK];  // critic action columns, gathered [k][o] from [o][D + k] (index clamped:
+                    // unconditional loads, only i < K * H is stored)
 #pragma unroll
   for (int j = 0; j < MK; ++j) {
-    const int i = (int)threadIdx.x + j * FW * 64, k = i / H, o = i - k * H;
-    const bool ok = i < K * H;
-    ca[0][j] = ok ? bb.w1c1[(size_t)o * DK + bb.D + k] : 0.f;
-    ca[1][j] = ok ? bb.w1c2[(size_t)o * DK + bb.D + k] : 0.f;
+    const int i = min((int)threadIdx.x + j * FW * 64, K * H - 1), k = i / H, o = i - k * H;
+    ca[0][j] = bb.w1c1[(size_t)o * DK + bb.D + k];
+    ca[1][j] = bb.w1c2[(size_t)o * DK + bb.D + k];
   }
   Reg<MK> whm, whl;
   whm.load(bb.wm, K * H);
@@ -409,7 +417,7 @@ __global__ __launch_bounds__(1024) void actor_chain_kernel(const AChainArgs g) {
   w3[1].store(sW3[1], H);
 #pragma unroll
   for (int i = 0; i < 4; ++i) bs[i].store(sBias[i], H);
-  if (threadIdx.x < 2) sB3[threadIdx.x] = b3v;
+  if (threadIdx.x < 2) sB3[threadIdx.x] = threadIdx.x ? b3b : b3a;
 #pragma unroll
   for (int j = 0; j < MK; ++j) {
     const int i = (int)threadIdx.x + j * FW * 64;

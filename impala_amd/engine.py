@@ -129,10 +129,14 @@ class Engine:
                                    sp), "impala_forward")
         return logits, values
 
-    def _batch(self, *batch) -> ImpalaBatch:
+    def _batch(self, *batch, device=None) -> ImpalaBatch:
         """IMPALA: (obs u8 [B,T,3,64,64], actions i64 [B,T], rewards [B,T], discounts [B,T],
         behaviour logits [B,T,A]).  PPO: (obs u8 [N,3,64,64], actions i64 [N], value targets
-        [N], behaviour logits [N,A]) -- passed to the library with rewards = targets."""
+        [N], behaviour logits [N,A]) -- passed to the library with rewards = targets.
+        A single ImpalaBatch (a staging-ring slot, slot_batch) passes through unchanged."""
+        if len(batch) == 1 and isinstance(batch[0], ImpalaBatch):
+            return batch[0]
+        device = self.device if device is None else torch.device(device)
         B, T, A = self.batch_size, self.rollout_length, self.num_actions
         if self.algo == "ppo":
             names = ("obs", "actions", "targets", "behaviour_logits")
@@ -147,8 +151,8 @@ class Engine:
         for k, t, (shape, dt) in zip(names, batch, exp):
             if tuple(t.shape) != shape or t.dtype != dt:
                 raise ValueError(f"{k}: expected {dt} {shape}, got {t.dtype} {tuple(t.shape)}")
-            if t.device != self.device or not t.is_contiguous():
-                raise ValueError(f"{k}: must be a contiguous tensor on {self.device}")
+            if t.device != device or not t.is_contiguous():
+                raise ValueError(f"{k}: must be a contiguous tensor on {device}")
         if self.algo == "ppo":
             obs, actions, targets, mu = batch
             return ImpalaBatch(ptr(obs), ptr(actions), ptr(targets), None, ptr(mu))
@@ -187,6 +191,39 @@ class Engine:
     def apply_update(self, stream=None):
         check(_lib.lib().impala_apply_update(self._h, stream_ptr(stream)), "impala_apply_update")
         self._updated()
+
+    # ------------------------------------------------------------------ host staging ring
+    def stage_init(self, nslots: int = 2):
+        """Allocate `nslots` device batch slots (impala_stage_init)."""
+        check(_lib.lib().impala_stage_init(self._h, int(nslots)), "impala_stage_init")
+        self.n_slots = int(nslots)
+        self._staged = [None] * self.n_slots
+
+    def stage(self, slot: int, *host_batch):
+        """Enqueue the H2D copies of a host batch (train_step's layout; page-locked memory for
+        an asynchronous copy) into ring slot `slot`, after the last step that read the slot."""
+        b = self._batch(*host_batch, device="cpu")
+        check(_lib.lib().impala_stage(self._h, C.byref(b), int(slot)), "impala_stage")
+        self._staged[slot] = host_batch  # the copies read these until stage_wait(slot)
+
+    def stage_wait(self, slot: int):
+        """Block until the copies into `slot` are done (its host batch may be reused)."""
+        check(_lib.lib().impala_stage_wait(self._h, int(slot)), "impala_stage_wait")
+        self._staged[slot] = None
+
+    def slot_batch(self, slot: int, stream=None) -> ImpalaBatch:
+        """The slot's device batch for train_step / compute_grads*; `stream` (torch's current
+        when None) waits for the slot's copies."""
+        b = ImpalaBatch()
+        check(_lib.lib().impala_slot_batch(self._h, int(slot), stream_ptr(stream), C.byref(b)),
+              "impala_slot_batch")
+        return b
+
+    def slot_release(self, slot: int, stream=None):
+        """The steps reading `slot` are enqueued on `stream`: the next stage() into it waits
+        for them."""
+        check(_lib.lib().impala_slot_release(self._h, int(slot), stream_ptr(stream)),
+              "impala_slot_release")
 
     # ------------------------------------------------------------------ live launch timer
     @staticmethod

@@ -107,13 +107,51 @@ class ImpalaLearner(Learner):
     def prepare(self):  # learning.py:116-117
         self._replay_buffer.warm_up(self._learning_starts)
 
+    def _stage_host(self, batch):
+        """learning.py:121-123,142 for host trajectories: collate into this step's page-locked
+        ring buffers and stage them through the library's H2D ring (impala_stage, two slots:
+        the copies of step k+1 wait only for the step that last read the slot).
+        -> (slot, the slot's device ImpalaBatch)."""
+        e = self._engine
+        if getattr(e, "n_slots", 0) == 0:
+            e.stage_init(2)
+            self._host_bufs = [None] * e.n_slots
+        self._slot = slot = (getattr(self, "_slot", -1) + 1) % e.n_slots
+        e.stage_wait(slot)  # the previous copies out of this slot's host buffers are done
+        if self._host_bufs[slot] is None:
+            B, T, A = self._batch_size, self._rollout_length, e.num_actions
+            pin = torch.cuda.is_available()
+            self._host_bufs[slot] = (
+                torch.empty(B, T, 3, 64, 64, dtype=torch.uint8, pin_memory=pin),
+                torch.empty(B, T, dtype=torch.int64, pin_memory=pin),
+                torch.empty(B, T, dtype=torch.float32, pin_memory=pin),
+                torch.empty(B, T, dtype=torch.float32, pin_memory=pin),
+                torch.empty(B, T, A, dtype=torch.float32, pin_memory=pin))
+        bufs = self._host_bufs[slot]
+        if len(batch) != bufs[0].shape[0]:
+            raise ValueError(f"replay returned {len(batch)} trajectories, expected {bufs[0].shape[0]}")
+        for i, item in enumerate(batch):
+            for j, buf in enumerate(bufs):
+                buf[i].copy_(item[j].reshape(buf.shape[1:]))
+        e.stage(slot, *bufs)
+        return slot, e.slot_batch(slot)
+
     def train_step(self):  # learning.py:119-138
         t0 = time.perf_counter()
         _, batch, _ = self._replay_buffer.sample(self._batch_size)
-        batch = _collate(batch, self.device())
-        n_samples = self._batch_size * batch[0].shape[1]
+        slot = None
+        if isinstance(batch, list) and batch and isinstance(batch[0][0], torch.Tensor) \
+                and batch[0][0].device.type == "cpu":
+            slot, b = self._stage_host(batch)
+            batch = (b,)
+            n_samples = self._batch_size * self._rollout_length
+        else:
+            batch = _collate(batch, self.device())
+            n_samples = self._batch_size * batch[0].shape[1]
         t1 = time.perf_counter()
         metrics = self._train_step(batch)
+        if slot is not None:
+            self._engine.slot_release(slot)
         t2 = time.perf_counter()
         update_time = 0
         self._step_count += 1

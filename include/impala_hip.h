@@ -158,6 +158,25 @@ size_t impala_grad_bucket_offset(const impala_learner* h);
 int impala_gather_rows(const void* const* src, void* const* dst, const size_t* row_bytes,
                        int nfields, const int64_t* idx, int n, void* stream);
 
+/* Host staging ring (SURVEY.md §8(b) impala_stage; replaces the 5·B pageable `.to(device)`
+ * copies of learning.py:121-123).  The handle owns `nslots` device batch slots of B*T frames
+ * and a non-blocking H2D stream:
+ *   impala_stage_init     allocate the ring (1..8 slots; re-init frees the old ring)
+ *   impala_stage          enqueue the H2D copies of one host batch (page-locked memory makes
+ *                         them asynchronous; discounts may be NULL on PPO handles) into `slot`,
+ *                         ordered after the last impala_slot_release of that slot
+ *   impala_stage_wait     block the host until the copies into `slot` have finished (the host
+ *                         batch may then be overwritten)
+ *   impala_slot_batch     make `stream` wait for the slot's copies; *out = its device views,
+ *                         to pass to impala_train_step / impala_compute_grads*
+ *   impala_slot_release   record on `stream` that the steps reading the slot are enqueued
+ * With two slots, staging batch k+1 overlaps the step on batch k. */
+int impala_stage_init(impala_learner* h, int nslots);
+int impala_stage(impala_learner* h, const impala_batch* host, int slot);
+int impala_stage_wait(impala_learner* h, int slot);
+int impala_slot_batch(impala_learner* h, int slot, void* stream, impala_batch* out);
+int impala_slot_release(impala_learner* h, int slot, void* stream);
+
 /* Live launch timer (bench / roofline): record a hipEvent pair around each of the next
  * `max_launches` launches of kernel `kernel_id` (see impala_kernel_name), on the stream it is
  * launched on; impala_timer_read() synchronises on them and returns the summed duration. */

@@ -72,3 +72,9 @@ def test_kernel_entry_points_validate_before_launch():
     assert lib.impala_train_step(None, None, None) == 1001
     assert lib.impala_forward(None, None, 1, None, None, None) == 1001
     assert lib.impala_gather_rows(None, None, None, 0, None, 0, None) == 1001
+    # host staging ring: a null handle is refused before any HIP call
+    assert lib.impala_stage_init(None, 2) == 1001
+    assert lib.impala_stage(None, None, 0) == 1001
+    assert lib.impala_stage_wait(None, 0) == 1001
+    assert lib.impala_slot_batch(None, 0, None, None) == 1001
+    assert lib.impala_slot_release(None, 0, None) == 1001

@@ -101,6 +101,42 @@ def test_device_replay_gather_and_learn():
     assert np.isfinite(float(met["train/loss"]))
 
 
+def test_host_staging_ring_matches_device_batches():
+    """impala_stage ring (2 slots, copies of step k+1 enqueued before step k) gives bitwise the
+    same weights and metrics as the same batches handed over already in HBM."""
+    dev = _dev()
+    from impala_amd.engine import Engine
+    from impala_amd.model import AtariPPOModel
+    B, T, A, steps = 4, 20, 15, 5
+    host = [[torch.from_numpy(x) for x in ref_cpu.synthetic_batch(B, T, A, seed=40 + s)]
+            for s in range(steps)]
+
+    def make():
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+        e = Engine(m, batch_size=B, rollout_length=T, dtype="fp32")
+        m._train_engine = e
+        return m, e
+
+    m1, e1 = make()
+    for hb in host:
+        e1.train_step(*[t.to(dev) for t in hb])
+    m2, e2 = make()
+    e2.stage_init(2)
+    pinned = [[t.pin_memory() for t in hb] for hb in host]
+    e2.stage(0, *pinned[0])
+    for k in range(steps):
+        s = k % 2
+        if k + 1 < steps:
+            e2.stage(1 - s, *pinned[k + 1])
+        e2.train_step(e2.slot_batch(s))
+        e2.slot_release(s)
+    torch.cuda.synchronize()
+    assert torch.equal(m1.flat, m2.flat)
+    assert torch.equal(e1.metrics, e2.metrics)
+    with pytest.raises(RuntimeError):
+        e2.slot_batch(2)
+
+
 def test_model_act_and_checkpoint_roundtrip(tmp_path):
     dev = _dev()
     from impala_amd.model import AtariPPOModel
