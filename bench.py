@@ -187,7 +187,10 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
                  "reduce_grads": "reduce_grads", "adam": "adam"}
 
 
-def profiled_traffic(kernel, dtype):
+SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}
+
+
+def profiled_traffic(kernel, dtype, names=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>/summary.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
     root = os.path.join(HERE, "profiles")
@@ -205,7 +208,7 @@ def profiled_traffic(kernel, dtype):
         if js.get("dtype", "bf16") != dtype:
             continue
         for k in js.get("kernels", []):
-            if k.get("kernel") == PROFILE_NAMES.get(kernel) and k.get("hbm_bytes"):
+            if k.get("kernel") == (names or PROFILE_NAMES).get(kernel) and k.get("hbm_bytes"):
                 best = (float(k["hbm_bytes"]), tag)
     return best if best else (None, None)
 
@@ -380,6 +383,9 @@ def run_sac(args):
         bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
+    traffic, tsrc = profiled_traffic(rk, args.dtype, SAC_PROFILE_NAMES)
+    traffic_src = (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+WRITE_SIZE, "
+                   "bytes per launch)") if tsrc else None
     # per-step algorithmic flops: the phases that ran (probe), else the fused step's phases
     ran = probe or ("critic_fwd_chain", "critic_loss_chain", "critic_wgrad", "actor_chain",
                     "actor_wgrad", "alpha_chain")
@@ -395,7 +401,8 @@ def run_sac(args):
                                f"0.005), obs {D}, action {K}, N={N} transitions/GPU",
                    "global_batch": N * world, "parallelism": f"replicas{world}"},
         "roofline": {"bound": bound, "kernel": rk, "achieved": round(achieved, 3), "peak": peak,
-                     "unit": unit, "frac": round(achieved / peak, 5), "traffic": None,
+                     "unit": unit, "frac": round(achieved / peak, 5), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "algorithmic": {"flops": flops, "bytes": nbytes},
                      "avg_launch_us": round(k_avg_ms * 1e3, 2), "launches": k_n,
                      "timing": "separate event-timed pass of --steps direct-launch steps"},

@@ -156,7 +156,15 @@ struct impala_learner {
   static constexpr int kMaxStageSlots = 8;
   StageSlot ring[kMaxStageSlots];
   int n_slots = 0;
-  hipStream_t h2d = nullptr;
+  // copy streams: IMPALA_H2D_STREAMS > 1 splits the obs block over several streams (stream 0
+  // joins the others and signals `ready`).  Measured on MI355X one stream is fastest: 29.7 GB/s
+  // pinned H2D, against 12.8 GB/s with 4 and 8.1 GB/s with 8 (profiles/r01k)
+  static constexpr int kMaxH2D = 8;
+  hipStream_t h2d_s[kMaxH2D] = {};
+  hipEvent_t h2d_join[kMaxH2D] = {};
+  int n_h2d = 0;
+  int h2d_pull_wg = 0;        // > 0: copy with h2d_pull_kernel on that many workgroups
+  hipStream_t h2d = nullptr;  // = h2d_s[0]
 };
 
 namespace {
@@ -438,7 +446,7 @@ void drop_graphs(impala_learner* h) {
 }
 
 void free_ring(impala_learner* h) {
-  if (h->h2d) (void)hipStreamSynchronize(h->h2d);
+  for (int i = 0; i < h->n_h2d; ++i) (void)hipStreamSynchronize(h->h2d_s[i]);
   for (auto& s : h->ring) {
     if (s.done) (void)hipEventSynchronize(s.done);
     if (s.ready) (void)hipEventDestroy(s.ready);
@@ -695,7 +703,10 @@ int impala_destroy(impala_learner* h) {
   (void)hipDeviceSynchronize();  // replays may still be in flight on the caller's streams
   drop_graphs(h);
   free_ring(h);
-  if (h->h2d) (void)hipStreamDestroy(h->h2d);
+  for (int i = 0; i < h->n_h2d; ++i) {
+    (void)hipStreamDestroy(h->h2d_s[i]);
+    if (h->h2d_join[i]) (void)hipEventDestroy(h->h2d_join[i]);
+  }
   if (h->timer_ev) {
     for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
     delete[] h->timer_ev;
@@ -899,7 +910,21 @@ int impala_stage_init(impala_learner* h, int nslots) {
     return fail(IMPALA_E_INVALID, "nslots must be in [1, 8]");
   CK(hipSetDevice(h->device));
   free_ring(h);
-  if (!h->h2d) CK(hipStreamCreateWithFlags(&h->h2d, hipStreamNonBlocking));
+  if (!h->n_h2d) {
+    int n = 1;
+    if (const char* e = std::getenv("IMPALA_H2D_STREAMS")) n = std::atoi(e);
+    n = std::max(1, std::min(n, (int)impala_learner::kMaxH2D));
+    for (int i = 0; i < n; ++i) {
+      CK(hipStreamCreateWithFlags(&h->h2d_s[i], hipStreamNonBlocking));
+      h->n_h2d = i + 1;
+      CK(hipEventCreateWithFlags(&h->h2d_join[i], hipEventDisableTiming));
+    }
+    h->h2d = h->h2d_s[0];
+    // pull kernel by default: 16 workgroups reach 41.5 GB/s pinned H2D on MI355X against
+    // 28.9 GB/s for hipMemcpyAsync (SDMA) and 36.6 GB/s for blit copies (profiles/r01k)
+    h->h2d_pull_wg = 16;
+    if (const char* e = std::getenv("IMPALA_H2D_KERNEL")) h->h2d_pull_wg = std::max(0, std::atoi(e));
+  }
   const size_t N = (size_t)h->N;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -940,14 +965,58 @@ int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
   CK(hipSetDevice(h->device));
   auto& s = h->ring[slot];
   const size_t N = (size_t)h->N;
-  CK(hipStreamWaitEvent(h->h2d, s.done, 0));  // the steps that read the slot have run
-  CK(hipMemcpyAsync((void*)s.dev.obs, b->obs, N * 3 * 64 * 64, hipMemcpyDefault, h->h2d));
-  CK(hipMemcpyAsync((void*)s.dev.actions, b->actions, N * 8, hipMemcpyDefault, h->h2d));
-  CK(hipMemcpyAsync((void*)s.dev.rewards, b->rewards, N * 4, hipMemcpyDefault, h->h2d));
-  if (b->discounts)
-    CK(hipMemcpyAsync((void*)s.dev.discounts, b->discounts, N * 4, hipMemcpyDefault, h->h2d));
-  CK(hipMemcpyAsync((void*)s.dev.behaviour_logits, b->behaviour_logits, N * (size_t)h->A * 4,
-                    hipMemcpyDefault, h->h2d));
+  const int ns = h->n_h2d;
+  for (int i = 0; i < ns; ++i)  // the steps that read the slot have run
+    CK(hipStreamWaitEvent(h->h2d_s[i], s.done, 0));
+  // pull-copy kernel (IMPALA_H2D_KERNEL=<workgroups>): only for page-locked, device-mapped
+  // host fields (hipHostGetDevicePointer); anything else takes the hipMemcpyAsync path
+  bool pull = h->h2d_pull_wg > 0;
+  const void* hsrc[5] = {b->obs, b->actions, b->rewards, b->discounts, b->behaviour_logits};
+  const void* msrc[5] = {};
+  for (int f = 0; f < 5 && pull; ++f) {
+    if (!hsrc[f]) continue;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, const_cast<void*>(hsrc[f]), 0) != hipSuccess || !dp ||
+        (((uintptr_t)dp) & 15) != 0) {
+      (void)hipGetLastError();
+      pull = false;
+    }
+    msrc[f] = dp;
+  }
+  if (pull) {
+    PullArgs pa{};
+    const void* const* src = msrc;
+    void* dst[5] = {(void*)s.dev.obs, (void*)s.dev.actions, (void*)s.dev.rewards,
+                    (void*)s.dev.discounts, (void*)s.dev.behaviour_logits};
+    const size_t bytes[5] = {N * 3 * 64 * 64, N * 8, N * 4, N * 4, N * (size_t)h->A * 4};
+    for (int f = 0; f < 5; ++f) {
+      if (!src[f]) continue;
+      pa.src[pa.nf] = (const char*)src[f];
+      pa.dst[pa.nf] = (char*)dst[f];
+      pa.bytes[pa.nf] = (long long)bytes[f];
+      ++pa.nf;
+    }
+    h2d_pull_kernel<<<h->h2d_pull_wg, 256, 0, h->h2d>>>(pa);
+    CK_LAUNCH("h2d_pull");
+  } else {
+    // obs in ns contiguous chunks (one per copy stream), the small fields on stream 0
+    const size_t ob = N * 3 * 64 * 64, chunk = (ob / ns + 4095) & ~(size_t)4095;
+    for (int i = 0; i < ns; ++i) {
+      const size_t o0 = std::min(ob, (size_t)i * chunk), o1 = std::min(ob, o0 + chunk);
+      if (o1 > o0)
+        CK(hipMemcpyAsync((char*)s.dev.obs + o0, b->obs + o0, o1 - o0, hipMemcpyDefault, h->h2d_s[i]));
+    }
+    CK(hipMemcpyAsync((void*)s.dev.actions, b->actions, N * 8, hipMemcpyDefault, h->h2d));
+    CK(hipMemcpyAsync((void*)s.dev.rewards, b->rewards, N * 4, hipMemcpyDefault, h->h2d));
+    if (b->discounts)
+      CK(hipMemcpyAsync((void*)s.dev.discounts, b->discounts, N * 4, hipMemcpyDefault, h->h2d));
+    CK(hipMemcpyAsync((void*)s.dev.behaviour_logits, b->behaviour_logits, N * (size_t)h->A * 4,
+                      hipMemcpyDefault, h->h2d));
+  }
+  for (int i = 1; i < ns; ++i) {
+    CK(hipEventRecord(h->h2d_join[i], h->h2d_s[i]));
+    CK(hipStreamWaitEvent(h->h2d, h->h2d_join[i], 0));
+  }
   CK(hipEventRecord(s.ready, h->h2d));
   return 0;
 }

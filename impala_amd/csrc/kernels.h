@@ -729,6 +729,37 @@ struct GatherArgs {
   int n;
 };
 
+// Host -> HBM pull copy for the staging ring (impala_stage, IMPALA_H2D_KERNEL=1): a few
+// workgroups read page-locked host memory over PCIe with 4 x 16-byte loads in flight per lane
+// (PCIe latency x bandwidth needs ~128 KB outstanding), on the copy stream beside the step.
+struct PullArgs {
+  const char* src[5];
+  char* dst[5];
+  long long bytes[5];
+  int nf;
+};
+__global__ __launch_bounds__(256) void h2d_pull_kernel(const PullArgs a) {
+  const long long stride = (long long)gridDim.x * 256;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (int f = 0; f < a.nf; ++f) {
+    const long long nv = a.bytes[f] >> 4;
+    const f32x4* s = reinterpret_cast<const f32x4*>(a.src[f]);
+    f32x4* d = reinterpret_cast<f32x4*>(a.dst[f]);
+    long long i = t;
+    for (; i + 3 * stride < nv; i += 4 * stride) {
+      const f32x4 v0 = __builtin_nontemporal_load(s + i), v1 = __builtin_nontemporal_load(s + i + stride);
+      const f32x4 v2 = __builtin_nontemporal_load(s + i + 2 * stride);
+      const f32x4 v3 = __builtin_nontemporal_load(s + i + 3 * stride);
+      d[i] = v0;
+      d[i + stride] = v1;
+      d[i + 2 * stride] = v2;
+      d[i + 3 * stride] = v3;
+    }
+    for (; i < nv; i += stride) d[i] = s[i];
+    for (long long b = (nv << 4) + t; b < a.bytes[f]; b += stride) a.dst[f][b] = a.src[f][b];
+  }
+}
+
 __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   const int i = blockIdx.x, f = blockIdx.y;
   if (i >= a.n || f >= a.nfields) return;

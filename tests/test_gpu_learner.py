@@ -101,10 +101,13 @@ def test_device_replay_gather_and_learn():
     assert np.isfinite(float(met["train/loss"]))
 
 
-def test_host_staging_ring_matches_device_batches():
-    """impala_stage ring (2 slots, copies of step k+1 enqueued before step k) gives bitwise the
-    same weights and metrics as the same batches handed over already in HBM."""
+@pytest.mark.parametrize("pull_wg", [0, 16])
+def test_host_staging_ring_matches_device_batches(pull_wg, monkeypatch):
+    """impala_stage ring (2 slots, copies of step k+1 enqueued before step k; hipMemcpyAsync or
+    the PCIe pull kernel) gives bitwise the same weights and metrics as the same batches handed
+    over already in HBM."""
     dev = _dev()
+    monkeypatch.setenv("IMPALA_H2D_KERNEL", str(pull_wg))
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
     B, T, A, steps = 4, 20, 15, 5

@@ -18,6 +18,11 @@ STEP_KERNELS = None
 
 def short(name):
     n = name.split("(")[0]
+    for k, tag in (("actor_chain_kernel", "actor_chain"), ("critic_chain_kernel", "critic_loss_chain"),
+                   ("chain_fwd_kernel", "chain_fwd"), ("adam_net_kernel", "sac_adam"),
+                   ("gemm_jobs", "sac_wgrad")):
+        if k in n:
+            return tag
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
     if "conv12_bwd_s2d" in n:
