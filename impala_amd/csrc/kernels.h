@@ -566,14 +566,19 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   if (in) {
     // 8 split loads in flight per round (the split count is >= 4 x SG by construction)
     const float* p = sg.slab + (size_t)v4 * 4;
+    // the loads are unconditional (split index clamped to S - 1) and out-of-range splits are
+    // dropped by a value select after them: a "load or zero" select per element compiles to a
+    // branch and a vmcnt(0) wait per load (one L2/HBM round trip per split)
     for (int q = grp; q < sg.S; q += 8 * SG) {
       f32x4 v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        v[j] = q + j * SG < sg.S ? *reinterpret_cast<const f32x4*>(p + (size_t)(q + j * SG) * sg.count)
-                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[j] = *reinterpret_cast<const f32x4*>(p + (size_t)min(q + j * SG, sg.S - 1) * sg.count);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += v[j];
+      for (int j = 0; j < 8; ++j) {
+        const float keep = q + j * SG < sg.S ? 1.f : 0.f;
+        acc += v[j] * keep;
+      }
     }
   }
   part[threadIdx.x] = acc;
