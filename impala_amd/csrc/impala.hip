@@ -655,9 +655,13 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   {
     RedArgs& ra = h->red;
     int ns = 0;
+    // split loads per thread the split-group count aims for (IMPALA_RED_LPT): 16 -> 10.3 us,
+    // 8 -> 10.7, 4 -> 11.2, 2 -> 11.6 (rocprof, B=64 T=20 bf16, profiles/r01k)
+    int lpt = 16;
+    if (const char* e = std::getenv("IMPALA_RED_LPT")) lpt = std::max(1, std::atoi(e));
     auto add = [&](const float* slab, int S, int count, int kind, long long canon) {
       int sg = 1;
-      while (sg < 16 && sg * 4 < S) sg <<= 1;  // ~4+ loads per thread, <= 16 groups
+      while (sg < 16 && sg * lpt < S) sg <<= 1;  // ~lpt+ loads per thread, <= 16 groups
       ra.seg[ns] = RedSeg{slab, S, count, kind, canon, sg};
       ra.wg_start[ns + 1] = ra.wg_start[ns] + cdiv(count / 4, 256 / sg);
       ++ns;
