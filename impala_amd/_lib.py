@@ -32,6 +32,7 @@ EXPORTS = (
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
     "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
     "impala_apply_update", "impala_compute_grads_part", "impala_grad_bucket_offset",
+    "impala_grad_bucket_offset_fc",
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
     "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
@@ -122,6 +123,8 @@ def _declare(lib):
     lib.impala_compute_grads_part.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int, _P]
     lib.impala_grad_bucket_offset.argtypes = [_P]
     lib.impala_grad_bucket_offset.restype = C.c_size_t
+    lib.impala_grad_bucket_offset_fc.argtypes = [_P]
+    lib.impala_grad_bucket_offset_fc.restype = C.c_size_t
     lib.impala_vtrace.argtypes = [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_float, C.c_float,
                                   C.c_float, _P, _P, _P, _P]
     lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
@@ -139,7 +142,8 @@ def _declare(lib):
     lib.impala_timer_start.argtypes = [_P, C.c_int, C.c_int]
     lib.impala_timer_read.argtypes = [_P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     for name in EXPORTS:
-        if name not in ("impala_last_error", "impala_param_count", "impala_kernel_name"):
+        if name not in ("impala_last_error", "impala_param_count", "impala_kernel_name",
+                        "impala_grad_bucket_offset", "impala_grad_bucket_offset_fc"):
             getattr(lib, name).restype = C.c_int
     lib.sac_config_default.argtypes = [C.POINTER(SacConfig)]
     lib.sac_actor_param_count.argtypes = [C.c_int, C.c_int]

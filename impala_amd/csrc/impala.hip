@@ -263,7 +263,11 @@ int reduce_segments(impala_learner* h, int s_lo, int s_hi, hipStream_t st, int f
 // part: -1 = the whole backward; 0 = through the conv3 weight gradient, ending with the
 // reduction of gradient bucket 1 (conv3 .. heads, canonical [cn.w3, total)); 1 = the rest
 // (conv2 weight gradient, conv2 dgrad + conv1 wgrad, bucket 0 = conv1 + conv2, loss metrics).
-// Data-parallel replicas all-reduce bucket 1 while part 1 runs.
+// Data-parallel replicas all-reduce bucket 1 while part 1 runs.  Three-bucket split: 2 = heads
+// step, FC weight gradient and FC dgrad, ending with the reduction of [cn.wfc, total) (FC +
+// heads); 3 = LayerNorm backward + conv3 dgrad and the conv3 weight gradient, ending with
+// [cn.w3, cn.wfc) (conv3 + LayerNorm); 4 = part 1.  Any split gives bit-identical gradients
+// (each reduction workgroup owns a fixed sum-of-squares slot).
 template <typename T>
 int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {
   using namespace net;
@@ -282,7 +286,8 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     CK(hipStreamWaitEvent(ss, h->ev_fork[i], 0));
     return 0;
   };
-  if (part == 1) goto part1;
+  if (part == 1 || part == 4) goto part1;
+  if (part == 3) goto stage_b;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
   {
     HeadArgs ha{};
@@ -324,6 +329,14 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     timer_end(h, K_FC_DGRAD, st);
     CK_LAUNCH("fc_dgrad");
   }
+  if (part == 2) {  // bucket FC + heads complete
+    if (h->use_side) {
+      CK(hipEventRecord(h->ev_join, ss));
+      CK(hipStreamWaitEvent(st, h->ev_join, 0));
+    }
+    return reduce_segments(h, RS_FC, RS_END, st, 0);
+  }
+stage_b:
   if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
     timer_begin(h, K_LNC3_BWD, st);
     lnc3_bwd<T><<<h->n_ln_wg, 256 * lnc3_groups<T>(), 0, st>>>(
@@ -358,12 +371,12 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     timer_end(h, K_CONV3_DGRAD, st);
     CK_LAUNCH("conv3_dgrad");
   }
-  if (part == 0) {  // bucket 1 complete
+  if (part == 0 || part == 3) {  // bucket 1 (or conv3 + LayerNorm) complete
     if (h->use_side) {
       CK(hipEventRecord(h->ev_join, ss));
       CK(hipStreamWaitEvent(st, h->ev_join, 0));
     }
-    return reduce_segments(h, RS_CONV3, RS_END, st, 0);
+    return reduce_segments(h, RS_CONV3, part == 0 ? RS_END : RS_FC, st, 0);
   }
 part1:
   if (int r = fork(3)) return r;  // dact2 ready
@@ -389,7 +402,7 @@ part1:
   CK_LAUNCH("conv2_dgrad_conv1_wgrad");
   // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were
   // reduced on the side stream right after their weight gradients ----
-  if (part == 1) {
+  if (part == 1 || part == 4) {
     if (h->use_side) {
       CK(hipEventRecord(h->ev_join, ss));
       CK(hipStreamWaitEvent(st, h->ev_join, 0));
@@ -778,7 +791,7 @@ int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, 
 extern "C++" {
 namespace {
 int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {
-  if (part != 1) {
+  if (part == -1 || part == 0 || part == 2) {
     int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st, false)
                     : launch_forward<float>(h, b->obs, h->N, st, false);
     if (r) return r;
@@ -837,7 +850,7 @@ int run_graphed(impala_learner* h, int kind, const impala_batch* b, hipStream_t 
   CK(hipGraphLaunch(exec, st));
   return 0;
 }
-enum { G_GRADS = 0, G_UPDATE = 1, G_STEP = 2, G_GRADS0 = 3, G_GRADS1 = 4 };
+enum { G_GRADS = 0, G_UPDATE = 1, G_STEP = 2, G_GRADS0 = 3 };  // G_GRADS0 + part (0..4)
 }  // namespace
 }  // extern "C++"
 
@@ -850,15 +863,16 @@ int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream)
 }
 
 int impala_compute_grads_part(impala_learner* h, const impala_batch* b, int part, void* stream) {
-  if (part != 0 && part != 1) return fail(IMPALA_E_INVALID, "part must be 0 or 1");
+  if (part < 0 || part > 4) return fail(IMPALA_E_INVALID, "part must be 0..4");
   if (int r = check_bound(h)) return r;
   if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));
-  return run_graphed(h, part ? G_GRADS1 : G_GRADS0, b, (hipStream_t)stream,
+  return run_graphed(h, G_GRADS0 + part, b, (hipStream_t)stream,
                      [&](hipStream_t s) { return enqueue_grads(h, b, s, part); });
 }
 
 size_t impala_grad_bucket_offset(const impala_learner* h) { return h ? h->cn.w3 : 0; }
+size_t impala_grad_bucket_offset_fc(const impala_learner* h) { return h ? h->cn.wfc : 0; }
 
 int impala_apply_update(impala_learner* h, void* stream) {
   if (int r = check_bound(h)) return r;

@@ -2,9 +2,9 @@
 
 Trajectories are independent and every loss term is a mean over (B, T-1) or (B, T), so with
 equal shards the mean of the replicas' gradients IS the full-batch gradient.  Each replica:
-``impala_compute_grads_part`` 0 (local mean of conv3..heads) -> ``all_reduce(sum)`` of that
-bucket, overlapped with ``impala_compute_grads_part`` 1 (conv1, conv2) -> ``all_reduce`` of the
-small conv bucket -> ``impala_apply_update`` (x 1/world, global-norm clip on the reduced
+``impala_compute_grads_part`` 2 / 3 / 4, each followed by an async ``all_reduce(sum)`` of the
+gradient bucket it finalised (FC + heads, conv3 + LayerNorm, conv1 + conv2), so the larger
+buckets travel while the backward continues -> ``impala_apply_update`` (x 1/world, global-norm clip on the reduced
 gradient -- identical on every replica -- and Adam).  Weights therefore stay bit-identical
 across replicas (checked by ``params_checksum``).
 """
@@ -52,19 +52,25 @@ def allreduce_grads(flat_grad: torch.Tensor, group=None) -> None:
 
 
 def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None) -> None:
-    """Local gradients of `batch` summed over replicas, in two buckets: the all-reduce of
-    bucket 1 (conv3, LayerNorm, FC, heads: 1.22 MB) is enqueued as soon as part 0 of the
-    backward has reduced it, so it runs on the collective stream while part 1 (conv2 weight
-    gradient, conv2 dgrad + conv1 weight gradient) computes; bucket 0 (conv1 + conv2, 156 KB)
-    follows part 1.  The caller's stream waits for both before it continues (apply_update)."""
+    """Local gradients of `batch` summed over replicas, in three buckets, each all-reduced as
+    soon as the backward has finalised it so that it runs on the collective stream beside the
+    rest of the backward: FC + heads (1.07 MB, after part 2: heads step, FC weight gradient and
+    dgrad) overlaps parts 3 and 4; conv3 + LayerNorm (156 KB, after part 3) overlaps part 4
+    (conv2 weight gradient, conv2 dgrad + conv1 weight gradient); conv1 + conv2 (157 KB)
+    follows part 4.  The caller's stream waits for all three before it continues
+    (apply_update)."""
     import torch.distributed as dist
-    engine.compute_grads_part(0, *batch)
-    off = engine.bucket_offset
-    w1 = dist.all_reduce(flat_grad[off:], op=dist.ReduceOp.SUM, group=group, async_op=True)
-    engine.compute_grads_part(1, *batch)
-    w0 = dist.all_reduce(flat_grad[:off], op=dist.ReduceOp.SUM, group=group, async_op=True)
-    w1.wait()
-    w0.wait()
+    engine.compute_grads_part(2, *batch)
+    off_fc, off = engine.bucket_offset_fc, engine.bucket_offset
+    w_fc = dist.all_reduce(flat_grad[off_fc:], op=dist.ReduceOp.SUM, group=group, async_op=True)
+    engine.compute_grads_part(3, *batch)
+    w_c3 = dist.all_reduce(flat_grad[off:off_fc], op=dist.ReduceOp.SUM, group=group,
+                           async_op=True)
+    engine.compute_grads_part(4, *batch)
+    w_c12 = dist.all_reduce(flat_grad[:off], op=dist.ReduceOp.SUM, group=group, async_op=True)
+    w_fc.wait()
+    w_c3.wait()
+    w_c12.wait()
 
 
 def params_checksum(flat: torch.Tensor) -> float:

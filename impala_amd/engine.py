@@ -174,10 +174,12 @@ class Engine:
               "impala_compute_grads")
 
     def compute_grads_part(self, part, *batch, stream=None):
-        """Half of compute_grads: part 0 finishes grads[bucket_offset:] (conv3 .. heads),
-        part 1 (same batch) finishes grads[:bucket_offset] (conv1, conv2) and the metrics."""
+        """A piece of compute_grads.  Two buckets: part 0 finishes grads[bucket_offset:]
+        (conv3 .. heads), part 1 (same batch) grads[:bucket_offset] (conv1, conv2) and the
+        metrics.  Three buckets: part 2 finishes grads[bucket_offset_fc:] (FC, heads), part 3
+        grads[bucket_offset:bucket_offset_fc] (conv3, LayerNorm), part 4 = part 1."""
         b = self._batch(*batch)
-        if part == 0:
+        if part in (0, 2):
             self._sync_weights(stream)
         check(_lib.lib().impala_compute_grads_part(self._h, C.byref(b), int(part),
                                                    stream_ptr(stream)),
@@ -187,6 +189,11 @@ class Engine:
     def bucket_offset(self) -> int:
         """First flat-gradient index of bucket 1 (all-reduced while part 1 runs)."""
         return int(_lib.lib().impala_grad_bucket_offset(self._h))
+
+    @property
+    def bucket_offset_fc(self) -> int:
+        """First flat-gradient index of the FC + heads bucket (final after part 2)."""
+        return int(_lib.lib().impala_grad_bucket_offset_fc(self._h))
 
     def apply_update(self, stream=None):
         check(_lib.lib().impala_apply_update(self._h, stream_ptr(stream)), "impala_apply_update")

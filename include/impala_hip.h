@@ -151,6 +151,12 @@ int impala_apply_update(impala_learner* h, void* stream);
  * final.  part 0 then part 1 give bit-identical grads to impala_compute_grads. */
 int impala_compute_grads_part(impala_learner* h, const impala_batch* batch, int part, void* stream);
 size_t impala_grad_bucket_offset(const impala_learner* h);
+/* Three buckets, for a longer all-reduce window: part 2 (forward, heads step, FC weight
+ * gradient, FC dgrad) leaves grads[impala_grad_bucket_offset_fc(h) ..] -- FC and heads, 1.07 MB
+ * of the 1.38 MB -- final; part 3 (same batch: LayerNorm backward, conv3 dgrad and weight
+ * gradient) finalises [impala_grad_bucket_offset(h), impala_grad_bucket_offset_fc(h)); part 4
+ * = part 1.  Parts 2, 3, 4 give bit-identical grads to impala_compute_grads. */
+size_t impala_grad_bucket_offset_fc(const impala_learner* h);
 
 /* Replay gather (agents/impala/builder.py:30-36 UniformSampler.sample + learning.py:121-123
  * collate/H2D, done in HBM): for each field f < nfields (<= 8), copy row idx[i] of src[f] to

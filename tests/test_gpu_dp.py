@@ -58,6 +58,20 @@ def test_grad_parts_match_whole_backward(dtype):
     np.testing.assert_array_equal(m2.flat_grad.cpu().numpy(), g_whole)
     np.testing.assert_array_equal(e2.metrics.cpu().numpy(), met_whole)
     assert off == 6144 + 32 + 32768 + 64  # conv1 + conv2 (state_dict order)
+    # three buckets: FC + heads final after part 2, conv3 + LayerNorm after part 3
+    m3, e3 = _setup(dev, 8, dtype=dtype)
+    e3.compute_grads_part(2, *batch)
+    off_fc = e3.bucket_offset_fc
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m3.flat_grad[off_fc:].cpu().numpy(), g_whole[off_fc:])
+    e3.compute_grads_part(3, *batch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m3.flat_grad[off:].cpu().numpy(), g_whole[off:])
+    e3.compute_grads_part(4, *batch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m3.flat_grad.cpu().numpy(), g_whole)
+    np.testing.assert_array_equal(e3.metrics.cpu().numpy(), met_whole)
+    assert off_fc == off + 36864 + 64 + 2 * 1024  # + conv3 + LayerNorm
 
 
 def _free_port():
