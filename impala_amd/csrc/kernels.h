@@ -674,9 +674,15 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   }
   const float step_size = a.sc[0], bc2s = a.sc[1];
   float sq = 0.f;  // partials are zero-padded to a multiple of 4 (see impala_create)
-  for (int q = threadIdx.x; q * 4 < a.n_part; q += 256) {
-    const f32x4 x = *reinterpret_cast<const f32x4*>(a.sumsq_part + 4 * q);
-    sq += (x[0] + x[1]) + (x[2] + x[3]);
+  // 4 float4 partial loads in flight per thread (unconditional, clamped; out-of-range ones
+  // weighted 0), same summation order as one at a time
+  const int nq = (a.n_part + 3) / 4;
+  for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * 4) {
+    f32x4 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = *reinterpret_cast<const f32x4*>(a.sumsq_part + 4 * min(q0 + 256 * j, nq - 1));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sq += ((x[j][0] + x[j][1]) + (x[j][2] + x[j][3])) * (q0 + 256 * j < nq ? 1.f : 0.f);
   }
   sq = wave_sum(sq);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;

@@ -656,10 +656,28 @@ template <typename T>
 __global__ __launch_bounds__(256) void adam_net_kernel(const AdamNetArgs a) {
   __shared__ float red[4];
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  // Every global load is issued first, unconditionally (index clamped, pointer -- not value --
+  // selects), so the whole prologue is one memory round trip: the parameter's state, then the
+  // norm partials 8 at a time (a "load or 0" select per element would become a branch and a
+  // vmcnt(0) wait per load).  Arithmetic and summation order are unchanged.
+  const bool in = i < a.n;
+  const long long ic = in ? i : a.n - 1;
+  float p = a.p[ic];
+  const float* gp = a.update ? a.g : a.p;
+  const float* mp = a.update ? a.m : a.p;
+  const float* vp = a.update ? a.v : a.p;
+  float g = gp[ic], m = mp[ic], v = vp[ic];
+  float tv = (a.tgt ? a.tgt : a.p)[ic];
   float coef = 1.f;
   if (a.update && a.max_norm > 0.f) {
     float sq = 0.f;
-    for (int q = threadIdx.x; q < a.nsq; q += 256) sq += a.sq[q];
+    for (int q0 = threadIdx.x; q0 < a.nsq; q0 += 256 * 8) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = a.sq[min(q0 + 256 * j, a.nsq - 1)];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq += x[j] * (q0 + 256 * j < a.nsq ? 1.f : 0.f);
+    }
     sq = wave_sum(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
     __syncthreads();
@@ -667,16 +685,13 @@ __global__ __launch_bounds__(256) void adam_net_kernel(const AdamNetArgs a) {
     coef = fminf(__fdiv_rn(a.max_norm, norm + 1e-6f), 1.f);
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.norm_out) *a.norm_out = norm;
   }
-  if (i >= a.n) return;
-  float p = a.p[i];
+  if (!in) return;
   if (a.update) {
     const double t = (double)(*a.step + 1);
     const double bc1 = 1.0 - pow(a.b1, t), bc2 = 1.0 - pow(a.b2, t);
     const float step_size = (float)(a.lr / bc1), bc2s = (float)sqrt(bc2);
-    float g = a.g[i];
     if (a.max_norm > 0.f) g = mul(g, coef);
     const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
-    float m = a.m[i], v = a.v[i];
     m = add(m, mul(w1, sub(g, m)));
     v = add(mul(v, b2f), mul(mul(w2, g), g));
     const float denom = add(__fdiv_rn(sqrtf(v), bc2s), a.eps);
@@ -689,7 +704,6 @@ __global__ __launch_bounds__(256) void adam_net_kernel(const AdamNetArgs a) {
   const int q = (a.nnet > 1 && i >= a.net[1].base) ? 1 : 0;
   emit_layout<T>(a.net[q], a.k[q], i, p);
   if (a.tgt) {
-    float tv = a.tgt[i];
     if (a.polyak) {
       const float tau = a.tau, omt = (float)(1.0 - (double)a.tau);
       tv = add(mul(tau, p), mul(omt, tv));
