@@ -788,6 +788,25 @@ int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, 
   return 0;
 }
 
+int impala_act(impala_learner* h, const uint8_t* obs, int n, const uint8_t* deterministic,
+               int deterministic_all, uint64_t seed, uint64_t counter, int64_t* actions,
+               float* logits, float* values, void* stream) {
+  if (int r = check_bound(h, false)) return r;
+  if (!obs || !actions || !logits || !values) return fail(IMPALA_E_INVALID, "null pointer");
+  if (n < 1 || n > h->N) return fail(IMPALA_E_INVALID, "n must be in [1, B*T]");
+  if (((uintptr_t)obs & 15) != 0) return fail(IMPALA_E_INVALID, "obs must be 16-byte aligned");
+  CK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  int r = h->bf16 ? launch_forward<__bf16>(h, obs, n, st, true)
+                  : launch_forward<float>(h, obs, n, st, true);
+  if (r) return r;
+  act_heads_kernel<<<cdiv(n, 256), 256, 0, st>>>(h->heads, n, h->A, deterministic,
+                                                 deterministic_all, seed, counter, actions,
+                                                 logits, values);
+  CK_LAUNCH("act_heads");
+  return 0;
+}
+
 extern "C++" {
 namespace {
 int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {

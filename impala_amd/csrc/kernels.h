@@ -727,6 +727,54 @@ __global__ void split_heads_kernel(const float* __restrict__ heads, int n, int A
   else if (j == VCOL) values[f] = heads[i];
 }
 
+// Actor inference head (models/distributed_models.py:21-32 AtariPPOModel.act): one thread per
+// frame splits the heads row into logits / value and picks the action -- argmax (first maximal
+// index, as torch.argmax) where the frame's deterministic flag is set, else a draw from
+// softmax(logits) by inverse CDF on a counter-based uniform (seed, counter, frame), the
+// distribution torch's softmax(-1).multinomial(1) samples from.
+DEV uint64_t act_mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void act_heads_kernel(const float* __restrict__ heads, int n, int A,
+                                                        const uint8_t* __restrict__ det, int det_all,
+                                                        uint64_t seed, uint64_t counter,
+                                                        int64_t* __restrict__ actions,
+                                                        float* __restrict__ logits,
+                                                        float* __restrict__ values) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= n) return;
+  float l[HEADS];
+#pragma unroll
+  for (int j = 0; j < HEADS; j += 4) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(heads + (size_t)f * HEADS + j);
+    l[j] = x[0]; l[j + 1] = x[1]; l[j + 2] = x[2]; l[j + 3] = x[3];
+  }
+  values[f] = l[VCOL];
+  float mx = l[0];
+  int am = 0;
+  for (int j = 0; j < A; ++j) {
+    logits[(size_t)f * A + j] = l[j];
+    if (l[j] > mx) { mx = l[j]; am = j; }
+  }
+  int a = am;
+  if (!(det ? det[f] != 0 : det_all != 0)) {
+    float sum = 0.f;
+    for (int j = 0; j < A; ++j) sum += expf(l[j] - mx);
+    const uint64_t r = act_mix64(act_mix64(seed ^ act_mix64(counter)) + (uint64_t)f);
+    const float u = (float)(uint32_t)(r >> 40) * (1.f / 16777216.f) * sum;  // [0, sum)
+    float c = 0.f;
+    a = A - 1;
+    for (int j = 0; j < A; ++j) {
+      c += expf(l[j] - mx);
+      if (u < c) { a = j; break; }
+    }
+  }
+  actions[f] = a;
+}
+
 // =========================================================================================
 // Replay gather: dst_f[i] = src_f[idx[i]] for up to 8 fields of fixed row size (bytes, multiple
 // of 4).  One workgroup per (row, field); 16-byte vector copies for the aligned bulk.

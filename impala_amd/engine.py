@@ -129,6 +129,45 @@ class Engine:
                                    sp), "impala_forward")
         return logits, values
 
+    def act(self, obs: torch.Tensor, deterministic=False, seed: int = 0, counter: int = 0,
+            stream=None):
+        """models/distributed_models.py:21-32 on device (impala_act): obs u8 [N,3,64,64],
+        deterministic a bool or a per-frame bool tensor -> (actions i64 [N,1], logits [N,A],
+        v [N,1]); stochastic actions are draws from softmax(logits) keyed by (seed, counter,
+        frame) -- pass a fresh counter per call."""
+        if obs.dtype != torch.uint8 or obs.shape[-3:] != (3, 64, 64):
+            raise ValueError("obs must be uint8 [..., 3, 64, 64]")
+        obs = obs.reshape(-1, 3, 64, 64)
+        if obs.device != self.device:
+            obs = obs.to(self.device, non_blocking=True)
+        obs = obs.contiguous()
+        self._sync_weights(stream)
+        n = obs.shape[0]
+        det_all, det = 0, None
+        if isinstance(deterministic, torch.Tensor):
+            d = deterministic.reshape(-1).to(self.device)
+            if d.numel() == 1:
+                det_all = int(bool(d.item()))
+            elif d.numel() == n:
+                det = d.to(torch.uint8).contiguous()
+            else:
+                raise ValueError(f"deterministic flags: {d.numel()} for {n} frames")
+        else:
+            det_all = int(bool(deterministic))
+        actions = torch.empty(n, 1, dtype=torch.int64, device=self.device)
+        logits = torch.empty(n, self.num_actions, dtype=torch.float32, device=self.device)
+        values = torch.empty(n, 1, dtype=torch.float32, device=self.device)
+        cap = self.frames
+        L = _lib.lib()
+        sp = stream_ptr(stream)
+        for s in range(0, n, cap):
+            e = min(n, s + cap)
+            # frame index within the call keys the draw: chunks offset the counter
+            check(L.impala_act(self._h, ptr(obs[s:e]), e - s, ptr(det[s:e]) if det is not None else None,
+                               det_all, int(seed), int(counter) * 1_000_003 + s, ptr(actions[s:e]),
+                               ptr(logits[s:e]), ptr(values[s:e]), sp), "impala_act")
+        return actions, logits, values
+
     def _batch(self, *batch, device=None) -> ImpalaBatch:
         """IMPALA: (obs u8 [B,T,3,64,64], actions i64 [B,T], rewards [B,T], discounts [B,T],
         behaviour logits [B,T,A]).  PPO: (obs u8 [N,3,64,64], actions i64 [N], value targets

@@ -9,6 +9,8 @@ pointer.  The compute path is the HIP library only: ``forward`` on a non-GPU ten
 """
 from __future__ import annotations
 
+import os
+
 import copy
 import math
 from typing import Dict, List, Optional, Tuple
@@ -74,6 +76,8 @@ class AtariPPOModel(nn.Module):
         self._version = 0          # bumped whenever self.flat changes
         self._train_engine = None  # Engine whose kernel-layout weights track every update
         self._infer_engine = None  # lazily created inference-only Engine
+        # act() sampling stream; drawn outside torch's generator so seeded inits are unchanged
+        self._act_seed = int.from_bytes(os.urandom(8), "little") >> 2
         off = 0
         for name, shape in self._specs:
             cnt = int(np.prod(shape))
@@ -156,14 +160,15 @@ class AtariPPOModel(nn.Module):
     def act(self, obs: torch.Tensor, deterministic_policy: torch.Tensor):
         """models/distributed_models.py:21-32: sample a ~ softmax(logits) (or argmax when
         deterministic); returns (action [N,1], logits [N,A], v [N,1]) on the CPU."""
-        device = self.flat.device
-        x = obs.to(device)
+        if self.flat.device.type != "cuda":
+            raise RuntimeError("AtariPPOModel.act runs on the HIP path only (cuda device)")
+        x = obs.to(self.flat.device)
         if x.dim() == 3:
             x = x.unsqueeze(0)
-        logits, v = self.forward(x)
-        action = logits.softmax(dim=-1).multinomial(1, replacement=True)
-        action = torch.where(deterministic_policy.to(device), logits.argmax(dim=-1, keepdim=True),
-                             action)
+        # forward + argmax / softmax draw in one HIP call (impala_act); each call draws fresh
+        self._act_calls = getattr(self, "_act_calls", 0) + 1
+        action, logits, v = self._engine().act(x, deterministic_policy, seed=self._act_seed,
+                                               counter=self._act_calls)
         return action.cpu(), logits.cpu(), v.cpu()
 
     def push(self) -> None:

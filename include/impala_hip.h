@@ -12,7 +12,8 @@
  *   impala_apply_update    learning.py:172-176 (clip_grad_norm_ + optimizer.step), after the
  *                          caller's gradient all-reduce in the data-parallel learner
  *   impala_forward         models/distributed_models.py:17-19 AtariPPOModel.forward
- *                          (also the actor's batched act(), :21-32)
+ *   impala_act             models/distributed_models.py:21-32 AtariPPOModel.act (forward +
+ *                          argmax / softmax-multinomial action)
  *   impala_vtrace          rlego.vtrace_td_error_and_advantage as called through
  *                          learning.py:15-26,150-153 (returns pg_advantage, td_error, q)
  *   impala_loss_head       learning.py:144-170 given network outputs (loss, metrics, d/dlogits,
@@ -131,7 +132,16 @@ int impala_set_step(impala_learner* h, int64_t step, void* stream);
 int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, float* values,
                    void* stream);
 
-/* Full learner update for one batch (world_size must be 1). */
+/* Actor inference (models/distributed_models.py:21-32 AtariPPOModel.act) for n frames: the
+ * forward, then per frame logits [n][A], value [n] and the action [n] -- argmax of the logits
+ * where deterministic[f] != 0 (deterministic may be NULL: deterministic_all applies to every
+ * frame), else a sample of softmax(logits) drawn from a counter-based uniform keyed by
+ * (seed, counter, f); pass a fresh counter per call. */
+int impala_act(impala_learner* h, const uint8_t* obs, int n, const uint8_t* deterministic,
+               int deterministic_all, uint64_t seed, uint64_t counter, int64_t* actions,
+               float* logits, float* values, void* stream);
+
+/* Full learner update for one batch (world_size must be 1). *//* Full learner update for one batch (world_size must be 1). */
 int impala_train_step(impala_learner* h, const impala_batch* batch, void* stream);
 /* PPOLearner._train_step (agents/ppo/learning.py:131-143) on an IMPALA_ALGO_PPO handle:
  * forward, ppo_loss, backward, clip_grad_norm_, Adam; metrics slots 0-8 (slot 8 = target).

@@ -78,3 +78,4 @@ def test_kernel_entry_points_validate_before_launch():
     assert lib.impala_stage_wait(None, 0) == 1001
     assert lib.impala_slot_batch(None, 0, None, None) == 1001
     assert lib.impala_slot_release(None, 0, None) == 1001
+    assert lib.impala_act(None, None, 1, None, 0, 0, 0, None, None, None, None) == 1001

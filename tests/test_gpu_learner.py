@@ -140,6 +140,41 @@ def test_host_staging_ring_matches_device_batches(pull_wg, monkeypatch):
         e2.slot_batch(2)
 
 
+def test_native_act_argmax_flags_and_sampling_distribution():
+    """impala_act (distributed_models.py:21-32): logits / values equal the forward, argmax where
+    deterministic (per call or per frame), draws reproducible per (seed, counter), and the
+    sampled frequencies follow softmax(logits) (chi-square)."""
+    from scipy.stats import chisquare
+    dev = _dev()
+    from impala_amd.model import AtariPPOModel
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=1)
+    e = m._engine()
+    g = torch.Generator().manual_seed(0)
+    obs = torch.randint(0, 256, (200, 3, 64, 64), dtype=torch.uint8, generator=g).to(dev)
+    a, lg, v = e.act(obs, True)
+    lg2, v2 = m(obs)
+    assert torch.equal(lg, lg2) and torch.equal(v, v2)
+    assert torch.equal(a.squeeze(1), lg.argmax(-1))
+    flags = torch.zeros(200, dtype=torch.bool)
+    flags[::2] = True
+    a2, _, _ = e.act(obs, flags, seed=3, counter=1)
+    assert torch.equal(a2[::2], a[::2])
+    b1, _, _ = e.act(obs, False, seed=3, counter=5)
+    b2, _, _ = e.act(obs, False, seed=3, counter=5)
+    b3, _, _ = e.act(obs, False, seed=3, counter=6)
+    assert torch.equal(b1, b2) and not torch.equal(b1, b3)
+    assert int(b1.min()) >= 0 and int(b1.max()) < 15
+    # one frame's logits, many draws: frequencies vs softmax
+    one = obs[:1].expand(128, 3, 64, 64).contiguous()
+    counts = torch.zeros(15, dtype=torch.int64)
+    for c in range(60):
+        s, l1, _ = e.act(one, False, seed=11, counter=100 + c)
+        counts += torch.bincount(s.squeeze(1).cpu(), minlength=15)
+    p = torch.softmax(l1[0].double().cpu(), -1).numpy()
+    n = int(counts.sum())
+    assert chisquare(counts.numpy(), p * n).pvalue > 1e-4
+
+
 def test_model_act_and_checkpoint_roundtrip(tmp_path):
     dev = _dev()
     from impala_amd.model import AtariPPOModel
