@@ -544,6 +544,24 @@ DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
   }
 }
 
+// Sum of splits grp, grp + SG, ... of one float4 column of a slab, in split order.  The loads
+// are unconditional (split index clamped to S - 1) and out-of-range splits are dropped by a
+// value select after them: a "load or zero" select per element compiles to a branch and a
+// vmcnt(0) wait per load.
+template <int R>
+DEV f32x4 sum_splits(const float* p, int grp, int SG, int S, int count) {
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q = grp; q < S; q += R * SG) {
+    f32x4 v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      v[j] = *reinterpret_cast<const f32x4*>(p + (size_t)min(q + j * SG, S - 1) * count);
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc += v[j] * (q + j * SG < S ? 1.f : 0.f);
+  }
+  return acc;
+}
+
 // Each segment is processed by workgroups of 256 threads = (256/SG) float4 columns x SG
 // split groups; split group g sums splits g, g+SG, ... and the SG partials are combined in
 // LDS in a fixed order (deterministic for a given SG).  wg_start[] holds each segment's
@@ -564,22 +582,11 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   const bool in = v4 * 4 < sg.count;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   if (in) {
-    // 8 split loads in flight per round (the split count is >= 4 x SG by construction)
+    // R split loads in flight per round, R = 8 or 16 by the splits this thread sums (one
+    // round for every segment at the default split-group rule)
     const float* p = sg.slab + (size_t)v4 * 4;
-    // the loads are unconditional (split index clamped to S - 1) and out-of-range splits are
-    // dropped by a value select after them: a "load or zero" select per element compiles to a
-    // branch and a vmcnt(0) wait per load (one L2/HBM round trip per split)
-    for (int q = grp; q < sg.S; q += 8 * SG) {
-      f32x4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = *reinterpret_cast<const f32x4*>(p + (size_t)min(q + j * SG, sg.S - 1) * sg.count);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float keep = q + j * SG < sg.S ? 1.f : 0.f;
-        acc += v[j] * keep;
-      }
-    }
+    acc = (sg.S + SG - 1) / SG <= 8 ? sum_splits<8>(p, grp, SG, sg.S, sg.count)
+                                    : sum_splits<16>(p, grp, SG, sg.S, sg.count);
   }
   part[threadIdx.x] = acc;
   __syncthreads();
