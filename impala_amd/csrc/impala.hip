@@ -164,6 +164,7 @@ struct impala_learner {
   hipEvent_t h2d_join[kMaxH2D] = {};
   int n_h2d = 0;
   int h2d_pull_wg = 0;        // > 0: copy with h2d_pull_kernel on that many workgroups
+  int h2d_pull_threads = 256; // threads per pull workgroup (IMPALA_H2D_THREADS)
   hipStream_t h2d = nullptr;  // = h2d_s[0]
 };
 
@@ -957,10 +958,13 @@ int impala_stage_init(impala_learner* h, int nslots) {
       CK(hipEventCreateWithFlags(&h->h2d_join[i], hipEventDisableTiming));
     }
     h->h2d = h->h2d_s[0];
-    // pull kernel by default: 16 workgroups reach 41.5 GB/s pinned H2D on MI355X against
-    // 28.9 GB/s for hipMemcpyAsync (SDMA) and 36.6 GB/s for blit copies (profiles/r01k)
-    h->h2d_pull_wg = 16;
+    // pull kernel by default: 8 workgroups of 256 threads (one per XCD) reach 45.4 GB/s pinned
+    // H2D on MI355X, against 28.9 GB/s for hipMemcpyAsync (SDMA), 36.6 GB/s for blit copies and
+    // 37.9-41.5 GB/s for larger pull grids or blocks (profiles/r01k)
+    h->h2d_pull_wg = 8;
     if (const char* e = std::getenv("IMPALA_H2D_KERNEL")) h->h2d_pull_wg = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("IMPALA_H2D_THREADS"))
+      h->h2d_pull_threads = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
   }
   const size_t N = (size_t)h->N;
   size_t off = 0;
@@ -1033,7 +1037,7 @@ int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
       pa.bytes[pa.nf] = (long long)bytes[f];
       ++pa.nf;
     }
-    h2d_pull_kernel<<<h->h2d_pull_wg, 256, 0, h->h2d>>>(pa);
+    h2d_pull_kernel<<<h->h2d_pull_wg, h->h2d_pull_threads, 0, h->h2d>>>(pa);
     CK_LAUNCH("h2d_pull");
   } else {
     // obs in ns contiguous chunks (one per copy stream), the small fields on stream 0

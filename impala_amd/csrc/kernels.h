@@ -804,9 +804,9 @@ struct PullArgs {
   long long bytes[5];
   int nf;
 };
-__global__ __launch_bounds__(256) void h2d_pull_kernel(const PullArgs a) {
-  const long long stride = (long long)gridDim.x * 256;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(1024) void h2d_pull_kernel(const PullArgs a) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (int f = 0; f < a.nf; ++f) {
     const long long nv = a.bytes[f] >> 4;
     const f32x4* s = reinterpret_cast<const f32x4*>(a.src[f]);
