@@ -140,14 +140,15 @@ def test_host_staging_ring_matches_device_batches(pull_wg, monkeypatch):
         e2.slot_batch(2)
 
 
-def test_native_act_argmax_flags_and_sampling_distribution():
+@pytest.mark.parametrize("A", [15, 6])
+def test_native_act_argmax_flags_and_sampling_distribution(A):
     """impala_act (distributed_models.py:21-32): logits / values equal the forward, argmax where
     deterministic (per call or per frame), draws reproducible per (seed, counter), and the
     sampled frequencies follow softmax(logits) (chi-square)."""
     from scipy.stats import chisquare
     dev = _dev()
     from impala_amd.model import AtariPPOModel
-    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=1)
+    m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=1)
     e = m._engine()
     g = torch.Generator().manual_seed(0)
     obs = torch.randint(0, 256, (200, 3, 64, 64), dtype=torch.uint8, generator=g).to(dev)
@@ -163,13 +164,13 @@ def test_native_act_argmax_flags_and_sampling_distribution():
     b2, _, _ = e.act(obs, False, seed=3, counter=5)
     b3, _, _ = e.act(obs, False, seed=3, counter=6)
     assert torch.equal(b1, b2) and not torch.equal(b1, b3)
-    assert int(b1.min()) >= 0 and int(b1.max()) < 15
+    assert int(b1.min()) >= 0 and int(b1.max()) < A
     # one frame's logits, many draws: frequencies vs softmax
     one = obs[:1].expand(128, 3, 64, 64).contiguous()
-    counts = torch.zeros(15, dtype=torch.int64)
+    counts = torch.zeros(A, dtype=torch.int64)
     for c in range(60):
         s, l1, _ = e.act(one, False, seed=11, counter=100 + c)
-        counts += torch.bincount(s.squeeze(1).cpu(), minlength=15)
+        counts += torch.bincount(s.squeeze(1).cpu(), minlength=A)
     p = torch.softmax(l1[0].double().cpu(), -1).numpy()
     n = int(counts.sum())
     assert chisquare(counts.numpy(), p * n).pvalue > 1e-4

@@ -153,6 +153,30 @@ def test_ppo_grad_parts_match_whole():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(m2.flat_grad.cpu().numpy(), g)
     np.testing.assert_array_equal(e2.metrics.cpu().numpy(), met)
+    m3, e3 = _setup(dev, 64)  # three buckets
+    for part in (2, 3, 4):
+        e3.compute_grads_part(part, *batch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m3.flat_grad.cpu().numpy(), g)
+    np.testing.assert_array_equal(e3.metrics.cpu().numpy(), met)
+
+
+@pytest.mark.parametrize("pull_wg", [0, 8])
+def test_ppo_host_staging_ring_matches_device_batch(pull_wg, monkeypatch):
+    """impala_stage on a PPO handle (no discounts field): bitwise the same step as the batch
+    handed over in HBM, with hipMemcpyAsync or the pull kernel."""
+    dev = _dev()
+    monkeypatch.setenv("IMPALA_H2D_KERNEL", str(pull_wg))
+    host = [torch.from_numpy(np.ascontiguousarray(x)) for x in ref_cpu.synthetic_ppo_batch(64, 6, seed=8)]
+    m1, e1 = _setup(dev, 64, A=6)
+    e1.train_step(*[t.to(dev) for t in host])
+    m2, e2 = _setup(dev, 64, A=6)
+    e2.stage_init(1)
+    e2.stage(0, *[t.pin_memory() for t in host])
+    e2.train_step(e2.slot_batch(0))
+    e2.slot_release(0)
+    torch.cuda.synchronize()
+    assert torch.equal(m1.flat, m2.flat) and torch.equal(e1.metrics, e2.metrics)
 
 
 def test_ppo_learner_interface_matches_reference():
