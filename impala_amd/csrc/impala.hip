@@ -131,6 +131,7 @@ struct impala_learner {
   bool fwd_fused = true;       // conv1 + conv2 forward in one per-frame kernel
   int red_mode = 0;           // slab reductions: 0 all at the end, 1 per branch, 2 side + conv1
   int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
+  int c12f_fpw = 0;           // conv1+conv2 forward frames per workgroup (0: N / CUs)
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
   hipEvent_t* timer_ev = nullptr;
   // hipGraph replay of whole steps: the launch sequence of a step is captured once per batch
@@ -202,7 +203,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
   if (h->fwd_fused) {  // conv1 + conv2 per frame (act1 consumed from LDS)
-    const int fpw = std::max(1, cdiv(n, h->n_cu));
+    const int fpw = h->c12f_fpw > 0 ? h->c12f_fpw : std::max(1, cdiv(n, h->n_cu));
     timer_begin(h, K_CONV12_FWD, st);
     conv12_fwd_s2d<T><<<cdiv(n, fpw), 256 * c12f_groups<T>(), 0, st>>>(
         obs, sw + sh.w1, vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
@@ -571,6 +572,8 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->sp3 = plan_split((long)N * P3, K3 / 192, 192);
   h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
   h->c1_fpw = std::max(1, cdiv(N, h->n_cu));
+  if (const char* e = std::getenv("IMPALA_C1_FPW")) h->c1_fpw = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("IMPALA_C12F_FPW")) h->c12f_fpw = std::max(0, std::atoi(e));
   h->c1_wg = cdiv(N, h->c1_fpw);
   h->sp1.S = h->c1_wg;  // slab splits of conv1 (one per workgroup)
 
