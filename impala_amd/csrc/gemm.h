@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NACC = TRW * TCW * 4;
   constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per buffer
-  constexpr int NXV = BM * (BR / VEC), NYV = BM * (BC / VEC);
+  constexpr int NXV = BM * (BR / VEC);
   constexpr int NX = (NXV + 255) / 256;
   // Y staging: thread t owns m-row (t % BM) of the chunk and column vectors t/BM + i*(256/BM),
   // so the im2col row context (n, oy, ox) is derived once per chunk, not per vector.
