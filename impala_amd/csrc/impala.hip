@@ -964,7 +964,10 @@ int impala_stage_init(impala_learner* h, int nslots) {
     // pull kernel by default: 8 workgroups of 256 threads (one per XCD) reach 45.4 GB/s pinned
     // H2D on MI355X, against 28.9 GB/s for hipMemcpyAsync (SDMA), 36.6 GB/s for blit copies and
     // 37.9-41.5 GB/s for larger pull grids or blocks (profiles/r01k)
-    h->h2d_pull_wg = 8;
+    // Data-parallel handles (world_size > 1) keep hipMemcpyAsync unless IMPALA_H2D_KERNEL asks
+    // for the pull kernel: it is validated on one GPU, and whether every device of a node maps
+    // a rank's page-locked buffers is not something this library checks.
+    h->h2d_pull_wg = h->cfg.world_size == 1 ? 8 : 0;
     if (const char* e = std::getenv("IMPALA_H2D_KERNEL")) h->h2d_pull_wg = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("IMPALA_H2D_THREADS"))
       h->h2d_pull_threads = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
