@@ -36,7 +36,7 @@ EXPORTS = (
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
     "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
-    "impala_slot_release", "impala_act",
+    "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
 )
 # every symbol declared in include/sac_hip.h
 SAC_EXPORTS = (
@@ -113,6 +113,7 @@ def _declare(lib):
     lib.impala_bind_state.argtypes = [_P, _P, _P, _P, _P, _P, _P]
     lib.impala_refresh_weights.argtypes = [_P, _P]
     lib.impala_set_step.argtypes = [_P, C.c_int64, _P]
+    lib.impala_set_debug_vtrace.argtypes = [_P, _P]
     lib.impala_forward.argtypes = [_P, _P, C.c_int, _P, _P, _P]
     lib.impala_act.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_uint64, C.c_uint64, _P, _P, _P,
                                _P]

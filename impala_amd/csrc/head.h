@@ -38,6 +38,8 @@ struct HeadArgs {
   float* slab_h;        // [gridDim.x][16][256]
   float* slab_bh;       // [gridDim.x][16]
   float* heads_out;     // optional [N][16] (logits + value), nullptr = skip
+  float* vt_dbg;        // optional debug export (IMPALA only): adv, err, q [3][B][T-1] then
+                        // rho [B][T] -- the step's own V-trace outputs (impala_set_debug_vtrace)
 };
 
 constexpr int HEAD_SPLIT = 4;              // workgroups per trajectory group (hidden-column slices)
@@ -209,6 +211,15 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
       const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
       const float qq = r + g * boot;
       const float adv = fminf(a.cpg, rho) * (qq - v);
+      if (a.vt_dbg && lead && valid) {
+        const size_t BL = (size_t)a.B * L, o = (size_t)(traj0 + tl) * L + t;
+        if (inL) {
+          a.vt_dbg[o] = adv;
+          a.vt_dbg[BL + o] = err;
+          a.vt_dbg[2 * BL + o] = qq;
+        }
+        a.vt_dbg[3 * BL + f0 + fl] = rho;
+      }
       if (valid) {
         const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T_);
         const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;

@@ -132,6 +132,7 @@ struct impala_learner {
   int red_mode = 0;           // slab reductions: 0 all at the end, 1 per branch, 2 side + conv1
   int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
   int c12f_fpw = 0;           // conv1+conv2 forward frames per workgroup (0: N / CUs)
+  float* vt_dbg = nullptr;    // impala_set_debug_vtrace: the step's V-trace outputs
   int timer_kernel = -1, timer_cap = 0, timer_n = 0;
   hipEvent_t* timer_ev = nullptr;
   // hipGraph replay of whole steps: the launch sequence of a step is captured once per batch
@@ -301,6 +302,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     ha.cpg = h->cfg.clip_pg_rho_threshold; ha.ent_coef = h->cfg.entropy_coeff;
     ha.dz = h->dz; ha.partials = h->loss_part; ha.slab_h = h->s_h; ha.slab_bh = h->s_bh;
     ha.heads_out = h->heads;
+    ha.vt_dbg = h->cfg.algo == IMPALA_ALGO_PPO ? nullptr : h->vt_dbg;
     // torch.clamp(ratio, 1 - clip, 1 + clip): the bounds are python floats cast to fp32
     ha.clip_lo = (float)(1.0 - (double)h->cfg.ppo_clip);
     ha.clip_hi = (float)(1.0 + (double)h->cfg.ppo_clip);
@@ -392,7 +394,9 @@ part1:
     CK_LAUNCH("conv2_wgrad");
     if (h->red_mode == 1) {
       if (int r = reduce_segments(h, RS_CONV2, RS_CONV3, ss, 0)) return r;
-    } else if (h->red_mode == 2) {
+    } else if (h->red_mode == 2 && part != 1 && part != 4) {
+      // (parts 1 / 4: conv3 .. heads were reduced by parts 0 / 2-3 and may be in an
+      // all-reduce right now; the final reduction below covers conv1 + conv2)
       if (int r = reduce_segments(h, RS_CONV2, RS_END, ss, 0)) return r;
     }
   }
@@ -755,6 +759,13 @@ int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp
   h->red.grads = grads;
   h->red.metrics = metrics;
   return impala_refresh_weights(h, stream);
+}
+
+int impala_set_debug_vtrace(impala_learner* h, float* out) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (h->vt_dbg != out) drop_graphs(h);  // captured launches hold the previous pointer
+  h->vt_dbg = out;
+  return 0;
 }
 
 int impala_refresh_weights(impala_learner* h, void* stream) {

@@ -546,8 +546,9 @@ DEV long long canon_index(const RedArgs& a, const RedSeg& sg, int k) {
 
 // Sum of splits grp, grp + SG, ... of one float4 column of a slab, in split order.  The loads
 // are unconditional (split index clamped to S - 1) and out-of-range splits are dropped by a
-// value select after them: a "load or zero" select per element compiles to a branch and a
-// vmcnt(0) wait per load.
+// value select after them (a select, not a multiply by 0: an Inf in the clamped split must not
+// become a NaN); a "load or zero" select per element compiles to a branch and a vmcnt(0) wait
+// per load.
 template <int R>
 DEV f32x4 sum_splits(const float* p, int grp, int SG, int S, int count) {
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -557,7 +558,7 @@ DEV f32x4 sum_splits(const float* p, int grp, int SG, int S, int count) {
     for (int j = 0; j < R; ++j)
       v[j] = *reinterpret_cast<const f32x4*>(p + (size_t)min(q + j * SG, S - 1) * count);
 #pragma unroll
-    for (int j = 0; j < R; ++j) acc += v[j] * (q + j * SG < S ? 1.f : 0.f);
+    for (int j = 0; j < R; ++j) acc += q + j * SG < S ? v[j] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   return acc;
 }
@@ -682,14 +683,14 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   const float step_size = a.sc[0], bc2s = a.sc[1];
   float sq = 0.f;  // partials are zero-padded to a multiple of 4 (see impala_create)
   // 4 float4 partial loads in flight per thread (unconditional, clamped; out-of-range ones
-  // weighted 0), same summation order as one at a time
+  // dropped by a select), same summation order as one at a time
   const int nq = (a.n_part + 3) / 4;
   for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * 4) {
     f32x4 x[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) x[j] = *reinterpret_cast<const f32x4*>(a.sumsq_part + 4 * min(q0 + 256 * j, nq - 1));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sq += ((x[j][0] + x[j][1]) + (x[j][2] + x[j][3])) * (q0 + 256 * j < nq ? 1.f : 0.f);
+    for (int j = 0; j < 4; ++j) sq += q0 + 256 * j < nq ? (x[j][0] + x[j][1]) + (x[j][2] + x[j][3]) : 0.f;
   }
   sq = wave_sum(sq);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;

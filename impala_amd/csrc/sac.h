@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256) void adam_net_kernel(const AdamNetArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = a.sq[min(q0 + 256 * j, a.nsq - 1)];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sq += x[j] * (q0 + 256 * j < a.nsq ? 1.f : 0.f);
+      for (int j = 0; j < 8; ++j) sq += q0 + 256 * j < a.nsq ? x[j] : 0.f;
     }
     sq = wave_sum(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;

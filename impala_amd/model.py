@@ -50,6 +50,33 @@ class _Node(nn.Module):
     pass
 
 
+def rebind_views(root: nn.Module, specs, flat: torch.Tensor, grad: Optional[torch.Tensor]) -> None:
+    """Point every registered parameter of ``root`` (``specs`` order) back at its view of
+    ``flat`` (and its ``.grad`` at the view of ``grad``).  Unpickling (``torch.load`` of a
+    whole model) and ``copy.deepcopy`` rebuild each ``nn.Parameter`` on its own storage and
+    drop ``.grad``; the HIP library reads and writes the model through the flat buffers only."""
+    off = 0
+    for name, shape in specs:
+        cnt = int(np.prod(shape))
+        param = root.get_parameter(name)
+        param.data = flat[off:off + cnt].view(shape)
+        param.grad = None if grad is None else grad[off:off + cnt].view(shape)
+        off += cnt
+    assert off == flat.numel()
+
+
+# attributes holding native handles (ctypes pointers): never pickled, recreated lazily
+ENGINE_ATTRS = ("_train_engine", "_infer_engine", "_engine")
+
+
+def picklable_state(module: nn.Module) -> dict:
+    state = dict(module.__dict__)
+    for k in ENGINE_ATTRS:
+        if k in state and not callable(state[k]):
+            state[k] = None
+    return state
+
+
 class AtariPPOModel(nn.Module):
     """Drop-in for ``models.distributed_models.AtariPPOModel`` on an MI355X.
 
@@ -139,6 +166,18 @@ class AtariPPOModel(nn.Module):
         res = super().load_state_dict(state_dict, strict=strict, assign=False)
         self.params_changed()
         return res
+
+    # ---------------------------------------------------------------- pickling
+    def __getstate__(self):
+        """``torch.save(builder.learner_model)`` (reference main.py:117) works with engines
+        attached: the engines hold native handles and are dropped (an unpickled model creates
+        its inference engine lazily; a learner re-attaches its own)."""
+        return picklable_state(self)
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        rebind_views(self, self._specs, self.flat, self.flat_grad)
+        self.params_changed()
 
     # ---------------------------------------------------------------- compute
     def _engine(self):

@@ -113,6 +113,10 @@ class DeviceReplayBuffer(ReplayBuffer):
         self._st_next = 0
         self._stream = torch.cuda.Stream(device=d)
         self._pending: List[torch.cuda.Event] = []
+        # the last gather enqueued by sample(): an append must not overwrite a slot that a
+        # queued gather still reads (gathers run in order on the learner's stream, so waiting
+        # for the latest one covers every earlier read)
+        self._last_read: Optional[torch.cuda.Event] = None
 
     def append(self, item: Sequence[torch.Tensor]) -> int:
         s, a, r, g, mu = item
@@ -131,6 +135,8 @@ class DeviceReplayBuffer(ReplayBuffer):
             sm[:, 3:].copy_(mu.reshape(T, self.A))
             slot = self._cursor
             with torch.cuda.stream(self._stream):
+                if self._last_read is not None:
+                    self._stream.wait_event(self._last_read)
                 self.obs[slot].copy_(self._st_obs[j], non_blocking=True)
                 self.act[slot].copy_(self._st_act[j], non_blocking=True)
                 small = sm.to(self.device, non_blocking=True)
@@ -161,5 +167,9 @@ class DeviceReplayBuffer(ReplayBuffer):
             cur.wait_event(ev)
         idx_t = torch.from_numpy(idx.astype(np.int64)).to(self.device, non_blocking=True)
         batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx_t, stream)
+        read = torch.cuda.Event()
+        read.record(cur)
+        with self._cv:
+            self._last_read = read
         probs = np.full(batch_size, 1.0 / self._size)
         return keys, batch, probs

@@ -31,6 +31,7 @@ import torch.nn as nn
 
 from impala_amd import _lib
 from impala_amd.core import Actor, Builder, Learner
+from impala_amd.model import picklable_state, rebind_views
 
 HIDDEN = 256
 LOG_STD_MAX = 2
@@ -156,6 +157,18 @@ class SoftCritic(nn.Module):
     def params_changed(self) -> None:
         self._version += 1
 
+    def __getstate__(self):  # whole-model torch.save: drop the native engine handle
+        return picklable_state(self)
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        D, K = self.obs_dim, self.act_dim
+        rebind_views(self, critic_specs("critic", D, K), self.flat, self.flat_grad)
+        rebind_views(self, critic_specs("target_critic", D, K), self.target_flat, None)
+        self.log_alpha.data = self.la_buf[0:1].view(())
+        self.log_alpha.grad = self.la_buf[1:2].view(())
+        self.params_changed()
+
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         res = super().load_state_dict(state_dict, strict=strict, assign=False)
         self.params_changed()
@@ -209,6 +222,14 @@ class SoftActor(nn.Module):
     # ------------------------------------------------------------- parameters
     def params_changed(self) -> None:
         self._version += 1
+
+    def __getstate__(self):  # whole-model torch.save: drop the native engine handles
+        return picklable_state(self)
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        rebind_views(self, actor_specs(self.obs_dim, self.act_dim), self.flat, self.flat_grad)
+        self.params_changed()
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         res = super().load_state_dict(state_dict, strict=strict, assign=False)

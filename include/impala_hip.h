@@ -128,6 +128,12 @@ int impala_refresh_weights(impala_learner* h, void* stream);
 /* Adam step counter (torch state['step']); for checkpoint resume. */
 int impala_set_step(impala_learner* h, int64_t step, void* stream);
 
+/* Debug export of the step's own V-trace (IMPALA handles): when `out` is non-NULL, every
+ * following training step writes the pg_advantage, td_error and q_estimate it computed inside
+ * the fused head ([3][B][T-1], learning.py:150-153) and the importance ratio rho ([B][T],
+ * learning.py:148) to `out` (3*B*(T-1) + B*T floats, device memory).  NULL disables it. */
+int impala_set_debug_vtrace(impala_learner* h, float* out);
+
 /* Policy/value forward of n frames (n <= B*T): logits [n][A], values [n]. */
 int impala_forward(impala_learner* h, const uint8_t* obs, int n, float* logits, float* values,
                    void* stream);
@@ -141,7 +147,7 @@ int impala_act(impala_learner* h, const uint8_t* obs, int n, const uint8_t* dete
                int deterministic_all, uint64_t seed, uint64_t counter, int64_t* actions,
                float* logits, float* values, void* stream);
 
-/* Full learner update for one batch (world_size must be 1). *//* Full learner update for one batch (world_size must be 1). */
+/* Full learner update for one batch (world_size must be 1). */
 int impala_train_step(impala_learner* h, const impala_batch* batch, void* stream);
 /* PPOLearner._train_step (agents/ppo/learning.py:131-143) on an IMPALA_ALGO_PPO handle:
  * forward, ppo_loss, backward, clip_grad_norm_, Adam; metrics slots 0-8 (slot 8 = target).

@@ -20,7 +20,7 @@ boundary) -> ``tests/golden/*.npz`` -> ``tests/test_oracle_golden.py``.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -153,11 +153,12 @@ def collate(batch: Sequence[Sequence[torch.Tensor]]):
 
 def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
                max_grad_norm: float = 0.5, entropy_coeff: float = 0.01,
-               collated: bool = False) -> Dict[str, torch.Tensor]:
+               collated: bool = False, capture: Optional[dict] = None) -> Dict[str, torch.Tensor]:
     """agents/impala/learning.py:140-177 restated. ``batch`` = list of B trajectories
     ``[s u8 (T,3,64,64), a i64 (T,1), r f32 (T,1), g f32 (T,1), mu f32 (T,A)]``
     (format of ``ImpalaActor._make_replay``, learning.py:77-80), or already-collated
-    ``(s, a, r, g, mu)`` tensors when ``collated``."""
+    ``(s, a, r, g, mu)`` tensors when ``collated``.  ``capture`` (a dict) receives the step's
+    intermediate values: logits, values, rho, and the V-trace adv / err / q."""
     optimizer.zero_grad(set_to_none=True)
     s, a, r, discount_t, pi_ref = batch if collated else collate(batch)
     pi, values = model.forward(s.flatten(0, 1))
@@ -166,8 +167,12 @@ def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
     pi = torch.distributions.Categorical(logits=pi)
     pi_ref = torch.distributions.Categorical(logits=pi_ref)
     rho_tm1 = torch.exp(pi.log_prob(a) - pi_ref.log_prob(a))
-    adv, err, _ = batched_vtrace(values[:, :-1], values[:, 1:], r[:, :-1],
+    adv, err, q = batched_vtrace(values[:, :-1], values[:, 1:], r[:, :-1],
                                  discount_t[:, :-1], rho_tm1[:, :-1])
+    if capture is not None:
+        capture.update(logits=pi.logits.detach().clone(), values=values.detach().clone(),
+                       rho=rho_tm1.detach().clone(), adv=adv.detach().clone(),
+                       err=err.detach().clone(), q=q.detach().clone())
     pg_loss = (pi.log_prob(a)[:, :-1] * adv).mean()
     value_loss = err.pow(2).mean()
     entropy_loss = pi.entropy().mean()
@@ -185,6 +190,35 @@ def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
     metrics["train/grad_norm"] = grad_norm
     optimizer.step()
     return metrics
+
+
+def train_step_fp64(flat: np.ndarray, batch_np, A: int = 15, steps: int = 1,
+                    capture: Optional[dict] = None):
+    """The same step in float64 (model, batch floats, autograd, Adam): the exact-arithmetic
+    yardstick against which both the fp32 oracle and the HIP fp32 path are measured.
+    -> (final flat params, flat post-clip grads (p.grad after clip_grad_norm_) of the last step, metrics of the last step)."""
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        ref = RefModel(A).double()
+        with torch.no_grad():
+            off = 0
+            for p in ref.parameters():
+                n = p.numel()
+                p.copy_(torch.from_numpy(np.asarray(flat[off:off + n], np.float64)).reshape(p.shape))
+                off += n
+        opt = make_optimizer(ref)
+        obs, act, rew, disc, mu = batch_np
+        b = [torch.from_numpy(obs), torch.from_numpy(act),
+             torch.from_numpy(rew.astype(np.float64)), torch.from_numpy(disc.astype(np.float64)),
+             torch.from_numpy(mu.astype(np.float64))]
+        for _ in range(steps):
+            met = train_step(ref, opt, b, collated=True, capture=capture)
+        grads = torch.cat([p.grad.detach().reshape(-1) for p in ref.parameters()]).numpy().copy()
+        params = torch.cat([p.detach().reshape(-1) for p in ref.parameters()]).numpy().copy()
+        return params, grads, {k: float(v) for k, v in met.items()}
+    finally:
+        torch.set_default_dtype(prev)
 
 
 def local_grads(model: nn.Module, batch_collated, entropy_coeff: float = 0.01) -> np.ndarray:

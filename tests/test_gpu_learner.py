@@ -219,3 +219,90 @@ def test_optimizer_state_resume_matches_uninterrupted():
     m_b.load_state_dict(sd)
     m_b, _ = run(batches[2:], m_b, st)
     torch.testing.assert_close(m_b.flat, m_full.flat, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("pull_wg", [0, 8])
+def test_learner_host_batches_distinct_per_step(pull_wg, monkeypatch):
+    """ImpalaLearner.train_step on host (list-of-trajectories) batches reuses two page-locked
+    staging buffers in place; with a DIFFERENT batch every step (hipMemcpyAsync or the PCIe
+    pull kernel) the weights and metrics are bitwise those of the same batches handed over
+    already in HBM -- a stale or torn read of a reused host buffer would show here."""
+    dev = _dev()
+    monkeypatch.setenv("IMPALA_H2D_KERNEL", str(pull_wg))
+    from impala_amd.engine import Engine
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    B, T, A, steps = 4, 20, 15, 6
+    batches = [ref_cpu.synthetic_batch(B, T, A, seed=500 + s) for s in range(steps)]
+    m1 = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+    ln = ImpalaLearner(m1, _FixedReplay([ref_cpu.to_trajectories(*b) for b in batches]),
+                       batch_size=B, rollout_length=T, model_push_period=1000)
+    mets = [ln.train_step() for _ in range(steps)]
+    m2 = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+    e2 = Engine(m2, batch_size=B, rollout_length=T)
+    m2._train_engine = e2
+    for s, b in enumerate(batches):
+        e2.train_step(*[torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in b])
+        torch.cuda.synchronize()
+        assert float(mets[s]["train/loss"]) == float(e2.metrics[0]), s
+    torch.cuda.synchronize()
+    assert torch.equal(m1.flat, m2.flat)
+
+
+def test_device_replay_overwrite_waits_for_queued_gather():
+    """An append into the slot a queued gather still reads must wait for that gather: fill a
+    capacity-4 ring, sample all 4, immediately append into the oldest slot, then check the
+    gathered batch holds the old trajectories (not the new one)."""
+    dev = _dev()
+    from impala_amd.replay import DeviceReplayBuffer
+    T, A = 20, 15
+
+    def item(i):
+        obs, act, rew, disc, mu = ref_cpu.synthetic_batch(1, T, A, seed=900 + i)
+        return [torch.from_numpy(obs[0]), torch.from_numpy(act[0]).unsqueeze(-1),
+                torch.from_numpy(rew[0]).unsqueeze(-1), torch.from_numpy(disc[0]).unsqueeze(-1),
+                torch.from_numpy(mu[0])]
+
+    rb = DeviceReplayBuffer(capacity=4, rollout_length=T, num_actions=A, device=dev, seed=1)
+    old = [item(i) for i in range(4)]
+    for it in old:
+        rb.append(it)
+    torch.cuda.synchronize()
+    # keep the learner stream busy so the gather is still queued when the append is issued
+    busy = torch.randn(4096, 4096, device=dev)
+    for _ in range(8):
+        busy = busy @ busy
+        busy = busy / busy.norm()
+    keys, batch, _ = rb.sample(4)
+    rb.append(item(99))  # overwrites slot 0 (key 0) on the replay's own stream
+    torch.cuda.synchronize()
+    for j, k in enumerate(keys.tolist()):
+        np.testing.assert_array_equal(batch[0][j].cpu().numpy(), old[k][0].numpy())
+        np.testing.assert_array_equal(batch[4][j].cpu().numpy(), old[k][4].numpy())
+
+
+def test_whole_model_checkpoint_after_learner_step(tmp_path):
+    """reference main.py:117 torch.save(builder.learner_model, ...) with the learner's engine
+    (a native handle) attached: the model pickles, reloads with its parameters and gradients
+    still views of the flat buffers, and serves forward through a fresh engine."""
+    dev = _dev()
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    B, T = 2, 20
+    batch = ref_cpu.synthetic_batch(B, T, 15, seed=77)
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+    ln = ImpalaLearner(m, _FixedReplay([ref_cpu.to_trajectories(*batch)]), batch_size=B,
+                       rollout_length=T)
+    ln.train_step()
+    obs = torch.from_numpy(batch[0][0]).to(dev)
+    lg0, v0 = m(obs)
+    torch.save(m, tmp_path / "model.pt")
+    m2 = torch.load(tmp_path / "model.pt", weights_only=False)  # our own file
+    assert m2._train_engine is None and m2._infer_engine is None
+    assert torch.equal(m2.flat, m.flat)
+    w = m2.get_parameter("model.projection.1.weight")
+    off = m2._views["model.projection.1.weight"][0]
+    assert w.data_ptr() == m2.flat[off:].data_ptr()
+    assert w.grad.data_ptr() == m2.flat_grad[off:].data_ptr()
+    lg1, v1 = m2(obs)
+    assert torch.equal(lg0, lg1) and torch.equal(v0, v1)
