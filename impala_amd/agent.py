@@ -1,18 +1,31 @@
-"""DistributedAgent — the learner-side driver of ``agents/distributed_agent.py:15-59``.
+"""DistributedAgent — the learner-side driver of ``agents/distributed_agent.py:15-68``.
 
-``train(num_steps)``: ``learner.prepare()`` then ``learner.train_step()`` x num_steps, metric
-aggregation and a log call every 100 steps, as the reference.  Improvement kept optional:
-``sync_every`` > 1 converts the device metrics to floats only every k steps (the reference's
-``float(v)`` per step is a host-device sync per step).  The rlmeta controller / eval loops
-are out of scope: a controller object with the reference's interface may be passed in.
+``train(num_steps)``: ``controller.set_phase(Phase.TRAIN)``, ``learner.prepare()``, then
+``learner.train_step()`` x num_steps with every metric folded into the stats dict and a log
+call every 100 steps; afterwards the controller's TRAIN episode statistics give
+``total_samples`` (mean episode length x episode count), logged with
+``debug/samples_per_second`` and the ``train_envs/*`` means, and returned -- as the reference.
+``eval`` runs the reference's controller protocol.  One optional change: ``sync_every`` > 1
+converts the device metrics to floats only every k steps (the reference's ``float(v)`` per step
+is a host-device sync per step).  The rlmeta controller itself is out of scope: any object with
+its interface (set_phase, reset_phase, count, stats, connect) may be passed in.
 """
 from __future__ import annotations
 
+import enum
 import time
 from collections import defaultdict
 from typing import Callable, Dict, Optional
 
 from impala_amd.core import Agent, Learner
+
+
+class Phase(enum.IntFlag):
+    """rlmeta.core.controller.Phase (the controller's phase flags)."""
+    NONE = 0
+    TRAIN = 1
+    EVAL = 2
+    BOTH = 3
 
 
 class StatsDict:
@@ -36,8 +49,7 @@ class StatsDict:
 
 
 class DistributedAgent(Agent):
-    def __init__(self, controller, learner: Learner, writer: Optional[Callable] = None,
-                 sync_every: int = 1):
+    def __init__(self, controller, learner: Learner, writer=None, sync_every: int = 1):
         self._controller = controller
         self._learner = learner
         self._writer = writer
@@ -45,17 +57,25 @@ class DistributedAgent(Agent):
         self._start_time = time.perf_counter()
         self._sync_every = max(1, int(sync_every))
 
-    def set_phase(self, phase=None):
+    def set_phase(self, phase=Phase.TRAIN):
         if self._controller is not None:
             self._controller.set_phase(phase=phase)
 
     def _log(self, d):
-        if self._writer is not None:
-            self._writer(d)
+        """The reference logs through ``writer.run.log`` (a wandb run); a plain callable works
+        too."""
+        w = self._writer
+        if w is None:
+            return
+        run = getattr(w, "run", None)
+        if run is not None and hasattr(run, "log"):
+            run.log(d)
+        elif callable(w):
+            w(d)
 
-    def train(self, num_steps: int) -> int:
+    def train(self, num_steps: int):
         if self._controller is not None:
-            self._controller.set_phase("TRAIN")
+            self._controller.set_phase(Phase.TRAIN)
         self._learner.prepare()
         pending = []
         for local_steps in range(num_steps):
@@ -67,12 +87,31 @@ class DistributedAgent(Agent):
                 pending = []
             if local_steps % 100 == 0:
                 self._log({k: float(v) for k, v in metrics.items()})
-        return num_steps
+        if self._controller is None:
+            # no actor side to ask: the frames this learner consumed
+            total_samples = float(num_steps * getattr(self._learner, "samples_per_step", 0))
+        else:
+            remote = self._controller.stats(Phase.TRAIN).dict()
+            total_samples = remote["episode_length"]["mean"] * remote["episode_length"]["count"]
+        delta = total_samples / (time.perf_counter() - self._start_time)
+        self._log({"debug/total_samples": total_samples})
+        if self._controller is not None:
+            self._log({f"train_envs/{k.replace('/', '_')}": v["mean"] for k, v in remote.items()})
+        self._log({"debug/samples_per_second": delta})
+        return total_samples
 
     def eval(self, num_episodes: Optional[int] = None, keep_training_loops: bool = True):
+        """distributed_agent.py:44-56: switch the controller to EVAL (or BOTH), wait until
+        ``num_episodes`` evaluation episodes are counted, log and return their stats."""
         if self._controller is None:
-            raise NotImplementedError("evaluation needs the actor/controller side (out of scope)")
-        raise NotImplementedError
+            raise RuntimeError("eval needs a controller (the actor side is out of scope)")
+        self._controller.set_phase(Phase.BOTH if keep_training_loops else Phase.EVAL)
+        self._controller.reset_phase(Phase.EVAL, limit=num_episodes)
+        while self._controller.count(Phase.EVAL) < num_episodes:
+            time.sleep(1)
+        stats = self._controller.stats(Phase.EVAL)
+        self._log({f"eval_envs/{k.replace('/', '_')}": v["mean"] for k, v in stats.dict().items()})
+        return stats
 
     def connect(self):
         if self._controller is not None and hasattr(self._controller, "connect"):

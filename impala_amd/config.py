@@ -1,10 +1,13 @@
-"""Config tree with the reference's Hydra keys (conf/config.yaml:1-46, conf/agent/impala.yaml,
-conf/deploy/local.yaml, conf/task/procgen.yaml), loaded with yaml.safe_load (Hydra is not a
-dependency).  Attribute access like OmegaConf: ``cfg.agent.batch_size``."""
+"""Config tree with the reference's Hydra surface (conf/config.yaml, conf/agent/*.yaml,
+conf/deploy/*.yaml, conf/task/*.yaml: the same files, keys and values; checked against the
+reference's key sets by tests/test_host_logic.py), loaded with yaml.safe_load (Hydra and
+OmegaConf are not dependencies): the defaults list picks the group files, ``${...}``
+interpolations are resolved, attribute access works like OmegaConf (``cfg.agent.batch_size``)."""
 from __future__ import annotations
 
 import copy
 import os
+import re
 from typing import Any, Dict, Optional
 
 import yaml
@@ -57,20 +60,68 @@ def _num(x):
     return x
 
 
-def load_config(overrides: Optional[Dict[str, Any]] = None, deploy: Optional[str] = None,
+_INTERP = re.compile(r"\$\{([^}]+)\}")
+
+
+def _lookup(root: Dict[str, Any], path: str):
+    node: Any = root
+    for part in path.strip().split("."):
+        if not isinstance(node, dict) or part not in node:
+            raise KeyError(f"interpolation ${{{path}}}: no key {part!r}")
+        node = node[part]
+    return node
+
+
+def _resolve(node: Any, root: Dict[str, Any], depth: int = 0):
+    """OmegaConf-style ``${a.b}`` interpolation (absolute key paths): a value that is exactly one
+    interpolation takes the referenced value (and type); otherwise the pieces are joined as a
+    string (conf/config.yaml:17 ``${distributed.server_addr}:${distributed.m_port}``)."""
+    if depth > 16:
+        raise ValueError("interpolation cycle")
+    if isinstance(node, dict):
+        return {k: _resolve(v, root, depth) for k, v in node.items()}
+    if isinstance(node, list):
+        return [_resolve(v, root, depth) for v in node]
+    if isinstance(node, str) and "${" in node:
+        m = _INTERP.fullmatch(node)
+        if m:
+            return _resolve(_lookup(root, m.group(1)), root, depth + 1)
+        return _INTERP.sub(lambda mm: str(_resolve(_lookup(root, mm.group(1)), root, depth + 1)),
+                           node)
+    return node
+
+
+def _defaults(spec) -> Dict[str, str]:
+    """Hydra defaults list -> {group: option}.  Accepts the reference's list form
+    (``- _self_``, ``- agent: impala``, ``- override hydra/...: disabled``; the hydra logging
+    overrides are ignored) and the older mapping form."""
+    out: Dict[str, str] = {}
+    if isinstance(spec, dict):
+        return dict(spec)
+    for item in spec or []:
+        if isinstance(item, dict):
+            for k, v in item.items():
+                if not str(k).startswith("override "):
+                    out[str(k)] = v
+    return out
+
+
+def load_config(overrides: Optional[Dict[str, Any]] = None, deploy: Optional[str] = "local",
                 agent: Optional[str] = None, task: Optional[str] = None) -> Cfg:
-    """Compose config.yaml + agent + task + deploy overlay (+ overrides), as main.py:39-53.
+    """Compose config.yaml + agent + task (its defaults list) + a deploy overlay (+ overrides)
+    and resolve interpolations, as main.py:39-53 under ``python main.py +deploy=local``.
     ``agent`` / ``task`` select the group files as Hydra's ``agent=sac task=mujoco`` would
-    (agent=sac alone implies task=mujoco, the reference's SAC task)."""
+    (agent=sac alone implies task=mujoco, the reference's SAC task); ``deploy=None`` composes
+    without an overlay."""
     base = _load(os.path.join(CONF_DIR, "config.yaml"))
-    defaults = base.pop("defaults", {})
+    defaults = _defaults(base.pop("defaults", []))
     cfg = dict(base)
     agent = agent or defaults.get("agent", "impala")
     task = task or ("mujoco" if agent == "sac" else defaults.get("task", "procgen"))
     cfg["agent"] = _load(os.path.join(CONF_DIR, "agent", f"{agent}.yaml"))
     cfg["task"] = _load(os.path.join(CONF_DIR, "task", f"{task}.yaml"))
-    dep = deploy or defaults.get("deploy", "local")
+    dep = deploy if deploy is not None else defaults.get("deploy")
     if dep:
         cfg = _merge(cfg, _load(os.path.join(CONF_DIR, "deploy", f"{dep}.yaml")))
     cfg = _merge(cfg, overrides or {})
-    return Cfg.wrap(_num(cfg))
+    return Cfg.wrap(_num(_resolve(cfg, cfg)))

@@ -104,6 +104,12 @@ class ImpalaLearner(Learner):
             self._device = self._model.flat.device
         return self._device
 
+    @property
+    def samples_per_step(self) -> int:
+        """Environment frames one train_step consumes (DistributedAgent.train's total without
+        a controller)."""
+        return self._batch_size * self._rollout_length
+
     def prepare(self):  # learning.py:116-117
         self._replay_buffer.warm_up(self._learning_starts)
 

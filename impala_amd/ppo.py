@@ -97,6 +97,12 @@ class PPOLearner(Learner):
             self._device = self._model.flat.device
         return self._device
 
+    @property
+    def samples_per_step(self) -> int:
+        """Environment frames one train_step consumes (DistributedAgent.train's total without
+        a controller)."""
+        return self._batch_size
+
     def prepare(self):  # learning.py:105-108
         if not self.can_train:
             self._replay_buffer.warm_up(self._learning_starts)

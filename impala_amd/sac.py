@@ -520,6 +520,12 @@ class SACLearner(Learner):
             self._device = self._model.flat.device
         return self._device
 
+    @property
+    def samples_per_step(self) -> int:
+        """Environment frames one train_step consumes (DistributedAgent.train's total without
+        a controller)."""
+        return self._batch_size
+
     def prepare(self):  # learning.py:141-144
         if self.can_train is False:
             self._replay_buffer.warm_up(self._learning_starts)

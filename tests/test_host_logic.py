@@ -59,6 +59,60 @@ def test_config_surface_matches_reference_keys():
     assert c2.agent.batch_size == 64 and c2.learner.dtype == "fp32"
 
 
+def _flatten(d, prefix=""):
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, dict):
+            out.update(_flatten(v, f"{prefix}{k}."))
+        else:
+            out[f"{prefix}{k}"] = v
+    return out
+
+
+# keys this repo adds on top of the reference's files (everything else must match exactly)
+_EXTRA_KEYS = {"config.yaml": ("learner.",), "agent/": ("name",)}
+
+
+def test_conf_surface_matches_reference():
+    """Every YAML file of the reference's conf/ exists here with the same keys and the same
+    values (tests/golden/conf_keys.json, generated from the reference by make_conf_keys.py);
+    additions are limited to the learner.* block and an agent `name`."""
+    import json
+    import yaml
+    from impala_amd.config import CONF_DIR
+    ref = json.load(open(os.path.join(G, "conf_keys.json")))
+    for rel, want in ref.items():
+        path = os.path.join(CONF_DIR, rel)
+        assert os.path.exists(path), f"conf/{rel} missing"
+        with open(path) as f:
+            got = _flatten(yaml.safe_load(f) or {})
+        extra = ()
+        for pre, keys in _EXTRA_KEYS.items():
+            if rel == pre or rel.startswith(pre):
+                extra = keys
+        added = [k for k in got if k not in want]
+        assert all(any(k.startswith(e) for e in extra) for k in added), (rel, added)
+        for k, v in want.items():
+            assert k in got, f"conf/{rel}: key {k} missing"
+            assert got[k] == v, f"conf/{rel}: {k} = {got[k]!r}, reference {v!r}"
+
+
+def test_config_interpolations_and_groups():
+    c = load_config()
+    assert c.distributed.m_server_addr == "127.0.0.1:4411"  # conf/config.yaml:17
+    assert c.distributed.r_server_addr == "127.0.0.1:4412"
+    assert c.distributed.c_server_addr == "127.0.0.1:4413"
+    assert c.hydra.run.dir == "." and c.hydra.output_subdir is None
+    c2 = load_config({"distributed": {"server_addr": "10.0.0.2"}})
+    assert c2.distributed.m_server_addr == "10.0.0.2:4411"
+    assert load_config(agent="apex").agent.target_sync_period == 2500
+    assert load_config(task="atari").task.env_id == "Breakout-v5"
+    assert load_config(deploy="mila").distributed.host == "mila"
+    assert load_config(deploy=None).agent.learning_starts == 100
+    # the drop-in default computes in the reference's arithmetic
+    assert load_config().learner.dtype == "fp32"
+
+
 def _traj(T=20, A=15, fill=0):
     return [torch.full((T, 3, 64, 64), fill, dtype=torch.uint8),
             torch.zeros(T, 1, dtype=torch.int64), torch.zeros(T, 1), torch.zeros(T, 1),
@@ -152,3 +206,76 @@ def test_ppo_collate_transitions_matches_torch_cat():
     s2, a2, t2, mu2 = collate_transitions([[x[0][0], x[1][0], x[2][0], x[3][0]] for x in items],
                                           torch.device("cpu"))
     assert torch.equal(s2, s) and torch.equal(a2, a) and torch.equal(t2, t) and torch.equal(mu2, mu)
+
+
+class _Ctl:
+    """rlmeta controller stand-in (set_phase / reset_phase / count / stats / connect)."""
+
+    def __init__(self):
+        self.phases, self.n = [], 0
+
+    def set_phase(self, phase):
+        self.phases.append(phase)
+
+    def reset_phase(self, phase, limit=None):
+        self.limit = limit
+
+    def count(self, phase):
+        self.n += 2
+        return self.n
+
+    def stats(self, phase):
+        from impala_amd.agent import StatsDict
+        s = StatsDict()
+        for x in (100, 200, 300):
+            s.extend({"episode_length": x, "episode_return": x / 10})
+        return s
+
+
+class _Learner:
+    samples_per_step = 160
+
+    def __init__(self):
+        self.steps = 0
+
+    def prepare(self):
+        pass
+
+    def connect(self):
+        pass
+
+    def train_step(self):
+        self.steps += 1
+        return {"train/loss": torch.tensor(1.0 / self.steps)}
+
+
+class _Writer:
+    def __init__(self):
+        self.logs = []
+
+        class _Run:
+            def log(run, d):
+                self.logs.append(d)
+        self.run = _Run()
+
+
+def test_distributed_agent_train_returns_total_samples():
+    """agents/distributed_agent.py:26-42: train returns total_samples = mean episode length x
+    episode count from the controller's TRAIN stats and logs debug/total_samples,
+    train_envs/* and debug/samples_per_second through writer.run.log."""
+    from impala_amd.agent import DistributedAgent, Phase
+    ctl, w = _Ctl(), _Writer()
+    ag = DistributedAgent(ctl, _Learner(), w)
+    total = ag.train(250)
+    assert total == 200 * 3
+    assert ctl.phases == [Phase.TRAIN]
+    keys = [k for d in w.logs for k in d]
+    assert keys.count("train/loss") == 3  # steps 0, 100, 200
+    assert "debug/total_samples" in keys and "debug/samples_per_second" in keys
+    assert "train_envs/episode_return" in keys
+    assert ag.stats.dict()["train/loss"]["count"] == 250
+    ev = ag.eval(num_episodes=6, keep_training_loops=False)
+    assert ctl.phases[-1] == Phase.EVAL and ctl.limit == 6
+    assert ev.dict()["episode_length"]["mean"] == 200
+    # without a controller: the frames the learner consumed
+    assert DistributedAgent(None, _Learner(), w).train(5) == 5 * 160
