@@ -11,9 +11,21 @@ backward, [RCCL gradient all-reduce], clip_grad_norm_(0.5), Adam) on a synthetic
 is resident in HBM before the timed region.  Multi-GPU: data-parallel
 replicas, B=64 per GPU (weak scaling), one flat fp32 gradient bucket all-reduced over RCCL.
 
-Also reported: the dominant kernel's roofline (algorithmic FLOPs / its live HIP-event launch
-duration vs the dense MFMA peak) and the reference CPU learner (the oracle's torch-CPU
-restatement of agents/impala/learning.py:140-177) timed on this host's cores.
+Also reported, all from the same run:
+* ``roofline`` / ``roofline_top2``: the two kernels with algorithmic work that take longest
+  (chosen from every kernel's average over --steps untimed steps, ``kernel_us``), each timed
+  live over the timed steps by hipExtLaunchKernel start/stop events (the kernel's own begin /
+  end stamps, the duration rocprofv3's kernel trace reports): algorithmic FLOPs or bytes /
+  that duration vs the dense MFMA or HBM peak, plus the PMC-measured HBM traffic per launch
+  from the newest matching profiles/*/summary.json;
+* ``step_roofline``: SURVEY.md §8(d)'s step-level figure, frames/s x 17.74 MFLOP/frame vs
+  the dense MFMA peak;
+* ``fp32_parity_mode``: the same workload in fp32 (the reference's arithmetic);
+* ``host_staged``: the PCIe-inclusive rate (batches from page-locked host memory), never
+  ``value``;
+* ``cpu_baseline``: the reference CPU learner (the oracle's torch-CPU restatement of
+  agents/impala/learning.py:140-177) on this host's cores, with a 1-thread leg and the host's
+  CPU share stated.
 """
 from __future__ import annotations
 
@@ -62,6 +74,8 @@ def kernel_work(es):
 
 
 STEP_FLOPS_PER_FRAME = 17_743_872  # fwd 6,836,224 + bwd 10,907,648 (no conv1 dgrad)
+# PPO: same trunk, one loss head per transition (the heads' work is ~0.1 % of the total)
+STEP_FLOPS_PER_FRAME_PPO = STEP_FLOPS_PER_FRAME
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA, MI355X_MICROARCH.md
 
@@ -109,14 +123,38 @@ def cpu_baseline_ppo(N, A, seconds):
                       f"{threads} threads) after 2 warm-up; median step {med * 1e3:.1f} ms"}
 
 
-def cpu_baseline(B, T, A, seconds):
+def host_cpu_info():
+    """CPU model, the CPUs this process may run on (the box's share) and the machine's total."""
+    try:
+        cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
+    except Exception:
+        cpu = "unknown"
+    try:
+        share = len(os.sched_getaffinity(0))
+    except Exception:
+        share = os.cpu_count()
+    return {"cpu": cpu, "cpus_allowed": share, "cpus_machine": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(B, T, A, seconds, threads=None, warmup=2):
     """The reference CPU learner (oracle port of learning.py:140-177), timed on host cores."""
     from oracle import ref_cpu
+    prev = torch.get_num_threads()
+    if threads:
+        torch.set_num_threads(threads)
+    try:
+        return _cpu_baseline(ref_cpu, B, T, A, seconds, warmup)
+    finally:
+        torch.set_num_threads(prev)
+
+
+def _cpu_baseline(ref_cpu, B, T, A, seconds, warmup):
     threads = torch.get_num_threads()
     batch = [torch.from_numpy(x) for x in ref_cpu.synthetic_batch(B, T, A, seed=1234)]
     model = ref_cpu.make_model(0, A)
     opt = ref_cpu.make_optimizer(model)
-    for _ in range(2):
+    for _ in range(warmup):
         ref_cpu.train_step(model, opt, batch, collated=True)
     times = []
     t_end = time.perf_counter() + seconds
@@ -125,13 +163,11 @@ def cpu_baseline(B, T, A, seconds):
         ref_cpu.train_step(model, opt, batch, collated=True)
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
-    try:
-        cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
-    except Exception:
-        cpu = "unknown"
+    cpu = host_cpu_info()["cpu"]
     return {"value": B * T / med, "unit": "env-frames/s", "cores": threads, "kind": "port",
             "sample": f"{len(times)} oracle learner steps (B={B},T={T},fp32 torch-CPU, "
-                      f"{threads} threads, {cpu}) after 2 warm-up; median step {med * 1e3:.1f} ms"}
+                      f"{threads} threads, {cpu}) after {warmup} warm-up; median step "
+                      f"{med * 1e3:.1f} ms"}
 
 
 def run_host_staged(eng, batch, args, dist, model, world):
@@ -190,9 +226,10 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}
 
 
-def profiled_traffic(kernel, dtype, names=None):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/<tag>/summary.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+def profiled_traffic(kernel, dtype, names=None, algo="impala"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
+    same algorithm and dtype (profiles/<tag>/summary.json: "algo" defaults to impala; FETCH_SIZE
+    x2 gfx950 correction + WRITE_SIZE), or None."""
     root = os.path.join(HERE, "profiles")
     if not os.path.isdir(root):
         return None, None
@@ -205,7 +242,7 @@ def profiled_traffic(kernel, dtype, names=None):
             js = json.load(open(p))
         except Exception:
             continue
-        if js.get("dtype", "bf16") != dtype:
+        if js.get("dtype", "bf16") != dtype or js.get("algo", "impala") != algo:
             continue
         for k in js.get("kernels", []):
             if k.get("kernel") == (names or PROFILE_NAMES).get(kernel) and k.get("hbm_bytes"):
@@ -383,7 +420,7 @@ def run_sac(args):
         bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
-    traffic, tsrc = profiled_traffic(rk, args.dtype, SAC_PROFILE_NAMES)
+    traffic, tsrc = profiled_traffic(rk, args.dtype, SAC_PROFILE_NAMES, algo="sac")
     traffic_src = (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+WRITE_SIZE, "
                    "bytes per launch)") if tsrc else None
     # per-step algorithmic flops: the phases that ran (probe), else the fused step's phases
@@ -429,6 +466,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--roofline-kernel", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds-1t", type=float, default=8.0,
+                    help="sample length of the 1-thread CPU baseline leg")
+    ap.add_argument("--no-fp32-line", action="store_true",
+                    help="skip the fp32 parity-mode sub-record of a bf16 run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-staged", action="store_true",
                     help="skip the PCIe-inclusive pass (host batches through impala_stage)")
@@ -479,32 +520,98 @@ def main():
         dist.broadcast(model.flat, 0)
         model.params_changed()
 
-    def step():
-        if dist is None:
-            eng.train_step(*batch)
-        else:
-            compute_grads_allreduced(eng, batch, model.flat_grad)
-            eng.apply_update()
+    def make_step(e, m):
+        def step():
+            if dist is None:
+                e.train_step(*batch)
+            else:
+                compute_grads_allreduced(e, batch, m.flat_grad)
+                e.apply_update()
+        return step
 
+    step = make_step(eng, model)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    rk = args.roofline_kernel
     work = kernel_work(2 if args.dtype == "bf16" else 4)
-    # dominant kernel: pick the one with the largest measured time in a short probe
-    probe = {}
-    if rk is None:
-        for kname in eng.kernel_names():
-            eng.timer_start(kname, 3)
-            for _ in range(3):
-                step()
-            ms, n = eng.timer_read()
-            if n:
-                probe[kname] = ms / n
-        rk = max((k for k in probe if k in work and work[k][0]), key=probe.get)
-    torch.cuda.synchronize()
+    kernel_us, top = select_kernels(eng, step, work, args)
+    elapsed, k_times = timed_steps(eng, step, top, args, dist, dev)
+    met = eng.metrics.cpu().numpy()
+    if not np.all(np.isfinite(met)):
+        raise RuntimeError(f"non-finite metrics {met}")
 
-    eng.timer_start(rk, args.steps)
+    frames = world * B * T * args.steps
+    value = frames / elapsed
+    ms_step = elapsed * 1e3 / args.steps
+    algo = args.algo
+    rooflines = [kernel_roofline(k, k_times[k], work, B * T, args.dtype, algo) for k in top]
+    metric = "learner env-frames/sec (IMPALA procgen T=20 B=64) at 1/2/4/8 MI355X"
+    workload = f"IMPALA procgen learner step, NatureCNN actor-critic, B={B}/GPU T={T} A={A}, " \
+               f"global B={B * world}"
+    if ppo:
+        metric = "PPO learner transitions/sec (procgen, NatureCNN, BASELINE config 4)"
+        workload = f"PPO learner step (clip 0.1), NatureCNN actor-critic, N={B} transitions/GPU"
+    step_flops_pf = STEP_FLOPS_PER_FRAME if not ppo else STEP_FLOPS_PER_FRAME_PPO
+    out = {
+        "metric": metric,
+        "value": round(value, 1), "unit": "env-frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "algo": algo,
+        "data": "synthetic rollouts resident in HBM (obs u8 uniform, BASELINE.md §3); "
+                "random-init weights (reference layer_init_truncated, seed 0)",
+        "config": {"workload": workload,
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+        "roofline": rooflines[0],
+        "roofline_top2": rooflines,
+        "step_roofline": step_roofline(value / world, step_flops_pf, args.dtype),
+        "kernel_us": kernel_us,
+    }
+    if not args.no_fp32_line and args.dtype == "bf16":
+        out["fp32_parity_mode"] = fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo)
+    if not args.no_host_staged:
+        out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if ppo:
+            out["cpu_baseline"] = cpu_baseline_ppo(B, A, args.cpu_seconds)
+        else:
+            cb = cpu_baseline(B, T, A, args.cpu_seconds)
+            cb["host"] = host_cpu_info()
+            cb["single_thread"] = cpu_baseline(B, T, A, args.cpu_seconds_1t, threads=1, warmup=1)
+            out["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def select_kernels(eng, step, work, args):
+    """Average duration of every kernel over --steps untimed steps (all kernel timers armed at
+    once; each launch stamped by hipExtLaunchKernel events), and the two with algorithmic work
+    that take longest -> (per-kernel us table, [dominant, second])."""
+    names = [k for k in eng.kernel_names()]
+    for k in names:
+        eng.timer_start(k, args.steps)
+    for _ in range(args.steps):
+        step()
+    avg = {}
+    for k in names:
+        ms, n = eng.timer_read(k)
+        if n:
+            avg[k] = ms / n
+    table = {k: round(v * 1e3, 2) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}
+    if args.roofline_kernel:
+        top = [args.roofline_kernel]
+    else:
+        ranked = [k for k in sorted(avg, key=avg.get, reverse=True) if k in work and work[k][0]]
+        top = ranked[:2]
+    return table, top
+
+
+def timed_steps(eng, step, kernels, args, dist, dev):
+    """The timed region: --steps steps between barriers + device syncs; the given kernels' own
+    durations are stamped live (hipExtLaunchKernel events on their launch stream)."""
+    for k in kernels:
+        eng.timer_start(k, args.steps)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -515,65 +622,74 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    k_ms, k_n = eng.timer_read()
+    k_times = {k: eng.timer_read(k) for k in kernels}
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    met = eng.metrics.cpu().numpy()
-    if not np.all(np.isfinite(met)):
-        raise RuntimeError(f"non-finite metrics {met}")
+    return elapsed, k_times
 
-    frames = world * B * T * args.steps
-    value = frames / elapsed
-    ms_step = elapsed * 1e3 / args.steps
-    k_avg_ms = k_ms / max(k_n, 1)
-    # roofline of the dominant kernel: the bound is whichever of MFMA time and HBM time of its
-    # algorithmic work is larger; `achieved` is that work over the measured launch time
-    fpf, bpf, bpl = work[rk]
-    flops, nbytes = fpf * B * T, bpf * B * T + bpl
+
+def kernel_roofline(k, timing, work, frames, dtype, algo):
+    """Roofline of one kernel: the bound is whichever of MFMA time and HBM time of its
+    algorithmic work is larger; `achieved` = that work / the kernel's average duration."""
+    ms, n = timing
+    k_avg_ms = ms / max(n, 1)
+    fpf, bpf, bpl = work[k]
+    flops, nbytes = fpf * frames, bpf * frames + bpl
     t_s = k_avg_ms * 1e-3
-    if flops / (PEAK_TFLOPS[args.dtype] * 1e12) >= nbytes / (PEAK_HBM_GBS * 1e9):
-        bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[args.dtype]
+    if flops / (PEAK_TFLOPS[dtype] * 1e12) >= nbytes / (PEAK_HBM_GBS * 1e9):
+        bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[dtype]
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
-    traffic, tsrc = profiled_traffic(rk, args.dtype)
-    traffic_src = (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+WRITE_SIZE, "
-                   "bytes per launch)") if tsrc else None
-    metric = "learner env-frames/sec (IMPALA procgen T=20 B=64) at 1/2/4/8 MI355X"
-    workload = f"IMPALA procgen learner step, NatureCNN actor-critic, B={B}/GPU T={T} A={A}, " \
-               f"global B={B * world}"
-    if ppo:
-        metric = "PPO learner transitions/sec (procgen, NatureCNN, BASELINE config 4)"
-        workload = f"PPO learner step (clip 0.1), NatureCNN actor-critic, N={B} transitions/GPU"
-    out = {
-        "metric": metric,
-        "value": round(value, 1), "unit": "env-frames/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-        "data": "synthetic rollouts resident in HBM (obs u8 uniform, BASELINE.md §3); "
-                "random-init weights (reference layer_init_truncated, seed 0)",
-        "config": {"workload": workload,
-                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
-        "roofline": {"bound": bound, "kernel": rk, "achieved": round(achieved, 2),
-                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic": {"flops": flops, "bytes": nbytes},
-                     "avg_launch_us": round(k_avg_ms * 1e3, 2),
-                     "launches": k_n},
-        "step_tflops": round(STEP_FLOPS_PER_FRAME * value / world / 1e12, 2),
-    }
-    if probe:
-        out["kernel_probe_us"] = {k: round(v * 1e3, 2) for k, v in sorted(probe.items(), key=lambda kv: -kv[1])}
-    if not args.no_host_staged:
-        out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = (cpu_baseline_ppo(B, A, args.cpu_seconds) if ppo
-                               else cpu_baseline(B, T, A, args.cpu_seconds))
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    traffic, tsrc = profiled_traffic(k, dtype, algo=algo)
+    return {"bound": bound, "kernel": k, "achieved": round(achieved, 2), "peak": peak,
+            "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
+            "traffic_source": (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+"
+                               "WRITE_SIZE, bytes per launch)") if tsrc else None,
+            "algorithmic": {"flops": flops, "bytes": nbytes},
+            "avg_launch_us": round(k_avg_ms * 1e3, 2), "launches": n,
+            "timing": "hipExtLaunchKernel start/stop events (kernel begin/end stamps) over the "
+                      "timed steps"}
+
+
+def step_roofline(frames_per_s_per_gpu, flops_per_frame, dtype):
+    """the whole step against the dense MFMA peak (frames/s x algorithmic
+    FLOPs per frame, per GPU)."""
+    ach = frames_per_s_per_gpu * flops_per_frame / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype],
+            "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dtype], 4),
+            "flops_per_frame": flops_per_frame}
+
+
+def fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo):
+    """The same workload in fp32 parity mode (the reference's arithmetic), in the same run:
+    value, step roofline and the dominant kernel's roofline."""
+    from impala_amd.engine import Engine
+    from impala_amd.model import AtariPPOModel
+    m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+    e = Engine(m, batch_size=B, rollout_length=T, world_size=world, algo=args.algo)
+    m._train_engine = e
     if dist is not None:
-        dist.destroy_process_group()
+        dist.broadcast(m.flat, 0)
+        m.params_changed()
+    step = make_step(e, m)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    work = kernel_work(4)
+    table, top = select_kernels(e, step, work, argparse.Namespace(steps=args.steps,
+                                                                   roofline_kernel=None))
+    elapsed, k_times = timed_steps(e, step, top[:1], args, dist, dev)
+    value = world * B * T * args.steps / elapsed
+    out = {"dtype": "fp32", "value": round(value, 1), "unit": "env-frames/s",
+           "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+           "step_roofline": step_roofline(value / world, STEP_FLOPS_PER_FRAME if not ppo
+                                          else STEP_FLOPS_PER_FRAME_PPO, "fp32"),
+           "roofline": kernel_roofline(top[0], k_times[top[0]], work, B * T, "fp32", args.algo),
+           "kernel_us": table}
+    e.close()
+    return out
 
 
 if __name__ == "__main__":

@@ -37,6 +37,7 @@ EXPORTS = (
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
     "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
     "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
+    "impala_timer_read_kernel",
 )
 # every symbol declared in include/sac_hip.h
 SAC_EXPORTS = (
@@ -144,6 +145,7 @@ def _declare(lib):
     lib.impala_kernel_name.restype = C.c_char_p
     lib.impala_timer_start.argtypes = [_P, C.c_int, C.c_int]
     lib.impala_timer_read.argtypes = [_P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    lib.impala_timer_read_kernel.argtypes = [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     for name in EXPORTS:
         if name not in ("impala_last_error", "impala_param_count", "impala_kernel_name",
                         "impala_grad_bucket_offset", "impala_grad_bucket_offset_fc"):

@@ -6,6 +6,7 @@
 // buffer (bound with impala_bind_state), so the Python host exposes them as ordinary torch
 // tensors (state_dict, checkpoint, RCCL all-reduce) without copies.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdio>
@@ -133,8 +134,15 @@ struct impala_learner {
   int c1_fpw = 1, c1_wg = 1;  // conv1 wgrad: frames per workgroup, workgroups (= splits)
   int c12f_fpw = 0;           // conv1+conv2 forward frames per workgroup (0: N / CUs)
   float* vt_dbg = nullptr;    // impala_set_debug_vtrace: the step's V-trace outputs
-  int timer_kernel = -1, timer_cap = 0, timer_n = 0;
-  hipEvent_t* timer_ev = nullptr;
+  // live launch timer (impala_timer_*): per kernel id, event pairs handed to
+  // hipExtLaunchKernel, which stamps the kernel's own start / end (as rocprofv3 does)
+  struct KTimer {
+    hipEvent_t* ev = nullptr;
+    int cap = 0, n = 0;
+    bool armed = false;
+  };
+  KTimer timers[K_COUNT];
+  int timers_armed = 0, timer_last = -1;
   // hipGraph replay of whole steps: the launch sequence of a step is captured once per batch
   // address set (on a private capture stream) and replayed with one hipGraphLaunch
   struct GraphSlot {
@@ -177,17 +185,25 @@ inline int persist_grid(const impala_learner* h, long tiles) {
   return (int)(tiles < cap ? tiles : cap);
 }
 
-// live launch timer: an event pair around every launch of the armed kernel id (steps run
-// without graph replay while it is armed)
-inline void timer_begin(impala_learner* h, int kid, hipStream_t st) {
-  if (h->timer_kernel == kid && h->timer_n < h->timer_cap)
-    (void)hipEventRecord(h->timer_ev[2 * h->timer_n], st);
-}
-inline void timer_end(impala_learner* h, int kid, hipStream_t st) {
-  if (h->timer_kernel == kid && h->timer_n < h->timer_cap) {
-    (void)hipEventRecord(h->timer_ev[2 * h->timer_n + 1], st);
-    h->timer_n++;
+// Every learner kernel is launched through klaunch: hipExtLaunchKernel, with the start / stop
+// events of the live timer when kernel id `kid` is armed (the events then carry the kernel's
+// own begin / end timestamps, so the timed duration excludes the launch and inter-kernel gap,
+// as rocprofv3's kernel trace does).  Steps run without graph replay while a timer is armed.
+template <typename... KArgs, typename... Args>
+int klaunch(impala_learner* h, int kid, const char* name, void (*kernel)(KArgs...), dim3 grid,
+            dim3 block, hipStream_t st, Args... args) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (kid >= 0) {
+    auto& t = h->timers[kid];
+    if (t.armed && t.n < t.cap) {
+      e0 = t.ev[2 * t.n];
+      e1 = t.ev[2 * t.n + 1];
+      t.n++;
+    }
   }
+  hipExtLaunchKernelGGL(kernel, grid, block, 0, st, e0, e1, 0, args...);
+  CK_LAUNCH(name);
+  return 0;
 }
 }  // namespace
 
@@ -205,23 +221,18 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   const float* vv = h->vecs;
   if (h->fwd_fused) {  // conv1 + conv2 per frame (act1 consumed from LDS)
     const int fpw = h->c12f_fpw > 0 ? h->c12f_fpw : std::max(1, cdiv(n, h->n_cu));
-    timer_begin(h, K_CONV12_FWD, st);
-    conv12_fwd_s2d<T><<<cdiv(n, fpw), 256 * c12f_groups<T>(), 0, st>>>(
-        obs, sw + sh.w1, vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
-        (T*)h->act2, n, fpw);
-    timer_end(h, K_CONV12_FWD, st);
-    CK_LAUNCH("conv12_fwd");
+    if (int r = klaunch(h, K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>, dim3(cdiv(n, fpw)),
+                        dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1, vv + Vecs::b1,
+                        sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1, (T*)h->act2, n, fpw))
+      return r;
   } else {
-    timer_begin(h, K_CONV1_FWD, st);
-    conv1_fwd_s2d<T><<<min(n, h->n_cu * 4), 256, 0, st>>>(obs, sw + sh.w1, vv + Vecs::b1,
-                                                           (T*)h->act1, h->mask1, n);
-    timer_end(h, K_CONV1_FWD, st);
-    CK_LAUNCH("conv1_fwd");
+    if (int r = klaunch(h, K_CONV1_FWD, "conv1_fwd", conv1_fwd_s2d<T>, dim3(min(n, h->n_cu * 4)),
+                        dim3(256), st, obs, sw + sh.w1, vv + Vecs::b1, (T*)h->act1, h->mask1, n))
+      return r;
     Conv2Fwd<T> op{n * P2, sw + sh.w2, vv + Vecs::b2, (const T*)h->act1, (T*)h->act2};
-    timer_begin(h, K_CONV2_FWD, st);
-    gemm_tile<T, 64, 128, BK(64), 1, 4><<<persist_grid(h, (long)(cdiv((long)n * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
-    timer_end(h, K_CONV2_FWD, st);
-    CK_LAUNCH("conv2_fwd");
+    if (int r = klaunch(h, K_CONV2_FWD, "conv2_fwd", gemm_tile<T, 64, 128, BK(64), 1, 4, Conv2Fwd<T>>,
+                        dim3(persist_grid(h, cdiv((long)n * P2, 128))), dim3(256), st, op, 1))
+      return r;
   }
   {
     Conv3LnFwd<T> op{};
@@ -229,24 +240,22 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     op.out = (T*)h->act3; op.gam = vv + Vecs::lng; op.bet = vv + Vecs::lnb; op.y = (T*)h->y;
     op.stats = h->lnstat;
     op.frames_per_tile = 64 / P3;
-    timer_begin(h, K_CONV3_FWD, st);
-    gemm_tile<T, 64, 64, BK(96), 2, 2><<<persist_grid(h, (long)(cdiv((long)n * P3, 64)) * (1)), 256, 0, st>>>(op, 1);
-    timer_end(h, K_CONV3_FWD, st);
-    CK_LAUNCH("conv3_fwd");
+    if (int r = klaunch(h, K_CONV3_FWD, "conv3_fwd", gemm_tile<T, 64, 64, BK(96), 2, 2, Conv3LnFwd<T>>,
+                        dim3(persist_grid(h, cdiv((long)n * P3, 64))), dim3(256), st, op, 1))
+      return r;
   }
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
-    timer_begin(h, K_FC_FWD, st);
-    gemm_tile<T, 64, 32, BK(256), 2, 2><<<persist_grid(h, (long)cdiv(n, 32) * (HID / 64)), 256, 0, st>>>(op, HID / 64);
-    timer_end(h, K_FC_FWD, st);
-    CK_LAUNCH("fc_fwd");
+    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 64, 32, BK(256), 2, 2, FcFwd<T>>,
+                        dim3(persist_grid(h, (long)cdiv(n, 32) * (HID / 64))), dim3(256), st, op,
+                        HID / 64))
+      return r;
   }
   if (with_heads) {  // inference; in training the fused head kernel computes the heads
     HeadsFwd<T> op{n, sw + sh.wh, vv + Vecs::bh, (const T*)h->h, h->heads};
-    timer_begin(h, K_HEADS_FWD, st);
-    gemm_rc<T, 1, 1><<<dim3(cdiv(n, 64), 1), 256, 0, st>>>(op);
-    timer_end(h, K_HEADS_FWD, st);
-    CK_LAUNCH("heads_fwd");
+    if (int r = klaunch(h, K_HEADS_FWD, "heads_fwd", gemm_rc<T, 1, 1, HeadsFwd<T>>,
+                        dim3(cdiv(n, 64), 1), dim3(256), st, op))
+      return r;
   }
   return 0;
 }
@@ -256,11 +265,8 @@ enum { RS_CONV1 = 0, RS_CONV2 = 2, RS_CONV3 = 4, RS_FC = 7, RS_END = 11 };
 
 int reduce_segments(impala_learner* h, int s_lo, int s_hi, hipStream_t st, int fin) {
   const int n = h->red.wg_start[s_hi] - h->red.wg_start[s_lo];
-  timer_begin(h, K_REDUCE, st);
-  reduce_grads_kernel<<<n, 256, 0, st>>>(h->red, s_lo, fin);
-  timer_end(h, K_REDUCE, st);
-  CK_LAUNCH("reduce_grads");
-  return 0;
+  return klaunch(h, K_REDUCE, "reduce_grads", reduce_grads_kernel, dim3(n), dim3(256), st, h->red,
+                 s_lo, fin);
 }
 
 // part: -1 = the whole backward; 0 = through the conv3 weight gradient, ending with the
@@ -306,32 +312,29 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     // torch.clamp(ratio, 1 - clip, 1 + clip): the bounds are python floats cast to fp32
     ha.clip_lo = (float)(1.0 - (double)h->cfg.ppo_clip);
     ha.clip_hi = (float)(1.0 + (double)h->cfg.ppo_clip);
-    timer_begin(h, K_HEAD_STEP, st);
-    if (h->cfg.algo == IMPALA_ALGO_PPO)
-      head_step_kernel<T, true><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
-    else
-      head_step_kernel<T><<<dim3(h->n_loss_wg, HEAD_SPLIT), 256, 0, st>>>(ha);
-    timer_end(h, K_HEAD_STEP, st);
-    CK_LAUNCH("head_step");
+    const dim3 hg(h->n_loss_wg, HEAD_SPLIT);
+    if (int r = h->cfg.algo == IMPALA_ALGO_PPO
+                    ? klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, true>, hg, dim3(256), st, ha)
+                    : klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, false>, hg, dim3(256), st, ha))
+      return r;
   }
   if (int r = fork(1)) return r;  // dz ready
   {
     FcWgrad<T> op{};
     op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
-    timer_begin(h, K_FC_WGRAD, ss);
-    gemm_wg<T, 64, 256, 1, 4, 32, WG2><<<dim3(FLAT / 256, HID / 64, h->spfc.S), 256 * WG2, 0, ss>>>(
-        op, h->s_fc, h->s_bfc, h->spfc.mps);
-    timer_end(h, K_FC_WGRAD, ss);
-    CK_LAUNCH("fc_wgrad");
+    if (int r = klaunch(h, K_FC_WGRAD, "fc_wgrad", gemm_wg<T, 64, 256, 1, 4, 32, WG2, FcWgrad<T>>,
+                        dim3(FLAT / 256, HID / 64, h->spfc.S), dim3(256 * WG2), ss, op, h->s_fc,
+                        h->s_bfc, h->spfc.mps))
+      return r;
     if (h->red_mode == 1)
       if (int r = reduce_segments(h, RS_FC, RS_END, ss, 0)) return r;  // fc + heads slabs
   }
   {
     FcDgrad<T> op{N, sw + sh.wfc, (const T*)h->dz, h->dy};
-    timer_begin(h, K_FC_DGRAD, st);
-    gemm_tile<T, 64, 64, BK(128), 2, 2><<<persist_grid(h, (long)(cdiv(N, 64)) * (FLAT / 64)), 256, 0, st>>>(op, FLAT / 64);
-    timer_end(h, K_FC_DGRAD, st);
-    CK_LAUNCH("fc_dgrad");
+    if (int r = klaunch(h, K_FC_DGRAD, "fc_dgrad", gemm_tile<T, 64, 64, BK(128), 2, 2, FcDgrad<T>>,
+                        dim3(persist_grid(h, (long)cdiv(N, 64) * (FLAT / 64))), dim3(256), st, op,
+                        FLAT / 64))
+      return r;
   }
   if (part == 2) {  // bucket FC + heads complete
     if (h->use_side) {
@@ -342,38 +345,33 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   }
 stage_b:
   if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
-    timer_begin(h, K_LNC3_BWD, st);
-    lnc3_bwd<T><<<h->n_ln_wg, 256 * lnc3_groups<T>(), 0, st>>>(
-        h->dy, (const T*)h->act3, h->lnstat, h->vecs + Vecs::lng, sw + sh.w3,
-        (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, N, h->ln_fpw);
-    timer_end(h, K_LNC3_BWD, st);
-    CK_LAUNCH("ln_bwd_conv3_dgrad");
+    if (int r = klaunch(h, K_LNC3_BWD, "ln_bwd_conv3_dgrad", lnc3_bwd<T>, dim3(h->n_ln_wg),
+                        dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy, (const T*)h->act3,
+                        (const float*)h->lnstat, (const float*)(h->vecs + Vecs::lng), sw + sh.w3,
+                        (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, N, h->ln_fpw))
+      return r;
   } else {
-    timer_begin(h, K_LN_BWD, st);
-    ln_bwd_kernel<T><<<h->n_ln_wg, 256, 0, st>>>(h->dy, (const T*)h->act3, h->lnstat,
-                                                  h->vecs + Vecs::lng, (T*)h->dact3, h->s_ln, N,
-                                                  h->ln_fpw);
-    timer_end(h, K_LN_BWD, st);
-    CK_LAUNCH("ln_bwd");
+    if (int r = klaunch(h, K_LN_BWD, "ln_bwd", ln_bwd_kernel<T>, dim3(h->n_ln_wg), dim3(256), st,
+                        (const float*)h->dy, (const T*)h->act3, (const float*)h->lnstat,
+                        (const float*)(h->vecs + Vecs::lng), (T*)h->dact3, h->s_ln, N, h->ln_fpw))
+      return r;
   }
   if (int r = fork(2)) return r;  // dact3 ready
   {
     Conv3Wgrad<T> op{};
     op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
-    timer_begin(h, K_CONV3_WGRAD, ss);
-    gemm_wg<T, 64, 192, 1, 4, 32, WG4><<<dim3(K3 / 192, 1, h->sp3.S), 256 * WG4, 0, ss>>>(
-        op, h->s_w3, h->s_b3, h->sp3.mps);
-    timer_end(h, K_CONV3_WGRAD, ss);
-    CK_LAUNCH("conv3_wgrad");
+    if (int r = klaunch(h, K_CONV3_WGRAD, "conv3_wgrad", gemm_wg<T, 64, 192, 1, 4, 32, WG4, Conv3Wgrad<T>>,
+                        dim3(K3 / 192, 1, h->sp3.S), dim3(256 * WG4), ss, op, h->s_w3, h->s_b3,
+                        h->sp3.mps))
+      return r;
     if (h->red_mode == 1)
       if (int r = reduce_segments(h, RS_CONV3, RS_FC, ss, 0)) return r;  // conv3 + LayerNorm
   }
   if (!h->lnc3_fused) {
     Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
-    timer_begin(h, K_CONV3_DGRAD, st);
-    gemm_tile<T, 64, 128, BK(64), 1, 4><<<persist_grid(h, (long)(cdiv((long)N * P2, 128)) * (1)), 256, 0, st>>>(op, 1);
-    timer_end(h, K_CONV3_DGRAD, st);
-    CK_LAUNCH("conv3_dgrad");
+    if (int r = klaunch(h, K_CONV3_DGRAD, "conv3_dgrad", gemm_tile<T, 64, 128, BK(64), 1, 4, Conv3Dgrad<T>>,
+                        dim3(persist_grid(h, cdiv((long)N * P2, 128))), dim3(256), st, op, 1))
+      return r;
   }
   if (part == 0 || part == 3) {  // bucket 1 (or conv3 + LayerNorm) complete
     if (h->use_side) {
@@ -387,11 +385,10 @@ part1:
   {
     Conv2Wgrad<T> op{};
     op.M = N * P2; op.x = (const T*)h->dact2; op.in = (const T*)h->act1;
-    timer_begin(h, K_CONV2_WGRAD, ss);
-    gemm_wg<T, 64, 128, 1, 4, 32, WG4><<<dim3(K2 / 128, 1, h->sp2.S), 256 * WG4, 0, ss>>>(
-        op, h->s_w2, h->s_b2, h->sp2.mps);
-    timer_end(h, K_CONV2_WGRAD, ss);
-    CK_LAUNCH("conv2_wgrad");
+    if (int r = klaunch(h, K_CONV2_WGRAD, "conv2_wgrad", gemm_wg<T, 64, 128, 1, 4, 32, WG4, Conv2Wgrad<T>>,
+                        dim3(K2 / 128, 1, h->sp2.S), dim3(256 * WG4), ss, op, h->s_w2, h->s_b2,
+                        h->sp2.mps))
+      return r;
     if (h->red_mode == 1) {
       if (int r = reduce_segments(h, RS_CONV2, RS_CONV3, ss, 0)) return r;
     } else if (h->red_mode == 2 && part != 1 && part != 4) {
@@ -401,11 +398,11 @@ part1:
     }
   }
   // conv2 input gradient (ReLU-masked) + conv1 weight gradient, fused per frame
-  timer_begin(h, K_CONV12_BWD, st);
-  conv12_bwd_s2d<T><<<h->c1_wg, 256 * c12_groups<T>(), 0, st>>>(b->obs, sw + sh.w2, (const T*)h->dact2, h->mask1,
-                                              h->s_w1, h->s_b1, N, h->c1_fpw);
-  timer_end(h, K_CONV12_BWD, st);
-  CK_LAUNCH("conv2_dgrad_conv1_wgrad");
+  if (int r = klaunch(h, K_CONV12_BWD, "conv2_dgrad_conv1_wgrad", conv12_bwd_s2d<T>,
+                      dim3(h->c1_wg), dim3(256 * c12_groups<T>()), st, b->obs, sw + sh.w2,
+                      (const T*)h->dact2, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
+                      h->c1_fpw))
+    return r;
   // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were
   // reduced on the side stream right after their weight gradients ----
   if (part == 1 || part == 4) {
@@ -442,11 +439,8 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.inv_world = 1.f / (float)h->cfg.world_size;
   aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
   aa.cn = h->cn; aa.sh = h->sh;
-  timer_begin(h, K_ADAM, st);
-  adam_kernel<T><<<cdiv((long)(h->cn.total + 3) / 4, 256), 256, 0, st>>>(aa);
-  timer_end(h, K_ADAM, st);
-  CK_LAUNCH("adam");
-  return 0;
+  return klaunch(h, K_ADAM, "adam", adam_kernel<T>, dim3(cdiv((long)(h->cn.total + 3) / 4, 256)),
+                 dim3(256), st, aa);
 }
 
 template <typename T>
@@ -732,9 +726,9 @@ int impala_destroy(impala_learner* h) {
     (void)hipStreamDestroy(h->h2d_s[i]);
     if (h->h2d_join[i]) (void)hipEventDestroy(h->h2d_join[i]);
   }
-  if (h->timer_ev) {
-    for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
-    delete[] h->timer_ev;
+  for (auto& t : h->timers) {
+    for (int i = 0; i < 2 * t.cap; ++i) (void)hipEventDestroy(t.ev[i]);
+    delete[] t.ev;
   }
   if (h->cap) (void)hipStreamDestroy(h->cap);
   for (int i = 0; i < 4; ++i)
@@ -835,10 +829,9 @@ int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int 
 
 int enqueue_update(impala_learner* h, hipStream_t st) {
   if (h->cfg.world_size > 1) {
-    timer_begin(h, K_SUMSQ, st);
-    sumsq_kernel<<<h->n_red_wg, 256, 0, st>>>(h->grads, h->cn.total, h->sumsq_part);
-    timer_end(h, K_SUMSQ, st);
-    CK_LAUNCH("sumsq");
+    if (int r = klaunch(h, K_SUMSQ, "sumsq", sumsq_kernel, dim3(h->n_red_wg), dim3(256), st,
+                        (const float*)h->grads, (size_t)h->cn.total, h->sumsq_part))
+      return r;
   }
   return h->bf16 ? launch_adam<__bf16>(h, st) : launch_adam<float>(h, st);
 }
@@ -854,7 +847,7 @@ bool same_batch(const impala_batch& a, const impala_batch& b) {
 // (its events must be recorded per launch) or IMPALA_GRAPH=0 the launches go straight to `st`.
 template <class Body>
 int run_graphed(impala_learner* h, int kind, const impala_batch* b, hipStream_t st, Body&& body) {
-  if (!h->use_graph || h->timer_kernel >= 0) return body(st);
+  if (!h->use_graph || h->timers_armed > 0) return body(st);
   const impala_batch key = b ? *b : impala_batch{};
   for (auto& g : h->graphs)
     if (g.exec && g.kind == kind && same_batch(g.key, key)) {
@@ -1113,34 +1106,56 @@ int impala_timer_start(impala_learner* h, int kernel_id, int max_launches) {
   if (kernel_id < -1 || kernel_id >= K_COUNT || max_launches < 0)
     return fail(IMPALA_E_INVALID, "bad kernel id / capacity");
   CK(hipSetDevice(h->device));
-  if (max_launches > h->timer_cap) {
-    if (h->timer_ev) {
-      for (int i = 0; i < 2 * h->timer_cap; ++i) (void)hipEventDestroy(h->timer_ev[i]);
-      delete[] h->timer_ev;
-    }
-    h->timer_ev = new hipEvent_t[2 * max_launches];
-    for (int i = 0; i < 2 * max_launches; ++i) CK(hipEventCreate(&h->timer_ev[i]));
-    h->timer_cap = max_launches;
+  if (kernel_id < 0) {  // disarm every timer
+    for (auto& t : h->timers) t.armed = false;
+    h->timers_armed = 0;
+    return 0;
   }
-  h->timer_kernel = kernel_id;
-  h->timer_n = 0;
+  auto& t = h->timers[kernel_id];
+  if (max_launches > t.cap) {
+    for (int i = 0; i < 2 * t.cap; ++i) (void)hipEventDestroy(t.ev[i]);
+    delete[] t.ev;
+    t.ev = new hipEvent_t[2 * max_launches]();
+    t.cap = 0;
+    for (int i = 0; i < 2 * max_launches; ++i) CK(hipEventCreate(&t.ev[i]));
+    t.cap = max_launches;
+  }
+  if (!t.armed) h->timers_armed++;
+  t.armed = true;
+  t.n = 0;
+  h->timer_last = kernel_id;
+  return 0;
+}
+
+int impala_timer_read_kernel(impala_learner* h, int kernel_id, float* total_ms, int* launches) {
+  if (!h || !total_ms || !launches) return fail(IMPALA_E_INVALID, "null argument");
+  if (kernel_id < 0 || kernel_id >= K_COUNT) return fail(IMPALA_E_INVALID, "bad kernel id");
+  CK(hipSetDevice(h->device));
+  auto& t = h->timers[kernel_id];
+  float tot = 0.f;
+  for (int i = 0; i < t.n; ++i) {
+    CK(hipEventSynchronize(t.ev[2 * i + 1]));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *launches = t.n;
+  if (t.armed) h->timers_armed--;
+  t.armed = false;
+  t.n = 0;
   return 0;
 }
 
 int impala_timer_read(impala_learner* h, float* total_ms, int* launches) {
-  if (!h || !total_ms || !launches) return fail(IMPALA_E_INVALID, "null argument");
-  CK(hipSetDevice(h->device));
-  float tot = 0.f;
-  for (int i = 0; i < h->timer_n; ++i) {
-    CK(hipEventSynchronize(h->timer_ev[2 * i + 1]));
-    float ms = 0.f;
-    CK(hipEventElapsedTime(&ms, h->timer_ev[2 * i], h->timer_ev[2 * i + 1]));
-    tot += ms;
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (h->timer_last < 0) {
+    if (!total_ms || !launches) return fail(IMPALA_E_INVALID, "null argument");
+    *total_ms = 0.f;
+    *launches = 0;
+    return 0;
   }
-  *total_ms = tot;
-  *launches = h->timer_n;
-  h->timer_kernel = -1;
-  return 0;
+  return impala_timer_read_kernel(h, h->timer_last, total_ms, launches);
 }
 
 int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,

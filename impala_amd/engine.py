@@ -298,10 +298,17 @@ class Engine:
         kid = self.kernel_names().index(kernel)
         check(_lib.lib().impala_timer_start(self._h, kid, int(max_launches)), "impala_timer_start")
 
-    def timer_read(self):
-        """-> (summed launch duration in ms, launches) of the kernel armed by timer_start."""
+    def timer_read(self, kernel: Optional[str] = None):
+        """-> (summed kernel duration in ms, launches) of `kernel` (default: the kernel armed
+        last); disarms it.  Several kernels may be armed at once."""
         ms, n = C.c_float(), C.c_int()
-        check(_lib.lib().impala_timer_read(self._h, C.byref(ms), C.byref(n)), "impala_timer_read")
+        if kernel is None:
+            check(_lib.lib().impala_timer_read(self._h, C.byref(ms), C.byref(n)),
+                  "impala_timer_read")
+        else:
+            kid = self.kernel_names().index(kernel)
+            check(_lib.lib().impala_timer_read_kernel(self._h, kid, C.byref(ms), C.byref(n)),
+                  "impala_timer_read_kernel")
         return float(ms.value), int(n.value)
 
     def _updated(self):

@@ -199,13 +199,18 @@ int impala_stage_wait(impala_learner* h, int slot);
 int impala_slot_batch(impala_learner* h, int slot, void* stream, impala_batch* out);
 int impala_slot_release(impala_learner* h, int slot, void* stream);
 
-/* Live launch timer (bench / roofline): record a hipEvent pair around each of the next
- * `max_launches` launches of kernel `kernel_id` (see impala_kernel_name), on the stream it is
- * launched on; impala_timer_read() synchronises on them and returns the summed duration. */
+/* Live launch timer (bench / roofline): arm kernel `kernel_id` (see impala_kernel_name) for its
+ * next `max_launches` launches; each is launched with hipExtLaunchKernel and a start / stop
+ * event pair, which the runtime stamps with the kernel's own begin / end (the duration
+ * rocprofv3's kernel trace reports, without the launch gap).  Several kernels may be armed at
+ * once; kernel_id -1 disarms all.  impala_timer_read_kernel() synchronises on a kernel's events,
+ * returns the summed duration and launch count, and disarms it; impala_timer_read() does the
+ * same for the kernel armed last. */
 int impala_kernel_count(void);
 const char* impala_kernel_name(int kernel_id);
 int impala_timer_start(impala_learner* h, int kernel_id, int max_launches);
 int impala_timer_read(impala_learner* h, float* total_ms, int* launches);
+int impala_timer_read_kernel(impala_learner* h, int kernel_id, float* total_ms, int* launches);
 
 /* Standalone batched V-trace, [B][L] row-major, L <= 64 (test / reuse entry point). */
 int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,

@@ -203,8 +203,15 @@ def test_train_step_edge_shapes_fp32(B, T, A):
     e.train_step(*[_t(x, dev) for x in batch])
     got = e.metrics.cpu().numpy()
     names = ("loss", "entropy", "td", "pg", "kl", "ratio", "grad_norm")
-    np.testing.assert_allclose(got[:7], [met["train/" + k] for k in names], rtol=1e-5, atol=1e-7)
-    assert _rel_l2(m.flat_grad.cpu().numpy(), ref_cpu.flat_grads(ref)) < 1e-5
+    # against float64 at 1e-5; against the fp32 oracle at 1e-5 or twice the fp32 oracle's own
+    # error vs float64 where that is larger (grad_norm at B=1, T=2: ~5e-6)
+    p64, g64, met64 = ref_cpu.train_step_fp64(flat0, batch, A)
+    for i, k in enumerate(names):
+        x32, x64 = met["train/" + k], met64["train/" + k]
+        assert abs(got[i] - x64) <= 1e-5 * abs(x64) + 1e-7, (k, got[i], x64)
+        bound = max(1e-5, 2 * abs(x32 - x64) / abs(x64))
+        assert abs(got[i] - x32) <= bound * abs(x32) + 1e-7, (k, got[i], x32)
+    assert _rel_l2(m.flat_grad.cpu().numpy(), g64) < 1e-5
     np.testing.assert_allclose(m.flat.cpu().numpy(), ref_cpu.flat_params(ref), atol=1e-6)
 
 

@@ -77,14 +77,18 @@ def main(tag, src_root="gpurun_out", dst_root="profiles"):
         p = os.path.join(src, k)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, k))
-    dtype = "bf16"
+    dtype, algo = "bf16", "impala"
     bj = os.path.join(src, "bench_stats.json")
     if os.path.exists(bj):
         try:
-            dtype = json.loads(open(bj).read().strip().splitlines()[-1]).get("dtype", "bf16")
+            line = json.loads(open(bj).read().strip().splitlines()[-1])
+            dtype = line.get("dtype", "bf16")
+            algo = line.get("algo") or ("ppo" if "PPO" in line.get("metric", "") else
+                                        "sac" if "SAC" in line.get("metric", "") else "impala")
         except Exception:
             pass
-    json.dump({"tag": tag, "dtype": dtype, "total_kernel_ns": total_ns, "kernels": out}, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    json.dump({"tag": tag, "algo": algo, "dtype": dtype, "total_kernel_ns": total_ns, "kernels": out},
+              open(os.path.join(dst, "summary.json"), "w"), indent=1)
     with open(os.path.join(dst, "summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary `{tag}`\n\n`tools/profile.sh {tag}` = `rocprofv3 --kernel-trace --stats` "
                 "over `bench.py --steps 20 --warmup 3` (23 learner steps), then separate `--pmc FETCH_SIZE` "
