@@ -10,6 +10,9 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 #define WAVE 64
 #define DEV __device__ __forceinline__
@@ -87,6 +90,13 @@ DEV void store4(__bf16* p, const float v[4]) {
   bf16x4 o;
   o[0] = (__bf16)v[0]; o[1] = (__bf16)v[1]; o[2] = (__bf16)v[2]; o[3] = (__bf16)v[3];
   *reinterpret_cast<bf16x4*>(p) = o;
+}
+// two floats -> two bf16 (round to nearest even, as a (__bf16) cast) packed in one dword
+DEV int pack_bf16x2(float a, float b) {
+  bf16x2 v;
+  v[0] = (__bf16)a;
+  v[1] = (__bf16)b;
+  return __builtin_bit_cast(int, v);
 }
 DEV void load4(const float* p, float v[4]) {
   f32x4 x = *reinterpret_cast<const f32x4*>(p);

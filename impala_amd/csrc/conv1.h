@@ -27,6 +27,18 @@ template <> struct L<__bf16> { static constexpr int LDI = 56; };  // 112 B rows:
 template <> struct L<float> { static constexpr int LDI = 52; };
 }  // namespace c1
 
+// Fused forward image layout: row-major s2d rows of LDI_F elements, GRID*GRID + 2 rows (the
+// conv1 pixel tiles are grid rows oy with lane = ox in 0..15, ox = 15 a pad column, whose taps
+// reach row 256).  With grid-indexed tiles the 16 lanes of a B fragment read 16 consecutive
+// rows, so 96-byte rows (bf16, no padding) make every ds_read_b128 conflict-free
+// (tools/ldsbank.py: 1.00x, against 2.80x for pixel-indexed tiles on 112-byte rows).
+namespace c1 {
+template <typename T> struct LF;
+template <> struct LF<__bf16> { static constexpr int LDI = 48; };
+template <> struct LF<float> { static constexpr int LDI = 52; };
+constexpr int FROWS = GRID * GRID + 2;
+}  // namespace c1
+
 // canonical conv1 weight index (oc, ci, kh, kw) <-> s2d kernel order k'
 DEV int c1_kprime(int ci, int kh, int kw) {
   return ((kh >> 2) * 2 + (kw >> 2)) * c1::CH + ci * 16 + (kh & 3) * 4 + (kw & 3);
@@ -61,6 +73,37 @@ DEV void c1_stash_frame(T* img, int tid, const uint4 v[3]) {
     for (int q = 0; q < 4; ++q) {  // 4 bytes = d 0..3 of grid column X = 4*xq + q
       T* dst = img + (Y * c1::GRID + 4 * xq + q) * LDI + ci * 16 + b * 4;
       const uint32_t u = w[q];
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(dst) = f32x4{(float)(u & 255u), (float)((u >> 8) & 255u),
+                                               (float)((u >> 16) & 255u), (float)(u >> 24)};
+      } else {
+        bf16x4 o;
+        o[0] = (__bf16)(float)(u & 255u);
+        o[1] = (__bf16)(float)((u >> 8) & 255u);
+        o[2] = (__bf16)(float)((u >> 16) & 255u);
+        o[3] = (__bf16)(float)(u >> 24);
+        *reinterpret_cast<bf16x4*>(dst) = o;
+      }
+    }
+  }
+}
+
+// frame bytes -> row-major s2d image of LDI-element rows, the four 8-byte (bf16) / 16-byte
+// (fp32) pieces of a lane's vector written in the rotated order q = (j + xq) & 3: the 16 lanes
+// of a store group then hit 16 different bank pairs (tools/ldsbank.py stash_rot: 1.00x; the
+// plain order is 4x on 96-byte rows)
+template <typename T, int LDI>
+DEV void c1_stash_frame_rot(T* img, int tid, const uint4 v[3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int vi = tid + i * 256, ci = vi >> 8, yy = (vi & 255) >> 2, xq = vi & 3;
+    const int Y = yy >> 2, b = yy & 3;
+    const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = (j + xq) & 3;
+      const uint32_t u = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+      T* dst = img + (Y * c1::GRID + 4 * xq + q) * LDI + ci * 16 + b * 4;
       if constexpr (sizeof(T) == 4) {
         *reinterpret_cast<f32x4*>(dst) = f32x4{(float)(u & 255u), (float)((u >> 8) & 255u),
                                                (float)((u >> 16) & 255u), (float)(u >> 24)};
@@ -162,12 +205,17 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
-  constexpr int LDI = c1::L<T>::LDI;
+  constexpr int LDI = c1::LF<T>::LDI;
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int LDA1 = OC1 + VEC;                    // act1 tile row (elements)
   constexpr int NKS1 = K1 / KS, NKS2 = K2 / KS;
   constexpr int G = c12f_groups<T>();
-  constexpr int IMGSZ = c1::GRID * c1::GRID * LDI, GSZ = IMGSZ + c1::NPIX * LDA1;
+  // act1 tile rows: row y * A1P + x (y, x < 15).  The pitch of 22 rows per act1 row makes the
+  // conv2 B fragment reads (16 output pixels x 16-byte chunks) conflict-free (tools/ldsbank.py
+  // search_a1_pitch: 1.00x, against 1.67x for pitches 15 and 16)
+  constexpr int A1P = 22;
+  // (16 act1 rows: wave 3's pad tile oy = 15 writes row 15, read by nobody)
+  constexpr int IMGSZ = c1::FROWS * LDI, GSZ = IMGSZ + A1P * 16 * LDA1;
   constexpr bool W2REG = sizeof(T) == 2;             // bf16: conv2 weights in registers
   __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
@@ -177,6 +225,20 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
   const int kl = KPL * (lane >> 4);
   uint4 nv[3];
   if (f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, tid, nv);
+  // biases: 16-byte loads issued with the frame, ahead of the weights (waiting for the weights
+  // then covers them: loads retire in order)
+  float bb1[2][4], bb2[4];
+  {
+    const f32x4 u0 = *reinterpret_cast<const f32x4*>(b1 + 4 * (lane >> 4));
+    const f32x4 u1 = *reinterpret_cast<const f32x4*>(b1 + 16 + 4 * (lane >> 4));
+    const f32x4 u2 = *reinterpret_cast<const f32x4*>(b2 + 16 * wave + 4 * (lane >> 4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bb1[0][q] = u0[q];
+      bb1[1][q] = u1[q];
+      bb2[q] = u2[q];
+    }
+  }
   // Weights: every wave needs all of W1 and its 16 rows of W2 as MFMA fragments.  For bf16
   // both are staged once per workgroup through LDS with coalesced 16-byte loads (76 KB per
   // workgroup instead of 8 waves x 28 KB of fragment loads through the CU's L2 port).
@@ -223,13 +285,6 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
 #pragma unroll
       for (int ks = 0; ks < NKS1; ++ks) wa1[i][ks] = F::load(w1 + (16 * i + (lane & 15)) * K1 + ks * KS + kl);
   }
-  float bb1[2][4], bb2[4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bb1[i][q] = b1[16 * i + 4 * (lane >> 4) + q];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bb2[q] = b2[16 * wave + 4 * (lane >> 4) + q];
   // consume the bias loads here: waits for them placed inside the loop would (merged over the
   // back-edge) also stall every iteration on its in-flight frame prefetch
 #pragma unroll
@@ -237,75 +292,144 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
     asm volatile("" ::"v"(bb1[0][q]), "v"(bb1[1][q]), "v"(bb2[q]));
   }
   const int n_it = (f1 - f0 + G - 1) / G;
+  // conv1 pixel tiles of this wave: rows oy = wave, wave + 4, wave + 8, wave + 12 of the 15x15
+  // output (lane & 15 = ox; ox = 15 and wave 3's oy = 15 are pad lanes / a pad tile).  The tiles
+  // run in two pairs: the second pair's MFMAs are issued while the first pair's epilogue
+  // (scale, bias, ReLU, bf16 pack, mask bits, stores) runs on the VALU.
+  int c1base[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) c1base[t] = (min(wave + 4 * t, 14) * c1::GRID + (lane & 15)) * LDI;
+  auto c1_off = [&](int ks) {
+    const int k = ks * KS + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
+    return ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
+  };
+  // conv2: 3 pixel tiles (3 accumulators), B fragments one k-step ahead
+  int c2row[3];
+#pragma unroll
+  for (int pt = 0; pt < 3; ++pt) {
+    const int px = min(pt * 16 + (lane & 15), P2 - 1), oy = px / H2, ox = px - oy * H2;
+    c2row[pt] = ((ST2 * oy) * A1P + ST2 * ox) * LDA1 + kl;
+  }
+  auto c2_off = [&](int ks) {
+    const int k = ks * KS, tap = k >> 5, ci = k & 31;
+    return ((tap >> 2) * A1P + (tap & 3)) * LDA1 + ci;
+  };
+  // Branch-free epilogue stores: act1 and the mask go through buffer stores whose pad lanes
+  // carry an out-of-range offset (dropped by the hardware bounds check); pad lanes' LDS act1
+  // stores land in the tile's unused pitch columns / pad rows.
+  const __amdgpu_buffer_rsrc_t rs_act1 =
+      __builtin_amdgcn_make_buffer_rsrc(act1, 0, N * c1::NPIX * OC1 * (int)sizeof(T), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_mask =
+      __builtin_amdgcn_make_buffer_rsrc(mask, 0, N * c1::NPIX * 4, 0x00020000);
+  constexpr int OOB = 0x7ffffff0;
+  auto c1_mma = [&](f32x4 (&acc)[2][2], int t0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    V bq[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) bq[0][u] = *reinterpret_cast<const V*>(img + c1base[t0 + u] + c1_off(0));
+#pragma unroll
+    for (int ks = 0; ks < NKS1; ++ks) {
+      if (ks + 1 < NKS1) {
+        const int off = c1_off(ks + 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) bq[(ks + 1) & 1][u] = *reinterpret_cast<const V*>(img + c1base[t0 + u] + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        acc[u][0] = F::mma(wa1[0][ks], bq[ks & 1][u], acc[u][0]);
+        acc[u][1] = F::mma(wa1[1][ks], bq[ks & 1][u], acc[u][1]);
+      }
+    }
+  };
+  auto c1_epi = [&](const f32x4 (&acc)[2][2], int t0, int f) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int oy = wave + 4 * (t0 + u), ox = lane & 15;
+      const bool st = oy < H1 && ox < H1;
+      const int pc = oy * H1 + ox;               // act1 / mask pixel (15 x 15)
+      T* arow = a1s + (oy * A1P + ox) * LDA1;    // LDS act1 row (pad lanes: unused slots)
+      const int gofs = st ? (int)((((size_t)f * c1::NPIX + pc) * OC1) * sizeof(T)) : OOB;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float xv = acc[u][i][q] * (1.f / 255.f) + bb1[i][q];
+          v[q] = fmaxf(xv, 0.f);
+          // ReLU mask bit = (x > 0): the float's bits as a signed int are > 0 exactly then
+          // (one v_med3_i32)
+          bits |= (uint32_t)min(max((int)__float_as_uint(xv), 0), 1) << (16 * i + 4 * (lane >> 4) + q);
+        }
+        const int oc = 16 * i + 4 * (lane >> 4);
+        store4(arow + oc, v);
+        if constexpr (sizeof(T) == 2) {
+          const i32x2 d = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(d, rs_act1, gofs + oc * 2, 0, 0);
+        } else {
+          const i32x4 d = {(int)__float_as_uint(v[0]), (int)__float_as_uint(v[1]),
+                           (int)__float_as_uint(v[2]), (int)__float_as_uint(v[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(d, rs_act1, gofs + oc * 4, 0, 0);
+        }
+      }
+      bits = xor32_or(xor16_or(bits));
+      __builtin_amdgcn_raw_buffer_store_b32((int)bits, rs_mask,
+                                            st && lane < 16 ? (int)(((size_t)f * c1::NPIX + pc) * 4) : OOB,
+                                            0, 0);
+    }
+  };
+  // the group's first frame goes into the image now (the weight staging area is free), and the
+  // second is fetched; every later frame is staged during the previous frame's conv2
+  if (f0 + grp < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
+  if (f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, tid, nv);
+  __syncthreads();
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
     const bool active = f < f1;
-    __syncthreads();  // the previous frame's readers of img / a1s are done
-    if (active) c1_stash_frame<T>(img, tid, nv);
-    __syncthreads();
-    if (f + G < f1) c1_load_frame<T>(x + (size_t)(f + G) * IMG, tid, nv);
     if (active) {
       // ---- conv1 -> act1 (HBM + LDS) and its ReLU bit mask ----
-      // (unrolled: a loop back-edge here makes the compiler wait for the frame prefetch)
-#pragma unroll
-      for (int tj = 0; tj < 4; ++tj) {
-        const int tile = wave + 4 * tj;
-        if (tile >= 15) break;
-        const int p = min(tile * 16 + (lane & 15), c1::NPIX - 1);
-        const int base = c1_row(p, 0) * LDI;
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int ks = 0; ks < NKS1; ++ks) {
-          const int k = ks * KS + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
-          const int off = ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
-          const V b = *reinterpret_cast<const V*>(img + base + off);
-          acc[0] = F::mma(wa1[0][ks], b, acc[0]);
-          acc[1] = F::mma(wa1[1][ks], b, acc[1]);
-        }
-        const int pc = tile * 16 + (lane & 15);
-        uint32_t bits = 0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v[q] = fmaxf(acc[i][q] * (1.f / 255.f) + bb1[i][q], 0.f);
-            bits |= (v[q] > 0.f ? 1u : 0u) << (16 * i + 4 * (lane >> 4) + q);
-          }
-          if (pc < c1::NPIX) {
-            const int oc = 16 * i + 4 * (lane >> 4);
-            store4(act1 + ((size_t)f * c1::NPIX + pc) * OC1 + oc, v);
-            store4(a1s + pc * LDA1 + oc, v);
-          }
-        }
-        bits = xor32_or(xor16_or(bits));
-        if (pc < c1::NPIX && lane < 16) mask[(size_t)f * c1::NPIX + pc] = bits;
-      }
+      f32x4 accA[2][2], accB[2][2];
+      c1_mma(accA, 0);
+      c1_mma(accB, 2);
+      c1_epi(accA, 0, f);
+      c1_epi(accB, 2, f);
     }
-    __syncthreads();
+    __syncthreads();  // the act1 tile is complete; the image is free
     if (active) {
-      // ---- conv2 from the LDS act1 tile -> act2 ----
+      // ---- conv2 from the LDS act1 tile -> act2, and the next frame into the image ----
+      f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                      f32x4{0.f, 0.f, 0.f, 0.f}};
+      V bq[2][3];
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) bq[0][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + c2_off(0));
+#pragma unroll
+      for (int ks = 0; ks < NKS2; ++ks) {
+        if (ks + 1 < NKS2) {
+          const int off = c2_off(ks + 1);
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) bq[(ks + 1) & 1][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + off);
+        }
+        V a;
+        if constexpr (W2REG) a = wa2[ks];
+        else a = F::load(w2row + ks * KS);
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma(a, bq[ks & 1][pt], acc[pt]);
+      }
+      if (f + G < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
+      if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt) {
-        const int px = min(pt * 16 + (lane & 15), P2 - 1), oy = px / H2, ox = px - oy * H2;
-        const T* brow = a1s + ((ST2 * oy) * H1 + ST2 * ox) * LDA1 + kl;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < NKS2; ++ks) {
-          const int k = ks * KS, tap = k >> 5, ci = k & 31;
-          const V b = *reinterpret_cast<const V*>(brow + ((tap >> 2) * H1 + (tap & 3)) * LDA1 + ci);
-          if constexpr (W2REG) acc = F::mma(wa2[ks], b, acc);
-          else acc = F::mma(F::load(w2row + ks * KS), b, acc);
-        }
         const int pc = pt * 16 + (lane & 15);
         if (pc < P2) {
           float v[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[q] + bb2[q], 0.f);
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[pt][q] + bb2[q], 0.f);
           store4(act2 + ((size_t)f * P2 + pc) * OC2 + 16 * wave + 4 * (lane >> 4), v);
         }
       }
     }
+    __syncthreads();  // the image holds the next frame; the act1 tile is free
   }
 }
 

@@ -360,8 +360,10 @@ stage_b:
   {
     Conv3Wgrad<T> op{};
     op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
-    if (int r = klaunch(h, K_CONV3_WGRAD, "conv3_wgrad", gemm_wg<T, 64, 192, 1, 4, 32, WG4, Conv3Wgrad<T>>,
-                        dim3(K3 / 192, 1, h->sp3.S), dim3(256 * WG4), ss, op, h->s_w3, h->s_b3,
+    // 64 x 64 tiles (9 column tiles x ~28 splits): 4.1 MB of partial slabs instead of 9.4 MB
+    // for 64 x 192 tiles x 64 splits, and 9.1 vs 9.8 us (profiles/r02b)
+    if (int r = klaunch(h, K_CONV3_WGRAD, "conv3_wgrad", gemm_wg<T, 64, 64, 2, 2, 32, WG4, Conv3Wgrad<T>>,
+                        dim3(K3 / 64, 1, h->sp3.S), dim3(256 * WG4), ss, op, h->s_w3, h->s_b3,
                         h->sp3.mps))
       return r;
     if (h->red_mode == 1)
@@ -567,7 +569,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
                       HID + HEADS * HID + HEADS) / 4 / 16;
   h->sph.S = h->n_loss_wg;  // heads weight-gradient partials: one slab per head workgroup
   h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), 96);
-  h->sp3 = plan_split((long)N * P3, K3 / 192, 192);
+  h->sp3 = plan_split((long)N * P3, K3 / 64, 256);
   h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
   h->c1_fpw = std::max(1, cdiv(N, h->n_cu));
   if (const char* e = std::getenv("IMPALA_C1_FPW")) h->c1_fpw = std::max(1, std::atoi(e));
