@@ -262,14 +262,18 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
 
 // Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split
 // blockIdx.z.  X is a row-major [M][x_ld] matrix (the channels-last output gradient); Y is a
-// gather (im2col of the layer input) returning 16-byte runs along c.  Each BM-row chunk of both
-// is staged row-major into LDS with 16-byte stores and the MFMA fragments are read along m
-// with the hardware transpose read (bf16).  The next chunk is loaded into registers while the
-// current one is multiplied (double-buffered LDS, one barrier per chunk), and a workgroup holds
-// G independent 4-wave groups on interleaved chunks (more loads in flight per CU without more
-// partial slabs); the groups' accumulators are summed in a fixed order at the end.
-// Output: fp32 partial slab [split][R][C] (+ per-split bias sums).
-template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op>
+// gather (im2col of the layer input) given as element offsets y_roff(m) + y_coff(c) of 16-byte
+// runs along c.  Each BM-row chunk of both is staged row-major into LDS with 16-byte stores and
+// the MFMA fragments are read along m with the hardware transpose read (bf16).  A workgroup
+// holds G independent 4-wave groups on interleaved chunks, and every group keeps PD chunks in
+// flight in a register ring (the chunk it multiplies was issued PD chunks earlier): the MFMA
+// work per chunk is a few hundred cycles against a ~2 us loaded memory round trip, so the
+// kernel is bound by how many chunk loads are in flight per CU.  All loads are buffer loads
+// issued unconditionally: rows past the split's end and chunks past the group's last one carry
+// an out-of-range offset and read as zero without touching memory (no branch around a load,
+// so the compiler's counted vmcnt waits stay exact).  The groups' accumulators are summed in
+// a fixed order at the end.  Output: fp32 partial slab [split][R][C] (+ per-split bias sums).
+template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op, int PD = 2>
 __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restrict__ slab,
                                                    float* __restrict__ slab_bias,
                                                    int m_per_split) {
@@ -282,13 +286,19 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
   constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per buffer
   constexpr int NXV = BM * (BR / VEC);
   constexpr int NX = (NXV + 255) / 256;
-  // Y staging: thread t owns m-row (t % BM) of the chunk and column vectors t/BM + i*(256/BM),
-  // so the im2col row context (n, oy, ox) is derived once per chunk, not per vector.
-  constexpr int YCS = 256 / BM, NY = (BC / VEC + YCS - 1) / YCS;
+  // Y staging: vector v = t + i*256 of a chunk is row v / (BC/VEC), column vector v % (BC/VEC),
+  // so consecutive lanes read one contiguous run of a row (the BC columns of a tile are one
+  // contiguous run of the im2col row: 4 taps x 32 channels of conv2, one tap of conv3, an FC
+  // row slice).  A wave instruction then touches a few whole 128-B lines instead of one 32-B
+  // piece of a line per row: the TA's per-line rate, not bytes, bounded the row-per-lane form
+  // (24 B/cycle per CU, profiles/r02c).
+  constexpr int YV = BC / VEC, NYV = BM * YV, NY = (NYV + 255) / 256;
+  constexpr int OOB = 0x7ffffff0;  // buffer offset past any extent: the load returns zero
   static_assert(256 % BM == 0, "Y staging");
   static_assert(WR * WC == 4, "4 waves per group");
   static_assert(TRW >= 1 && TCW >= 1 && BR % 16 == 0 && BC % 16 == 0, "tile");
   static_assert(BM % F::KSTEP == 0, "chunk");
+  static_assert(PD >= 1, "prefetch depth");
   static_assert((size_t)STAGE * 2 * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
                 "LDS reuse for the group reduction");
   __shared__ __attribute__((aligned(16))) T smem[STAGE * 2 * G];
@@ -302,80 +312,105 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
   const int m_end = min(op.M, m_beg + m_per_split);
   const int wr = wave / WC, wc = wave % WC;
   const bool do_bias = slab_bias != nullptr && bx == 0;
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(op.x), 0, op.M * op.x_ld * (int)sizeof(T), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(op.ybase()), 0, op.y_bytes(), 0x00020000);
   f32x4 acc[TRW][TCW];
 #pragma unroll
   for (int i = 0; i < TRW; ++i)
 #pragma unroll
     for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bias_acc = 0.f;
-  V rx[NX], ry[NY];
-  auto fetch = [&](int m0) {
+  // per-thread constant parts of the staging addresses (bytes)
+  int xcol[NX], ycol[NY];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int e = min(tid + i * 256, NXV - 1);
+    xcol[i] = (r0 + (e % (BR / VEC)) * VEC) * (int)sizeof(T);
+  }
+#pragma unroll
+  for (int i = 0; i < NY; ++i) ycol[i] = op.y_coff(c0 + ((tid + i * 256) % YV) * VEC) * (int)sizeof(T);
+  V rx[PD][NX], ry[PD][NY];
+  // chunk `it` of this group -> ring slot d.  Offsets are computed for a clamped row and
+  // replaced by OOB with a select afterwards (unsigned: OOB + a column offset stays out of
+  // range), so no load sits behind a branch.
+  auto fetch = [&](int d, int it) {
+    const int m0 = m_beg + (it * G + grp) * BM;
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
-      const int e = tid + i * 256, mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
-      rx[i] = (e < NXV && m0 + mm < m_end)
-                  ? *reinterpret_cast<const V*>(op.x + (size_t)(m0 + mm) * op.x_ld + r0 + rr)
-                  : F::zero();
+      const int m = m0 + (tid + i * 256) / (BR / VEC);
+      const uint32_t off = (uint32_t)(min(m, m_end - 1) * op.x_ld * (int)sizeof(T) + xcol[i]);
+      rx[d][i] = __builtin_bit_cast(
+          V, __builtin_amdgcn_raw_buffer_load_b128(rs_x, (int)(m < m_end ? off : (uint32_t)OOB), 0, 0));
     }
-    {
-      const int mm = tid % BM, cv0 = tid / BM;
-      const bool mok = m0 + mm < m_end;
-      const auto yc = op.y_row(mok ? m0 + mm : m_beg);
 #pragma unroll
-      for (int i = 0; i < NY; ++i) {
-        const int cv = cv0 + i * YCS, cc = cv * VEC;
-        ry[i] = (cv < BC / VEC && mok && c0 + cc < op.C) ? op.load_y(yc, c0 + cc) : F::zero();
-      }
+    for (int i = 0; i < NY; ++i) {
+      const int m = m0 + min(tid + i * 256, NYV - 1) / YV;
+      const uint32_t yr = m < m_end ? (uint32_t)(op.y_roff(min(m, m_end - 1)) * (int)sizeof(T)) : (uint32_t)OOB;
+      ry[d][i] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs_y, (int)(yr + (uint32_t)ycol[i]), 0, 0));
     }
   };
-  auto stash = [&](T* Xs) {
+  auto stash = [&](int d, T* Xs) {
     T* Ys = Xs + BM * LDX;
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       const int e = tid + i * 256, mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
-      if (e < NXV) *reinterpret_cast<V*>(Xs + mm * LDX + rr) = rx[i];
+      if (e < NXV) *reinterpret_cast<V*>(Xs + mm * LDX + rr) = rx[d][i];
     }
-    {
-      const int mm = tid % BM, cv0 = tid / BM;
 #pragma unroll
-      for (int i = 0; i < NY; ++i) {
-        const int cv = cv0 + i * YCS;
-        if (cv < BC / VEC) *reinterpret_cast<V*>(Ys + mm * LDY + cv * VEC) = ry[i];
-      }
+    for (int i = 0; i < NY; ++i) {
+      const int v = tid + i * 256;
+      if (v < NYV) *reinterpret_cast<V*>(Ys + (v / YV) * LDY + (v % YV) * VEC) = ry[d][i];
     }
   };
   const int n_it = (m_end - m_beg + BM * G - 1) / (BM * G);
-  if (n_it > 0) fetch(m_beg + grp * BM);
-  for (int it = 0; it < n_it; ++it) {
-    const int m0 = m_beg + (it * G + grp) * BM;
-    const bool active = m0 < m_end;
-    T* Xs = smem + (grp * 2 + (it & 1)) * STAGE;
-    const T* Ys = Xs + BM * LDX;
-    if (active) stash(Xs);
-    __syncthreads();
-    if (it + 1 < n_it) fetch(m0 + G * BM);  // in flight under this chunk's MFMAs
-    if (active) {
-      if (do_bias) {  // (256/BR) row groups x BR channels; summed across groups at the end
-        constexpr int RG = 256 / BR;
-        const int rch = tid % BR, rg = tid / BR;
-        float s0 = 0.f;
+  // sched_barrier(0) keeps the ring slots' loads in issue order (the scheduler otherwise
+  // interleaves the prologue's fetches, and the first stash then waits for all of them)
 #pragma unroll
-        for (int mm = rg; mm < BM; mm += RG) s0 += (float)Xs[mm * LDX + rch];
-        bias_acc += s0;
-      }
+  for (int d = 0; d < PD; ++d) {
+    fetch(d, d);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int it0 = 0; it0 < n_it; it0 += PD) {
 #pragma unroll
-      for (int kk = 0; kk < BM; kk += F::KSTEP) {
-        V a[TRW], b[TCW];
+    for (int d = 0; d < PD; ++d) {
+      const int it = it0 + d;
+      // no early exit: the trip count is padded to a multiple of PD and chunks past n_it are
+      // all-OOB (zero, no memory traffic, MFMAs skipped).  An exit from the middle of the
+      // unrolled ring is funnelled through the loop latch by the CFG structurizer, which merges
+      // a rotated ring state into the loop header and forces vmcnt(0) at every stash.
+      const int m0 = m_beg + (it * G + grp) * BM;
+      const bool active = m0 < m_end;
+      T* Xs = smem + (grp * 2 + (it & 1)) * STAGE;
+      const T* Ys = Xs + BM * LDX;
+      stash(d, Xs);
+      __syncthreads();
+      fetch(d, it + PD);  // in flight under the next PD - 1 chunks
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) {
+        if (do_bias) {  // (256/BR) row groups x BR channels; summed across groups at the end
+          constexpr int RG = 256 / BR;
+          const int rch = tid % BR, rg = tid / BR;
+          float s0 = 0.f;
 #pragma unroll
-        for (int i = 0; i < TRW; ++i)
-          a[i] = lds_frag_k(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
+          for (int mm = rg; mm < BM; mm += RG) s0 += (float)Xs[mm * LDX + rch];
+          bias_acc += s0;
+        }
 #pragma unroll
-        for (int j = 0; j < TCW; ++j)
-          b[j] = lds_frag_k(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
+        for (int kk = 0; kk < BM; kk += F::KSTEP) {
+          V a[TRW], b[TCW];
 #pragma unroll
-        for (int i = 0; i < TRW; ++i)
+          for (int i = 0; i < TRW; ++i)
+            a[i] = lds_frag_k(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
 #pragma unroll
-          for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+          for (int j = 0; j < TCW; ++j)
+            b[j] = lds_frag_k(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
+#pragma unroll
+          for (int i = 0; i < TRW; ++i)
+#pragma unroll
+            for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+        }
       }
     }
   }

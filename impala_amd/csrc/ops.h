@@ -214,10 +214,11 @@ template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
   const T* x;  // dz
   int x_ld = HID;
   const T* y;
-  DEV const T* y_row(int m) const { return y + (size_t)m * FLAT; }
-  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
-    return *reinterpret_cast<const typename Frag<T>::vec*>(row + c);
-  }
+  // Y gather as element offsets from y (buffer loads: out-of-range rows read as zero)
+  DEV int y_roff(int m) const { return m * FLAT; }
+  DEV int y_coff(int c) const { return c; }
+  DEV int y_bytes() const { return M * FLAT * (int)sizeof(T); }
+  DEV const T* ybase() const { return y; }
 };
 template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3+kw)*64 + ci
   static constexpr int R = OC3, C = K3;
@@ -226,14 +227,16 @@ template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3
   const T* x;  // dact3
   int x_ld = OC3;
   const T* in;  // act2
-  DEV const T* y_row(int m) const {  // top-left input pixel of the 3x3 patch
+  DEV int y_roff(int m) const {  // top-left input pixel of the 3x3 patch
     const int n = m / P3, p = m - n * P3, oy = p / H3, ox = p - oy * H3;
-    return in + ((size_t)(n * H2 + oy) * H2 + ox) * OC2;
+    return ((n * H2 + oy) * H2 + ox) * OC2;
   }
-  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
+  DEV int y_coff(int c) const {
     const int tap = c >> 6, ci = c & 63, kh = tap / 3, kw = tap - kh * 3;
-    return *reinterpret_cast<const typename Frag<T>::vec*>(row + (kh * H2 + kw) * OC2 + ci);
+    return (kh * H2 + kw) * OC2 + ci;
   }
+  DEV int y_bytes() const { return (M / P3) * (H2 * H2 * OC2) * (int)sizeof(T); }
+  DEV const T* ybase() const { return in; }
 };
 template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4+kw)*32 + ci
   static constexpr int R = OC2, C = K2;
@@ -242,12 +245,14 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
   const T* x;  // dact2
   int x_ld = OC2;
   const T* in;  // act1
-  DEV const T* y_row(int m) const {
+  DEV int y_roff(int m) const {
     const int n = m / P2, p = m - n * P2, oy = p / H2, ox = p - oy * H2;
-    return in + ((size_t)(n * H1 + ST2 * oy) * H1 + ST2 * ox) * OC1;
+    return ((n * H1 + ST2 * oy) * H1 + ST2 * ox) * OC1;
   }
-  DEV typename Frag<T>::vec load_y(const T* row, int c) const {
+  DEV int y_coff(int c) const {
     const int tap = c >> 5, ci = c & 31, kh = tap >> 2, kw = tap & 3;
-    return *reinterpret_cast<const typename Frag<T>::vec*>(row + (kh * H1 + kw) * OC1 + ci);
+    return (kh * H1 + kw) * OC1 + ci;
   }
+  DEV int y_bytes() const { return (M / P2) * (H1 * H1 * OC1) * (int)sizeof(T); }
+  DEV const T* ybase() const { return in; }
 };
