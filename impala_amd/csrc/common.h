@@ -152,6 +152,12 @@ DEV float row16_sum(float v) {
   v += dppf<DPP_ROW_MIRROR>(v);
   return v;
 }
+DEV float row16_max(float v) {
+  v = fmaxf(v, dppf<DPP_QP_1032>(v));
+  v = fmaxf(v, dppf<DPP_QP_2301>(v));
+  v = fmaxf(v, dppf<DPP_ROW_HALF_MIRROR>(v));
+  return fmaxf(v, dppf<DPP_ROW_MIRROR>(v));
+}
 DEV float wave_sum(float v) { return xor32_sum(xor16_sum(row16_sum(v))); }
 DEV float wave_max(float v) {
   v = fmaxf(v, dppf<DPP_QP_1032>(v));
@@ -175,4 +181,10 @@ DEV float gelu_grad(float z) {
   const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752440f));
   const float pdf = 0.39894228040143267794f * expf(-0.5f * z * z);
   return cdf + z * pdf;
+}
+// GELU and its derivative from one erf (the FC forward epilogue keeps gelu'(z) for the backward)
+DEV void gelu_fwd_grad(float z, float& h, float& g) {
+  const float e = erff(z * 0.70710678118654752440f);
+  h = 0.5f * z * (1.f + e);
+  g = 0.5f * (1.f + e) + z * (0.39894228040143267794f * expf(-0.5f * z * z));
 }

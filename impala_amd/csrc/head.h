@@ -3,9 +3,13 @@
 // heads' weight-gradient partial -- one workgroup per group of whole trajectories.
 //
 //   phase 1  stage h[F][256] of the group's F frames in LDS; heads = Wh . h + bh (MFMA)
-//   phase 2  wave 0: one lane per (trajectory, t); V-trace as a wavefront shuffle scan
-//            (seg_rev_scan); d loss / d logits, d loss / d value -> dH[F][32] in LDS
-//   phase 3  dz[f][j] = gelu'(z[f][j]) * sum_o' dH[f][o'] Wh[o'][j]        (MFMA, K = 32)
+//   phase 2a all 4 waves, one 16-lane row per frame, one lane per action: log-softmax of the
+//            policy and behaviour logits, entropy, KL, log pi(a), rho (row reductions by DPP)
+//   phase 2b wave 0: one lane per (trajectory, t); V-trace as a wavefront shuffle scan
+//            (seg_rev_scan) -> d loss / d value and the per-frame policy-gradient coefficient
+//   phase 2c all 4 waves, frame x action lanes again: d loss / d logits -> dH[F][32] in LDS
+//   phase 3  dz[f][j] = gelu'(z[f][j]) * sum_o' dH[f][o'] Wh[o'][j]        (MFMA, K = 32;
+//            gelu'(z) comes precomputed from the FC forward epilogue)
 //   phase 4  dWh[o'][j] += sum_f dH[f][o'] h[f][j]  (MFMA over frames, LDS transpose reads)
 //            -> fp32 partial slab per workgroup (+ bias sums), reduced by reduce_grads
 //
@@ -17,13 +21,15 @@
 
 using namespace net;
 
-DEV float fast_exp(float x) { return exp2f(x * 1.4426950408889634f); }
-DEV float fast_log(float x) { return log2f(x) * 0.69314718055994531f; }
+// the hardware exp2 / log2 (v_exp_f32 / v_log_f32, ~1 ulp): exp2f / log2f add a denormal
+// range reduction around them that costs 4 instructions per call and changes nothing here
+DEV float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+DEV float fast_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 
 struct HeadArgs {
   // phase 1 inputs
   const void* h;      // T [N][256]
-  const float* z;     // [N][256] pre-GELU
+  const float* zg;    // [N][256] gelu'(pre-GELU), from the FC forward
   const void* wh;     // T [16][256]
   const void* wht;    // T [256][32]
   const float* bh;    // [16]
@@ -61,6 +67,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   __shared__ float lg_s[64][HEADS + 1];
   __shared__ __attribute__((aligned(16))) float zs[64 * (HEAD_JC + 4)];  // z slice (phase 3)
   __shared__ float bred[4][HEADS];
+  __shared__ float fsc[5][64];  // per frame: rho, entropy, KL, log pi(a), dH coefficient kappa
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T_ = a.T, S = a.S;
   const int traj0 = blockIdx.x * a.TPW;
@@ -76,16 +83,24 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   const bool valid = wave == 0 && tl < ntraj && t < T_;
   const bool inL = valid && t < L;
   const int fl = valid ? tl * T_ + t : 0;
-  float mu[MAX_A], r = 0.f, g = 0.f;
-  int act = 0;
+  float r = 0.f, g = 0.f;
   if (wave == 0) {
     const size_t n = f0 + fl;
-    const float* mrow = a.mu + n * A;
-#pragma unroll
-    for (int j = 0; j < MAX_A; ++j) mu[j] = mrow[j < A ? j : A - 1];
-    act = (int)a.act[n];
     r = a.rew[n];
     if constexpr (!PPO) g = a.disc[n];
+  }
+  // phase 2a/2c lanes: frame f = 16 p + 4 wave + (lane >> 4) in pass p, action ja = lane & 15.
+  // The behaviour logits and actions of every pass are loaded now (clamped addresses, values
+  // selected later) so their latency overlaps phase 1.
+  constexpr int NPASS = 4;
+  const int ja = lane & 15;
+  float muv[NPASS];
+  int actv[NPASS];
+#pragma unroll
+  for (int p = 0; p < NPASS; ++p) {
+    const size_t n = f0 + min(16 * p + 4 * wave + (lane >> 4), nf - 1);
+    muv[p] = a.mu[n * A + min(ja, A - 1)];
+    actv[p] = (int)a.act[n];
   }
   // ---- every global load of the kernel is issued here, in one round trip: h rows, this
   // workgroup's z slice, the heads weights (both orientations) and bias ----
@@ -102,7 +117,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
 #pragma unroll
   for (int i = 0; i < NZV; ++i) {
     const int e = tid + i * 256, f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
-    zv[i] = f < nf ? *reinterpret_cast<const f32x4*>(a.z + (f0 + f) * HID + jw + c)
+    zv[i] = f < nf ? *reinterpret_cast<const f32x4*>(a.zg + (f0 + f) * HID + jw + c)
                    : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   V whf[NKH], wtf[NKT];
@@ -145,51 +160,51 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     for (int e = tid; e < nf * HEADS; e += 256)
       a.heads_out[(f0 + e / HEADS) * HEADS + e % HEADS] = lg_s[e / HEADS][e % HEADS];
   }
-  // ---- phase 2: loss head on wave 0 (one lane per (trajectory, t)) ----
+  // ---- phase 2a: per-frame log-softmax statistics, frame x action lanes ----
+  const float ke = a.ent_coef * (1.f / (float)(a.B * T_));  // d(-ent_coef * mean H) / d H per frame
+  float pv[NPASS], lpv[NPASS], Hv[NPASS];
+#pragma unroll
+  for (int p = 0; p < NPASS; ++p) {
+    if (16 * p >= nf) continue;  // workgroup-uniform
+    const int f = 16 * p + 4 * wave + (lane >> 4);
+    const bool on = ja < A;
+    const float lgv = on ? lg_s[f][ja] : -INFINITY;
+    const float mv = on ? muv[p] : -INFINITY;
+    const float m = row16_max(lgv), mm = row16_max(mv);
+    const float e = on ? fast_exp(lgv - m) : 0.f, em = on ? fast_exp(mv - mm) : 0.f;
+    const float s = row16_sum(e), sm = row16_sum(em);
+    const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm);
+    const float logp = on ? lgv - lse : 0.f, pp = e * (1.f / s), lmu = on ? mv - lse_mu : 0.f;
+    const float H = -row16_sum(pp * logp);
+    const float kld = row16_sum(pp * (logp - lmu));
+    // log pi(a), log mu(a): the taken action's logit from LDS (one address per row) and its
+    // behaviour logit from the row's lane a (ds_bpermute)
+    const int aa = min(actv[p], A - 1);
+    const float logpa = lg_s[f][aa] - lse;
+    const float muA = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
+        4 * ((lane & 48) + aa), __builtin_bit_cast(int, mv)));
+    const float logmua = muA - lse_mu;
+    pv[p] = pp; lpv[p] = logp; Hv[p] = H;
+    if (ja == 0 && f < nf) {
+      fsc[0][f] = fast_exp(logpa - logmua);
+      fsc[1][f] = H;
+      fsc[2][f] = kld;
+      fsc[3][f] = logpa;
+    }
+  }
+  __syncthreads();
+  // ---- phase 2b: loss head on wave 0 (one lane per (trajectory, t)) ----
   if (wave == 0) {
     const int f = fl;
-    float lg[MAX_A], p[MAX_A], logp[MAX_A];
-    float H = 0.f, kld = 0.f, logpa = 0.f, rho = 0.f;
-    float v = lg_s[f][VCOL];
-    float m = -INFINITY, mm = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < MAX_A; ++j) {
-      lg[j] = j < A ? lg_s[f][j] : -INFINITY;
-      mu[j] = j < A ? mu[j] : -INFINITY;
-      m = fmaxf(m, lg[j]);
-      mm = fmaxf(mm, mu[j]);
-    }
-    float s = 0.f, sm = 0.f;
-#pragma unroll
-    for (int j = 0; j < MAX_A; ++j) {
-      p[j] = j < A ? fast_exp(lg[j] - m) : 0.f;
-      s += p[j];
-      sm += j < A ? fast_exp(mu[j] - mm) : 0.f;
-    }
-    const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm), inv_s = 1.f / s;
-    float logmua = 0.f;
-    // selects, not branches on the runtime action count: a uniform `if (j < A)` per action
-    // makes the compiler carry whole copies of the p/logp arrays through every branch
-#pragma unroll
-    for (int j = 0; j < MAX_A; ++j) {
-      const bool on = j < A;
-      logp[j] = on ? lg[j] - lse : 0.f;
-      p[j] *= inv_s;  // 0 for padded actions
-      const float lmu = on ? mu[j] - lse_mu : 0.f;
-      H -= p[j] * logp[j];
-      kld += p[j] * (logp[j] - lmu);
-      logpa = j == act ? logp[j] : logpa;
-      logmua = j == act ? lmu : logmua;
-    }
-    rho = fast_exp(logpa - logmua);
-    if (!valid) { H = 0.f; kld = 0.f; rho = 0.f; v = 0.f; r = 0.f; g = 0.f; }
+    float rho = valid ? fsc[0][f] : 0.f, H = valid ? fsc[1][f] : 0.f;
+    const float kld = valid ? fsc[2][f] : 0.f, logpa = valid ? fsc[3][f] : 0.f;
+    float v = valid ? lg_s[f][VCOL] : 0.f;
+    if (!valid) { r = 0.f; g = 0.f; }
     if constexpr (PPO) {
       const PpoFrame pf = ppo_frame(rho, v, r, a.clip_lo, a.clip_hi);
       if (valid) {
-        const float c = 1.f / (float)a.B, ke = a.ent_coef * c, kr = c * pf.dr * rho;
-#pragma unroll
-        for (int j = 0; j < MAX_A; ++j)
-          if (j < A) dHs[f * LDD + j] = (T)(ke * p[j] * (logp[j] + H) + kr * ((j == act ? 1.f : 0.f) - p[j]));
+        const float c = 1.f / (float)a.B;
+        fsc[4][f] = c * pf.dr * rho;
         dHs[f * LDD + VCOL] = (T)(-pf.adv * c);
       }
       float q[6] = {valid ? pf.pgl : 0.f, valid ? pf.adv * pf.adv : 0.f, H, kld, rho, r};
@@ -221,11 +236,8 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         a.vt_dbg[3 * BL + f0 + fl] = rho;
       }
       if (valid) {
-        const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T_);
-        const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;
-#pragma unroll
-        for (int j = 0; j < MAX_A; ++j)
-          if (j < A) dHs[f * LDD + j] = (T)(ke * p[j] * (logp[j] + H) - kp * ((j == act ? 1.f : 0.f) - p[j]));
+        const float c_pg = 1.f / (float)(a.B * L);
+        fsc[4][f] = inL ? -c_pg * adv : 0.f;
         dHs[f * LDD + VCOL] = (T)(inL ? -2.f * c_pg * err : 0.f);
       }
       float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
@@ -236,6 +248,14 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
       }
     }  // V-trace loss
+  }
+  __syncthreads();
+  // ---- phase 2c: dH[f][j] = ke p_j (log p_j + H) + kappa_f ([j == a] - p_j) ----
+#pragma unroll
+  for (int p = 0; p < NPASS; ++p) {
+    const int f = 16 * p + 4 * wave + (lane >> 4);
+    if (16 * p < nf && f < nf && ja < A)
+      dHs[f * LDD + ja] = (T)(ke * pv[p] * (lpv[p] + Hv[p]) + fsc[4][f] * ((ja == actv[p] ? 1.f : 0.f) - pv[p]));
   }
   __syncthreads();
   // ---- phase 3: dz = gelu'(z) * (dH . Wh)   rows j (256: wave w -> 4 row tiles), cols f ----
@@ -255,7 +275,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
           const f32x4 zz = *reinterpret_cast<const f32x4*>(zs + f * (HEAD_JC + 4) + j - jw);
           float o[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = acc[q] * gelu_grad(zz[q]);
+          for (int q = 0; q < 4; ++q) o[q] = acc[q] * zz[q];
           store4(dz + (f0 + f) * HID + j, o);
         }
       }

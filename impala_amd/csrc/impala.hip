@@ -114,7 +114,7 @@ struct impala_learner {
   float* vecs = nullptr;
   void *act1, *act2, *act3, *y, *h, *dH, *dz, *dact3, *dact2;
   uint32_t* mask1;  // conv1 ReLU bit mask [N][225]
-  float *lnstat, *z, *heads, *dy;
+  float *lnstat, *zg, *heads, *dy;  // zg = gelu'(FC pre-activation)
   float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
   float *loss_part, *sumsq_part, *adam_sc;
   int64_t* step;
@@ -245,7 +245,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
       return r;
   }
   {
-    FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->z, (T*)h->h};
+    FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->zg, (T*)h->h};
     if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 64, 32, BK(256), 2, 2, FcFwd<T>>,
                         dim3(persist_grid(h, (long)cdiv(n, 32) * (HID / 64))), dim3(256), st, op,
                         HID / 64))
@@ -300,7 +300,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
   {
     HeadArgs ha{};
-    ha.h = h->h; ha.z = h->z; ha.wh = sw + sh.wh; ha.wht = sw + sh.wht;
+    ha.h = h->h; ha.zg = h->zg; ha.wh = sw + sh.wh; ha.wht = sw + sh.wht;
     ha.bh = h->vecs + Vecs::bh;
     ha.act = b->actions; ha.rew = b->rewards; ha.disc = b->discounts; ha.mu = b->behaviour_logits;
     ha.B = B; ha.T = Tl; ha.A = h->A; ha.S = h->S_seg; ha.TPW = 64 / h->S_seg;
@@ -633,7 +633,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->act1 = w + o_act1; h->act2 = w + o_act2; h->act3 = w + o_act3; h->y = w + o_y;
   h->h = w + o_h; h->dH = w + o_dH; h->dz = w + o_dz; h->dact3 = w + o_dact3;
   h->dact2 = w + o_dact2; h->mask1 = (uint32_t*)(w + o_mask1);
-  h->lnstat = (float*)(w + o_lnstat); h->z = (float*)(w + o_z); h->heads = (float*)(w + o_heads);
+  h->lnstat = (float*)(w + o_lnstat); h->zg = (float*)(w + o_z); h->heads = (float*)(w + o_heads);
   h->dy = (float*)(w + o_dy);
   h->s_w1 = (float*)(w + o_sw1); h->s_b1 = (float*)(w + o_sb1);
   h->s_w2 = (float*)(w + o_sw2); h->s_b2 = (float*)(w + o_sb2);

@@ -82,7 +82,7 @@ template <typename T> struct FcFwd {
   const T* w;
   const float* b;
   const T* y;
-  float* z;  // pre-activation (fp32, kept for the GELU backward)
+  float* zg;  // gelu'(pre-activation), fp32: the GELU backward's factor (head_step phase 3)
   T* h;
   struct ColCtx { const T* p; };
   DEV ColCtx col_ctx(int c) const { return ColCtx{y + (size_t)c * FLAT}; }
@@ -91,13 +91,10 @@ template <typename T> struct FcFwd {
   struct Epi { float b[4]; };
   DEV Epi epi(int r, int) const { return Epi{{b[r], b[r + 1], b[r + 2], b[r + 3]}}; }
   DEV void store(int r, int c, float v[4], const Epi& e) const {
-    float zz[4], hh[4];
+    float gg[4], hh[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      zz[i] = v[i] + e.b[i];
-      hh[i] = gelu_f(zz[i]);
-    }
-    store4(z + (size_t)c * HID + r, zz);
+    for (int i = 0; i < 4; ++i) gelu_fwd_grad(v[i] + e.b[i], hh[i], gg[i]);
+    store4(zg + (size_t)c * HID + r, gg);
     store4(h + (size_t)c * HID + r, hh);
   }
 };
