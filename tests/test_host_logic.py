@@ -22,7 +22,10 @@ def test_param_specs_match_reference_state_dict():
 def test_model_views_and_reference_init_on_cpu():
     d = np.load(os.path.join(G, "model_forward.npz"), allow_pickle=False)
     m = AtariPPOModel((3, 64, 64), 15, device="cpu", seed=0)
-    np.testing.assert_array_equal(m.flat.numpy(), d["params"])
+    # bit-exact on the host that generated the fixture; torch's CPU erfinv goes through the host
+    # libm's log, whose ifunc variant depends on the CPU, so other hosts differ by 1-2 ulp in
+    # ~0.6 % of the weights (same bound as test_gpu_parity.py's init check)
+    np.testing.assert_allclose(m.flat.numpy(), d["params"], rtol=1e-6, atol=1e-9)
     sd = m.state_dict()
     assert list(sd.keys()) == [str(k) for k in d["keys"]]
     # parameters and grads are views of the flat buffers

@@ -36,7 +36,9 @@ def test_forward_matches_reference():
 def test_seed0_init_matches_reference():
     d = _load("model_forward.npz")
     m = ref_cpu.make_model(0)
-    np.testing.assert_array_equal(ref_cpu.flat_params(m), d["params"])
+    # bit-exact on the fixture's host; torch's CPU erfinv uses the host libm's log (CPU-dependent
+    # ifunc variant), so other hosts differ by 1-2 ulp in ~0.6 % of the weights
+    np.testing.assert_allclose(ref_cpu.flat_params(m), d["params"], rtol=1e-6, atol=1e-9)
 
 
 def test_train_steps_match_reference():
@@ -65,7 +67,9 @@ def test_head_loss_matches_reference():
     for k in ("adv", "err", "q", "rho", "dlogits", "dvalues"):
         np.testing.assert_allclose(out[k], d[k], rtol=1e-5, atol=1e-7, err_msg=k)
     got = [out[k] for k in ("loss", "entropy", "td", "pg", "kl", "ratio")]
-    np.testing.assert_allclose(got, d["scalars"], rtol=1e-6)
+    # 1e-5 (the north-star bar): pg is a mean of mixed-sign terms (0.0071), so the host libm's
+    # exp/log (CPU-dependent ifunc variants) moves it by ~2e-6 relative on other hosts
+    np.testing.assert_allclose(got, d["scalars"], rtol=1e-5)
 
 
 @pytest.mark.parametrize("tag,lam", [("l100", 1.0), ("l095", 0.95)])
