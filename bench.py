@@ -70,6 +70,9 @@ def kernel_work(es):
         # per-parameter traffic: grads, m, v, params read + written, shadow weight written
         "adam": (0, 0, 344_496 * (8 * 4 + es)),
         "reduce_grads": (0, 0, 0),
+        # fused reduction + Adam: params, m, v read; grads, m, v, params written; shadow written
+        # (the gradient slabs are an implementation artefact, not algorithmic bytes)
+        "reduce_grads_adam": (0, 0, 344_496 * (7 * 4 + es)),
     }
 
 
@@ -220,7 +223,7 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
                  "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "ln_bwd_conv3_dgrad": "LnConv3Bwd", "fc_wgrad": "FcWgrad",
                  "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
-                 "reduce_grads": "reduce_grads", "adam": "adam"}
+                 "reduce_grads": "reduce_grads", "adam": "adam", "reduce_grads_adam": "reduce_adam"}
 
 
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}

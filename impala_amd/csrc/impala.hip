@@ -89,12 +89,12 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 enum KernelId {
   K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
   K_LN_BWD, K_CONV3_DGRAD, K_LNC3_BWD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
-  K_SUMSQ, K_ADAM, K_COUNT
+  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
     "ln_bwd", "conv3_dgrad", "ln_bwd_conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
-    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam"};
+    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam"};
 
 struct impala_learner {
   impala_config cfg;
@@ -118,6 +118,8 @@ struct impala_learner {
   float *s_w1, *s_b1, *s_w2, *s_b2, *s_w3, *s_b3, *s_ln, *s_fc, *s_bfc, *s_h, *s_bh;
   float *loss_part, *sumsq_part, *adam_sc;
   int64_t* step;
+  FusedSync fsync{};  // reduce_adam_kernel's granules, epoch counter and fault word
+  bool fused_update = false;  // world_size 1: slab reduction + clip + Adam in one launch
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   RedArgs red{};
@@ -419,6 +421,7 @@ part1:
       CK(hipEventRecord(h->ev_join, ss));
       CK(hipStreamWaitEvent(st, h->ev_join, 0));
     }
+    if (part == 5) return 0;  // the fused update kernel reduces the slabs
     if (int r = reduce_segments(h, RS_CONV1, RS_END, st, 1)) return r;
   } else {
     if (int r = reduce_segments(h, RS_CONV1, RS_CONV2, st, 1)) return r;
@@ -443,6 +446,23 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.cn = h->cn; aa.sh = h->sh;
   return klaunch(h, K_ADAM, "adam", adam_kernel<T>, dim3(cdiv((long)(h->cn.total + 3) / 4, 256)),
                  dim3(256), st, aa);
+}
+
+// slab reduction + clip + Adam in one launch (world_size 1; backward run with part 5)
+template <typename T>
+int launch_reduce_adam(impala_learner* h, hipStream_t st) {
+  AdamArgs aa{};
+  aa.params = h->params; aa.grads = h->grads; aa.m = h->exp_avg; aa.v = h->exp_avg_sq;
+  aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_red_wg;
+  aa.step = h->step;
+  aa.sc = h->adam_sc; aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
+  aa.eps = h->cfg.adam_eps; aa.max_norm = h->cfg.max_grad_norm;
+  aa.inv_world = 1.f / (float)h->cfg.world_size;
+  aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
+  aa.cn = h->cn; aa.sh = h->sh;
+  return klaunch(h, K_REDUCE_ADAM, "reduce_grads_adam", reduce_adam_kernel<T>,
+                 dim3(cdiv(h->n_red_wg, FU_MAX_UNITS)),
+                 dim3(256), st, h->red, aa, h->fsync);
 }
 
 template <typename T>
@@ -615,6 +635,8 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t o_spart = take((size_t)(h->n_red_wg + 3) / 4 * 16);  // zero tail: float4 reads
   const size_t o_adsc = take(2 * 4);
   const size_t o_step = take(8);
+  const size_t o_gran = take((size_t)h->n_red_wg * 8);  // fused update granules (upper bound)
+  const size_t o_fsync = take(16);                       // epoch counter, fault word
   h->ws_bytes = off;
   hipError_t e = hipMalloc(&h->ws, off);
   if (e != hipSuccess) {
@@ -643,6 +665,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->loss_part = (float*)(w + o_lpart); h->sumsq_part = (float*)(w + o_spart);
   h->adam_sc = (float*)(w + o_adsc);
   h->step = (int64_t*)(w + o_step);
+  h->fsync.gran = (unsigned long long*)(w + o_gran);
+  h->fsync.epoch_ctr = (unsigned*)(w + o_fsync);
+  h->fsync.fault = (unsigned*)(w + o_fsync + 4);
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
@@ -714,6 +739,15 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     ra.lr = dec(cfg->lr); ra.b1 = dec(cfg->adam_beta1); ra.b2 = dec(cfg->adam_beta2);
     ra.adam_sc = h->adam_sc;
   }
+  // fused slab reduction + clip + Adam (reduce_adam_kernel, IMPALA_FUSED_UPDATE=1): world_size
+  // 1, the single-stream end-of-backward reduction, and every reduction unit on a resident
+  // workgroup.  Opt-in: bitwise equal to reduce_grads + adam but slower on MI355X (20 vs
+  // 10.3 + 6.0 us at B=64 T=20 bf16; the all-gather of the norm partials alone takes ~4.5 us
+  // after the last unit publishes, more than the kernel boundary it removes: DESIGN.md §7)
+  h->fsync.n_units = h->n_red_wg;
+  if (const char* e = std::getenv("IMPALA_FUSED_UPDATE")) h->fused_update = e[0] == '1';
+  if (cfg->world_size != 1 || h->red_mode != 0 || h->n_red_wg > 3 * FU_MAX_UNITS * h->n_cu)
+    h->fused_update = false;
   *out = h;
   return 0;
 }
@@ -821,7 +855,7 @@ int impala_act(impala_learner* h, const uint8_t* obs, int n, const uint8_t* dete
 extern "C++" {
 namespace {
 int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {
-  if (part == -1 || part == 0 || part == 2) {
+  if (part == -1 || part == 0 || part == 2 || part == 5) {
     int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st, false)
                     : launch_forward<float>(h, b->obs, h->N, st, false);
     if (r) return r;
@@ -925,6 +959,10 @@ int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
   if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));
   return run_graphed(h, G_STEP, b, (hipStream_t)stream, [&](hipStream_t s) {
+    if (h->fused_update) {
+      if (int r = enqueue_grads(h, b, s, 5)) return r;
+      return h->bf16 ? launch_reduce_adam<__bf16>(h, s) : launch_reduce_adam<float>(h, s);
+    }
     if (int r = enqueue_grads(h, b, s)) return r;
     return enqueue_update(h, s);
   });

@@ -563,6 +563,51 @@ DEV f32x4 sum_splits(const float* p, int grp, int SG, int S, int count) {
   return acc;
 }
 
+// torch Adam's step size lr / (1 - b1^t) and sqrt(1 - b2^t) for step t (double, as torch's
+// python scalars), rounded to fp32
+DEV void adam_scalars(const RedArgs& a, int64_t t, float& step_size, float& bc2s) {
+  const double bc1 = 1.0 - pow(a.b1, (double)t), bc2 = 1.0 - pow(a.b2, (double)t);
+  step_size = (float)(a.lr / bc1);
+  bc2s = (float)sqrt(bc2);
+}
+
+// One reduction unit = one workgroup of reduce_grads_kernel (global index `wg`): the SG split
+// groups' sums are combined in LDS; threads of split group 0 whose column is in range get the 4
+// reduced values and their canonical indices (-1: padding / out of range).  Returns the
+// thread's sum-of-squares contribution (in element order).
+DEV float reduce_unit(const RedArgs& a, int wg, f32x4* part, f32x4& acc, long long (&ci)[4]) {
+  int s = 0;
+  while (wg >= a.wg_start[s + 1]) ++s;
+  const RedSeg& sg = a.seg[s];
+  const int SG = sg.sg, cols = 256 / SG;
+  const int col = threadIdx.x % cols, grp = threadIdx.x / cols;
+  const int v4 = (wg - a.wg_start[s]) * cols + col;  // float4 index in the segment
+  const bool in = v4 * 4 < sg.count;
+  acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (in) {
+    // R split loads in flight per round, R = 8 or 16 by the splits this thread sums (one
+    // round for every segment at the default split-group rule)
+    const float* p = sg.slab + (size_t)v4 * 4;
+    acc = (sg.S + SG - 1) / SG <= 8 ? sum_splits<8>(p, grp, SG, sg.S, sg.count)
+                                    : sum_splits<16>(p, grp, SG, sg.S, sg.count);
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ci[i] = -1;
+  if (grp == 0 && in) {
+    for (int g2 = 1; g2 < SG; ++g2) acc += part[g2 * cols + col];
+    const int k = v4 * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ci[i] = canon_index(a, sg, k + i);
+      if (ci[i] >= 0) sq += acc[i] * acc[i];
+    }
+  }
+  return sq;
+}
+
 // Each segment is processed by workgroups of 256 threads = (256/SG) float4 columns x SG
 // split groups; split group g sums splits g, g+SG, ... and the SG partials are combined in
 // LDS in a fixed order (deterministic for a given SG).  wg_start[] holds each segment's
@@ -574,36 +619,12 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   __shared__ f32x4 part[256];
   __shared__ float red[4];
   const int wg = a.wg_start[s_lo] + (int)blockIdx.x;
-  int s = s_lo;
-  while (wg >= a.wg_start[s + 1]) ++s;
-  const RedSeg& sg = a.seg[s];
-  const int SG = sg.sg, cols = 256 / SG;
-  const int col = threadIdx.x % cols, grp = threadIdx.x / cols;
-  const int v4 = (wg - a.wg_start[s]) * cols + col;  // float4 index in the segment
-  const bool in = v4 * 4 < sg.count;
-  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (in) {
-    // R split loads in flight per round, R = 8 or 16 by the splits this thread sums (one
-    // round for every segment at the default split-group rule)
-    const float* p = sg.slab + (size_t)v4 * 4;
-    acc = (sg.S + SG - 1) / SG <= 8 ? sum_splits<8>(p, grp, SG, sg.S, sg.count)
-                                    : sum_splits<16>(p, grp, SG, sg.S, sg.count);
-  }
-  part[threadIdx.x] = acc;
-  __syncthreads();
-  float sq = 0.f;
-  if (grp == 0 && in) {
-    for (int g2 = 1; g2 < SG; ++g2) acc += part[g2 * cols + col];
-    const int k = v4 * 4;
+  f32x4 acc;
+  long long ci[4];
+  float sq = reduce_unit(a, wg, part, acc, ci);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long long c = canon_index(a, sg, k + i);
-      if (c >= 0) {
-        a.grads[c] = acc[i];
-        sq += acc[i] * acc[i];
-      }
-    }
-  }
+  for (int i = 0; i < 4; ++i)
+    if (ci[i] >= 0) a.grads[ci[i]] = acc[i];
   sq = wave_sum(sq);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
@@ -617,9 +638,7 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   if (fin && blockIdx.x == 0 && threadIdx.x == 128) {  // step += 1 and its bias corrections
     const int64_t t = *a.step + 1;
     *a.step = t;
-    const double bc1 = 1.0 - pow(a.b1, (double)t), bc2 = 1.0 - pow(a.b2, (double)t);
-    a.adam_sc[0] = (float)(a.lr / bc1);
-    a.adam_sc[1] = (float)sqrt(bc2);
+    adam_scalars(a, t, a.adam_sc[0], a.adam_sc[1]);
   }
 }
 
@@ -653,6 +672,22 @@ struct AdamArgs {
   Canon cn;
   Shadow sh;
 };
+
+// torch.optim.Adam's update of one element (lerp form of exp_avg, sqrt(v) / sqrt(bc2) + eps),
+// on the clipped gradient g * gscale; shared by the unfused and the fused update kernels so both
+// compile the same arithmetic
+DEV void adam_elem(const AdamArgs& a, float gscale, float step_size, float bc2s, float& g,
+                   float& m, float& v, float& p) {
+  // every multiply and add rounded on its own, as written: no FMA contraction, whose choice
+  // depends on the surrounding code and would make the two kernels differ in the last bit
+#pragma clang fp contract(off)
+  const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
+  g = g * gscale;
+  m = m + w1 * (g - m);
+  v = v * b2f + w2 * g * g;
+  const float denom = sqrtf(v) / bc2s + a.eps;
+  p = p - step_size * (m / denom);
+}
 
 // clip + Adam on 4 consecutive parameters per thread; re-emits the kernel-layout weights.
 // (A row-wise variant that re-emits the big matrices through an LDS permutation with 16-byte
@@ -703,15 +738,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   }
   if (n == 0) return;
   const float gscale = a.inv_world * coef;
-  const float w1 = (float)(1.0 - a.b1), b2f = (float)a.b2, w2 = (float)(1.0 - a.b2);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    g[k] = g[k] * gscale;
-    m[k] = m[k] + w1 * (g[k] - m[k]);
-    v[k] = v[k] * b2f + w2 * g[k] * g[k];
-    const float denom = sqrtf(v[k]) / bc2s + a.eps;
-    p[k] = p[k] - step_size * (m[k] / denom);
-  }
+  for (int k = 0; k < 4; ++k) adam_elem(a, gscale, step_size, bc2s, g[k], m[k], v[k], p[k]);
   if (n == 4) {
     *reinterpret_cast<f32x4*>(a.grads + i0) = f32x4{g[0], g[1], g[2], g[3]};
     *reinterpret_cast<f32x4*>(a.m + i0) = f32x4{m[0], m[1], m[2], m[3]};
@@ -723,6 +751,158 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     }
   }
   for (int k = 0; k < n; ++k) write_shadow<T>(a.sp, a.cn, a.sh, i0 + k, p[k]);
+}
+
+// =========================================================================================
+// Fused slab reduction + clip + Adam (world_size 1): one launch instead of reduce_grads and
+// adam.  The workgroups run the reduction units of reduce_grads_kernel (unit u on workgroup
+// u % grid, at most FU_MAX_UNITS each), keep each thread's reduced values and canonical indices in
+// registers and issue that element's parameter / moment loads at once.  Each unit's sum of
+// squares is published as one 8-byte {epoch, value} granule (an agent-scope relaxed atomic store:
+// the data is its own flag, MI355X_MICROARCH.md "R2"); every workgroup then sweeps all granules
+// until each carries this launch's epoch, sums them in adam_kernel's order (same norm bits), and
+// updates its own elements -- no grid barrier and no other cross-workgroup payload.  Every
+// workgroup must be resident at once: the grid is the CU count (one 256-thread workgroup per
+// CU), and the sweep is bounded (a timeout sets `fault` and a NaN grad_norm instead of hanging).
+// epoch = *epoch_ctr + 1 (never 0), read by every workgroup before it publishes; workgroup 0
+// stores it back after its sweep has seen every granule, i.e. after every read.  The Adam step
+// counter is handled the same way.  Bitwise equal to reduce_grads + adam (tests).
+// =========================================================================================
+constexpr int FU_MAX_UNITS = 1;  // units per workgroup (the grid is the unit count)
+struct FusedSync {
+  unsigned long long* gran;  // [n_units] {epoch << 32 | float bits}
+  unsigned* epoch_ctr;
+  unsigned* fault;
+  int n_units;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void reduce_adam_kernel(const RedArgs a, const AdamArgs aa,
+                                                          const FusedSync fs) {
+  __shared__ f32x4 part[256];
+  __shared__ float red[4];
+  __shared__ unsigned s_epoch;
+  __shared__ long long s_step;
+  // the epoch counter and the step are read first but only waited for after the reduction
+  unsigned e_ld = 0u;
+  unsigned long long st_ld = 0ull;
+  if (threadIdx.x == 0) {
+    e_ld = __hip_atomic_load(fs.epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_ld = __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.step), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+  }
+  float g[FU_MAX_UNITS][4], m[FU_MAX_UNITS][4], v[FU_MAX_UNITS][4], p[FU_MAX_UNITS][4];
+  long long ci[FU_MAX_UNITS][4];
+  // ---- reduction units; the Adam operands of each element are loaded beside its slabs ----
+#pragma unroll
+  for (int j = 0; j < FU_MAX_UNITS; ++j) {
+    const int u = (int)blockIdx.x + j * (int)gridDim.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ci[j][i] = -1;
+    if (u >= fs.n_units) continue;  // uniform over the workgroup
+    {  // this thread's canonical indices (reduce_unit's column mapping) -> p, m, v loads now
+      int s = 0;
+      while (u >= a.wg_start[s + 1]) ++s;
+      const RedSeg& sg = a.seg[s];
+      const int cols = 256 / sg.sg, col = threadIdx.x % cols, grp = threadIdx.x / cols;
+      const int v4 = (u - a.wg_start[s]) * cols + col;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long c = grp == 0 && v4 * 4 < sg.count ? canon_index(a, sg, v4 * 4 + i) : -1;
+        const long long cc = c >= 0 ? c : 0;  // clamped address, value dropped later
+        p[j][i] = aa.params[cc];
+        m[j][i] = aa.m[cc];
+        v[j][i] = aa.v[cc];
+      }
+    }
+    f32x4 acc;
+    float sq = reduce_unit(a, u, part, acc, ci[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[j][i] = acc[i];
+    if (j == 0 && threadIdx.x == 0) {
+      s_epoch = e_ld + 1u == 0u ? 1u : e_ld + 1u;
+      s_step = (long long)st_ld;
+    }
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float part_sq = red[0] + red[1] + red[2] + red[3];
+      __hip_atomic_store(fs.gran + u,
+                         ((unsigned long long)s_epoch << 32) | (unsigned long long)__float_as_uint(part_sq),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // part / red are reused by the next unit
+  }
+  const unsigned epoch = s_epoch;
+  const int64_t t = (int64_t)s_step + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 64) {
+    if (a.algo == 1)
+      finalize_ppo_metrics(a.loss_part, a.n_loss_part, a.B * a.T, a.ent_coef, a.metrics);
+    else
+      finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
+  }
+  // step size and bias correction (double pow) by one lane, while the others start sweeping
+  __shared__ float s_sc[2];
+  if (threadIdx.x == 0) adam_scalars(a, t, s_sc[0], s_sc[1]);
+  // ---- sweep the granules: thread q holds partials 4q .. 4q+3 (adam_kernel's float4 q) ----
+  const int nq = (fs.n_units + 3) / 4;
+  float x[4] = {0.f, 0.f, 0.f, 0.f};
+  bool timed_out = false;
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    if ((int)threadIdx.x < nq) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = 4 * (int)threadIdx.x + k;
+        if (q < fs.n_units) {
+          const unsigned long long w = __hip_atomic_load(fs.gran + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = ok && (unsigned)(w >> 32) == epoch;
+          x[k] = __uint_as_float((unsigned)w);
+        }
+      }
+    }
+    if (__syncthreads_and(ok)) break;
+    if (spins > (1u << 22)) {  // ~0.1 s: a workgroup never ran; give up instead of hanging
+      timed_out = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(10);
+  }
+  float sq = 0.f;
+  if ((int)threadIdx.x < nq) sq += (x[0] + x[1]) + (x[2] + x[3]);
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  float norm = sqrtf(red[0] + red[1] + red[2] + red[3]) * aa.inv_world;
+  if (timed_out) {
+    norm = __builtin_nanf("");
+    if (threadIdx.x == 0) __hip_atomic_store(fs.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const float coef = fminf(aa.max_norm / (norm + 1e-6f), 1.f);
+  const float step_size = s_sc[0], bc2s = s_sc[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    aa.metrics[6] = norm;
+    aa.metrics[7] = (float)t;
+    *a.step = t;
+    a.adam_sc[0] = step_size;
+    a.adam_sc[1] = bc2s;
+    __hip_atomic_store(fs.epoch_ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const float gscale = aa.inv_world * coef;
+#pragma unroll
+  for (int j = 0; j < FU_MAX_UNITS; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long c = ci[j][i];
+      if (c < 0) continue;
+      adam_elem(aa, gscale, step_size, bc2s, g[j][i], m[j][i], v[j][i], p[j][i]);
+      aa.grads[c] = g[j][i];
+      aa.m[c] = m[j][i];
+      aa.v[c] = v[j][i];
+      aa.params[c] = p[j][i];
+      write_shadow<T>(aa.sp, aa.cn, aa.sh, (size_t)c, p[j][i]);
+    }
 }
 
 // heads output [n][16] -> logits [n][A], values [n]

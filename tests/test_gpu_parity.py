@@ -247,7 +247,35 @@ def test_train_step_deterministic(dtype):
     np.testing.assert_array_equal(flats[0][1], flats[1][1])
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_update_matches_reduce_then_adam(dtype, monkeypatch):
+    """The fused slab reduction + clip + Adam launch (reduce_adam_kernel, world_size 1, opt-in
+    IMPALA_FUSED_UPDATE=1) is bitwise equal to reduce_grads + adam at BASELINE config 2's size (B=64, T=20):
+    params, post-clip grads, both Adam moments and every metric, over 3 steps."""
+    dev = _dev()
+    batches = [[_t(x, dev) for x in ref_cpu.synthetic_batch(64, 20, 15, seed=70 + i)]
+               for i in range(3)]
+
+    def run():
+        m = _model(dev, dtype, seed=0)
+        e = _engine(m, 64, 20)
+        for b in batches:
+            e.train_step(*b)
+        torch.cuda.synchronize()
+        return [x.cpu().numpy().copy() for x in (m.flat, m.flat_grad, e.exp_avg, e.exp_avg_sq,
+                                                 e.metrics)]
+
+    monkeypatch.setenv("IMPALA_FUSED_UPDATE", "1")
+    fused = run()
+    monkeypatch.setenv("IMPALA_FUSED_UPDATE", "0")
+    ref = run()
+    for a, b, name in zip(fused, ref, ("params", "grads", "exp_avg", "exp_avg_sq", "metrics")):
+        np.testing.assert_array_equal(a, b, err_msg=name)
+    assert np.isfinite(fused[4]).all() and fused[4][7] == 3.0  # step counter
+
+
 @pytest.mark.parametrize("env,exact", [({"IMPALA_GRAPH": "1"}, True),
+                                       ({"IMPALA_FUSED_UPDATE": "1"}, True),
                                        ({"IMPALA_SIDE_STREAM": "1"}, True),
                                        ({"IMPALA_FWD_FUSED": "0"}, True),
                                        ({"IMPALA_LNC3_FUSED": "0"}, False)])

@@ -23,6 +23,8 @@ def short(name):
                    ("gemm_jobs", "sac_wgrad")):
         if k in n:
             return tag
+    if "reduce_adam_kernel" in n:
+        return "reduce_adam"
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
     if "conv12_bwd_s2d" in n:
