@@ -272,7 +272,13 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
 // issued unconditionally: rows past the split's end and chunks past the group's last one carry
 // an out-of-range offset and read as zero without touching memory (no branch around a load,
 // so the compiler's counted vmcnt waits stay exact).  The groups' accumulators are summed in
-// a fixed order at the end.  Output: fp32 partial slab [split][R][C] (+ per-split bias sums).
+// a fixed order at the end.  Output: fp32 partial slab [split][R][C] (+ per-split bias sums),
+// or, for an Op with DIRECT (one split: the tile is final), the canonical gradient itself plus
+// the workgroup's sum of squares in op.sumsq[workgroup].
+template <class Op, class = void> struct wg_direct { static constexpr bool value = false; };
+template <class Op> struct wg_direct<Op, decltype(void(Op::DIRECT))> {
+  static constexpr bool value = Op::DIRECT;
+};
 template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op, int PD = 2>
 __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restrict__ slab,
                                                    float* __restrict__ slab_bias,
@@ -311,7 +317,8 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
   const int m_beg = split * m_per_split;
   const int m_end = min(op.M, m_beg + m_per_split);
   const int wr = wave / WC, wc = wave % WC;
-  const bool do_bias = slab_bias != nullptr && bx == 0;
+  constexpr bool DIRECT = wg_direct<Op>::value;
+  const bool do_bias = (DIRECT || slab_bias != nullptr) && bx == 0;
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<T*>(op.x), 0, op.M * op.x_ld * (int)sizeof(T), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(
@@ -441,6 +448,7 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
       __syncthreads();
     }
   }
+  float bias_sq = 0.f;  // DIRECT: this thread's final bias element, squared
   if (do_bias) {  // combine the (256/BR) row groups of group 0's bias sums, fixed order
     constexpr int RG = 256 / BR;
     float* redb = reinterpret_cast<float*>(smem);
@@ -450,8 +458,43 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
       float bsum = 0.f;
 #pragma unroll
       for (int g = 0; g < RG; ++g) bsum += redb[g * BR + tid];
-      slab_bias[(size_t)split * op.R + r0 + tid] = bsum;
+      if constexpr (DIRECT) {
+        op.grads[op.bias_canon(r0 + tid)] = bsum;
+        bias_sq = bsum * bsum;
+      } else {
+        slab_bias[(size_t)split * op.R + r0 + tid] = bsum;
+      }
     }
+  }
+  if constexpr (DIRECT) {
+    __syncthreads();  // the bias sums above are read from smem before it is reused below
+    float sq = 0.f;
+    if (grp == 0) {
+#pragma unroll
+      for (int j = 0; j < TCW; ++j) {
+        const int c = c0 + (wc * TCW + j) * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < TRW; ++i) {
+          const int r = r0 + (wr * TRW + i) * 16 + 4 * (lane >> 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = acc[i][j][q] * op.out_scale;
+            if (c < op.C) {
+              op.grads[op.canon(r + q, c)] = v;
+              sq += v * v;
+            }
+          }
+        }
+      }
+      sq = wave_sum(sq + bias_sq);
+    }
+    float* redq = reinterpret_cast<float*>(smem);
+    if (grp == 0 && lane == 0) redq[wave] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      op.sumsq[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] =
+          (redq[0] + redq[1]) + (redq[2] + redq[3]);
+    return;
   }
   if (grp != 0) return;
   const float sc = op.out_scale;

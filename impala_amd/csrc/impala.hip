@@ -71,6 +71,8 @@ inline double dec(float x) {
 struct Split {
   int S = 1, mps = 32;  // splits, m per split
 };
+// direct (one-split) FC weight-gradient tile: BR x BC outputs, WR x WC waves, G 4-wave groups
+constexpr int FCD_BR = 32, FCD_BC = 64, FCD_WR = 2, FCD_WC = 2, FCD_G = 4, FCD_PD = 2;
 Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
   Split s;
   const long chunks = (M + chunk - 1) / chunk;
@@ -122,6 +124,11 @@ struct impala_learner {
   bool fused_update = false;  // world_size 1: slab reduction + clip + Adam in one launch
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
+  // FC weight gradient in one split written straight into the canonical gradient (gemm_wg
+  // direct mode, no slab); its workgroups' sums of squares follow the reduction's partials
+  bool fc_direct = false;
+  int n_fc_wg = 0;
+  int n_norm_part = 0;  // clip-norm partials: n_red_wg (+ n_fc_wg)
   RedArgs red{};
   // side stream for the weight-gradient branches (fork/join with events, graph-capturable)
   hipStream_t side = nullptr;
@@ -321,13 +328,25 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
       return r;
   }
   if (int r = fork(1)) return r;  // dz ready
-  {
+  if (h->fc_direct) {
+    FcWgradDirect<T> op{};
+    op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
+    op.grads = h->grads; op.wcanon = (long long)h->cn.wfc; op.sumsq = h->sumsq_part + h->n_red_wg;
+    constexpr int G = sizeof(T) == 2 ? FCD_G : 1;
+    if (int r = klaunch(h, K_FC_WGRAD, "fc_wgrad",
+                        gemm_wg<T, FCD_BR, FCD_BC, FCD_WR, FCD_WC, 32, G, FcWgradDirect<T>, FCD_PD>,
+                        dim3(FLAT / FCD_BC, HID / FCD_BR, 1), dim3(256 * G), ss, op, nullptr,
+                        nullptr, N))
+      return r;
+  } else {
     FcWgrad<T> op{};
     op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
     if (int r = klaunch(h, K_FC_WGRAD, "fc_wgrad", gemm_wg<T, 64, 256, 1, 4, 32, WG2, FcWgrad<T>>,
                         dim3(FLAT / 256, HID / 64, h->spfc.S), dim3(256 * WG2), ss, op, h->s_fc,
                         h->s_bfc, h->spfc.mps))
       return r;
+  }
+  {
     if (h->red_mode == 1)
       if (int r = reduce_segments(h, RS_FC, RS_END, ss, 0)) return r;  // fc + heads slabs
   }
@@ -437,7 +456,7 @@ template <typename T>
 int launch_adam(impala_learner* h, hipStream_t st) {
   AdamArgs aa{};
   aa.params = h->params; aa.grads = h->grads; aa.m = h->exp_avg; aa.v = h->exp_avg_sq;
-  aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_red_wg;
+  aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_norm_part;
   aa.step = h->step;
   aa.sc = h->adam_sc; aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
   aa.eps = h->cfg.adam_eps; aa.max_norm = h->cfg.max_grad_norm;
@@ -453,7 +472,7 @@ template <typename T>
 int launch_reduce_adam(impala_learner* h, hipStream_t st) {
   AdamArgs aa{};
   aa.params = h->params; aa.grads = h->grads; aa.m = h->exp_avg; aa.v = h->exp_avg_sq;
-  aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_red_wg;
+  aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_norm_part;
   aa.step = h->step;
   aa.sc = h->adam_sc; aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
   aa.eps = h->cfg.adam_eps; aa.max_norm = h->cfg.max_grad_norm;
@@ -589,6 +608,14 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
                       HID + HEADS * HID + HEADS) / 4 / 16;
   h->sph.S = h->n_loss_wg;  // heads weight-gradient partials: one slab per head workgroup
   h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), 96);
+  // one-split FC weight gradient written straight into the canonical gradient (opt-in,
+  // IMPALA_FC_DIRECT=1, up to 8192 frames): it drops the 6.3 MB FC slab and 256 reduction
+  // workgroups, but the one-split GEMM is latency-bound on its per-CU load concurrency and the
+  // step measured 0.1340-0.1368 ms in every tile shape against 0.1325-0.1330 ms for the split
+  // slab (profiles/r02d/fc_direct_variants.txt)
+  h->fc_direct = false;
+  if (const char* e = std::getenv("IMPALA_FC_DIRECT")) h->fc_direct = N <= 8192 && e[0] == '1';
+  h->n_fc_wg = (FLAT / FCD_BC) * (HID / FCD_BR);
   h->sp3 = plan_split((long)N * P3, K3 / 64, 256);
   h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
   h->c1_fpw = std::max(1, cdiv(N, h->n_cu));
@@ -716,11 +743,13 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     add(h->s_w3, h->sp3.S, OC3 * K3, RK_CONV3, (long long)h->cn.w3);
     add(h->s_b3, h->sp3.S, OC3, RK_ID, (long long)h->cn.b3);
     add(h->s_ln, h->n_ln_wg, 2 * FLAT, RK_LN, (long long)h->cn.lng);
-    add(h->s_fc, h->spfc.S, HID * FLAT, RK_FC, (long long)h->cn.wfc);
-    add(h->s_bfc, h->spfc.S, HID, RK_ID, (long long)h->cn.bfc);
+    // (direct FC: empty segments, so the segment indices stay fixed)
+    add(h->s_fc, h->spfc.S, h->fc_direct ? 0 : HID * FLAT, RK_FC, (long long)h->cn.wfc);
+    add(h->s_bfc, h->spfc.S, h->fc_direct ? 0 : HID, RK_ID, (long long)h->cn.bfc);
     add(h->s_h, h->sph.S, HEADS * HID, RK_HEADS_W, 0);
     add(h->s_bh, h->sph.S, HEADS, RK_HEADS_B, 0);
     h->n_red_wg = ra.wg_start[ns];
+    h->n_norm_part = h->n_red_wg + (h->fc_direct ? h->n_fc_wg : 0);
     if (ns != RS_END) {
       impala_destroy(h);
       return fail(IMPALA_E_STATE, "reduce segment table out of sync");
@@ -745,7 +774,11 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   // 10.3 + 6.0 us at B=64 T=20 bf16; the all-gather of the norm partials alone takes ~4.5 us
   // after the last unit publishes, more than the kernel boundary it removes: DESIGN.md §7)
   h->fsync.n_units = h->n_red_wg;
+  h->fsync.n_part = h->n_norm_part;
+  h->fsync.part = h->sumsq_part;
   if (const char* e = std::getenv("IMPALA_FUSED_UPDATE")) h->fused_update = e[0] == '1';
+  // (it updates exactly the elements it reduces, so the direct FC gradient is off with it)
+  if (h->fused_update && h->fc_direct) h->fused_update = false;
   if (cfg->world_size != 1 || h->red_mode != 0 || h->n_red_wg > 3 * FU_MAX_UNITS * h->n_cu)
     h->fused_update = false;
   *out = h;
@@ -865,7 +898,7 @@ int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int 
 
 int enqueue_update(impala_learner* h, hipStream_t st) {
   if (h->cfg.world_size > 1) {
-    if (int r = klaunch(h, K_SUMSQ, "sumsq", sumsq_kernel, dim3(h->n_red_wg), dim3(256), st,
+    if (int r = klaunch(h, K_SUMSQ, "sumsq", sumsq_kernel, dim3(h->n_norm_part), dim3(256), st,
                         (const float*)h->grads, (size_t)h->cn.total, h->sumsq_part))
       return r;
   }

@@ -774,6 +774,8 @@ struct FusedSync {
   unsigned* epoch_ctr;
   unsigned* fault;
   int n_units;
+  int n_part;          // clip-norm partials: the n_units granules, then part[n_units, n_part)
+  const float* part;   // partials written by earlier launches (direct-mode weight gradients)
 };
 
 template <typename T>
@@ -846,8 +848,15 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const RedArgs a, const
   __shared__ float s_sc[2];
   if (threadIdx.x == 0) adam_scalars(a, t, s_sc[0], s_sc[1]);
   // ---- sweep the granules: thread q holds partials 4q .. 4q+3 (adam_kernel's float4 q) ----
-  const int nq = (fs.n_units + 3) / 4;
+  const int nq = (fs.n_part + 3) / 4;
   float x[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((int)threadIdx.x < nq) {  // partials of earlier launches (no wait needed)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 4 * (int)threadIdx.x + k;
+      if (q >= fs.n_units && q < fs.n_part) x[k] = fs.part[q];
+    }
+  }
   bool timed_out = false;
   for (unsigned spins = 0;; ++spins) {
     bool ok = true;

@@ -217,6 +217,21 @@ template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
   DEV int y_bytes() const { return M * FLAT * (int)sizeof(T); }
   DEV const T* ybase() const { return y; }
 };
+// The FC weight gradient over the whole batch in one split (gemm_wg direct mode): the tile is
+// final, so it is written straight into the canonical gradient (o*1024 + c*16 + p for kernel
+// column j = p*64 + c; the bias into bfc) and the workgroup's sum of squares goes to its own
+// clip-norm partial slot -- no fp32 partial slab and no reduction pass for this layer.
+template <typename T> struct FcWgradDirect : FcWgrad<T> {
+  static constexpr bool DIRECT = true;
+  float* grads;       // canonical gradient buffer
+  long long wcanon;   // canonical offset of wfc (bfc follows at wcanon + HID * FLAT)
+  float* sumsq;       // [workgroups] partial sums of squares
+  DEV long long canon(int o, int j) const {
+    return wcanon + (long long)o * FLAT + (j & 63) * 16 + (j >> 6);
+  }
+  DEV long long bias_canon(int o) const { return wcanon + (long long)HID * FLAT + o; }
+};
+
 template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3+kw)*64 + ci
   static constexpr int R = OC3, C = K3;
   int M;
