@@ -65,6 +65,8 @@ def kernel_work(es):
         "conv2_dgrad_conv1_wgrad": (2 * 36 * 64 * 512 + 2 * 225 * 32 * 192, obs + a2 + m1,
                                     64 * 512 * es),
         "fc_wgrad": (2 * 256 * 1024, 256 * es + a3, 0),
+        # FC weight + input gradient in one launch (dz read once for both)
+        "fc_wgrad_fc_dgrad": (2 * 2 * 256 * 1024, 256 * es + a3 + 1024 * 4, 256 * 1024 * es),
         "conv3_wgrad": (2 * 16 * 64 * 576, a3 + a2, 0),
         "conv2_wgrad": (2 * 36 * 64 * 512, a2 + a1, 0),
         # per-parameter traffic: grads, m, v, params read + written, shadow weight written
@@ -223,7 +225,8 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
                  "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "ln_bwd_conv3_dgrad": "LnConv3Bwd", "fc_wgrad": "FcWgrad",
                  "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
-                 "reduce_grads": "reduce_grads", "adam": "adam", "reduce_grads_adam": "reduce_adam"}
+                 "reduce_grads": "reduce_grads", "adam": "adam", "reduce_grads_adam": "reduce_adam",
+                 "fc_wgrad_fc_dgrad": "FcBwd"}
 
 
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}

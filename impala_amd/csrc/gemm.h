@@ -101,8 +101,17 @@ template <class Op> struct EpiTypes<Op, true> {
 // forward weight consumed by a dgrad); its chunk is staged [k][r] and the A fragments are
 // read with the LDS transpose read, so no transposed weight copy is kept in HBM.
 // Requires K % BK == 0, R % BR == 0 and no A dependence on columns inside one BC tile.
+// The body runs on NT = 64 * WR * WC threads as virtual workgroup `vbid` of `vgrid`, with the
+// LDS passed in (gemm_tile_smem elements), so a launch can host it beside another body.
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
-__global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
+constexpr int gemm_tile_smem() {
+  constexpr int VEC = 16 / (int)sizeof(T), LD = BK + VEC;
+  constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + VEC) : BR * LD;
+  return 2 * (ASZ + BC * LD);
+}
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
+DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __restrict__ smem) {
+  constexpr int NT = 64 * WR * WC;
   constexpr bool AK = Op::A_KMAJOR;
   using F = Frag<T>;
   typedef typename F::vec V;
@@ -110,22 +119,22 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   constexpr int KV = BK / VEC;            // 16-byte vectors per tile row per chunk
   constexpr int LD = BK + VEC;            // padded row (elements)
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
-  constexpr int NA = BR * KV / 256, NB = BC * KV / 256;
+  constexpr int NA = BR * KV / NT, NB = BC * KV / NT;
   constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
   constexpr int LDA = AK ? BR + VEC : LD; // A tile row length (elements)
   constexpr int ASZ = AK ? BK * LDA : BR * LD;
   constexpr int NK = Op::K / BK;
-  static_assert(WR * WC == 4 && TRW >= 1 && TCW >= 1, "tile");
-  static_assert(BR * KV % 256 == 0 && BC * KV % 256 == 0, "staging");
+  static_assert((WR * WC == 4 || (WR * WC == 8 && !Op::TILE_EPI)) && TRW >= 1 && TCW >= 1, "tile");
+  static_assert(BR * KV % NT == 0 && BC * KV % NT == 0, "staging");
   static_assert(Op::K % BK == 0 && BK % F::KSTEP == 0, "K chunking");
-  __shared__ __attribute__((aligned(16))) T smem[2 * (ASZ + BC * LD)];
+  constexpr int SMEM = 2 * (ASZ + BC * LD);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
   // staging element e = tid + i*256 of a chunk -> (tile row e / KV, 16-byte vector e % KV)
-  auto srow = [&](int i) { return (tid + i * 256) / KV; };
-  auto skv = [&](int i) { return (tid + i * 256) % KV; };
+  auto srow = [&](int i) { return (tid + i * NT) / KV; };
+  auto skv = [&](int i) { return (tid + i * NT) % KV; };
   const int n_tiles = n_rtiles * ((op.C + BC - 1) / BC);
-  const int ft = xcd_swizzle(blockIdx.x, gridDim.x);  // first tile of this workgroup
+  const int ft = xcd_swizzle(vbid, vgrid);  // first tile of this workgroup
   if (ft >= n_tiles) return;
   // per-thread staging contexts of the fetch tile
   const T* arow[NA];
@@ -147,7 +156,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
     if constexpr (AK) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, kr = e / RV, rv = e % RV;
+        const int e = tid + i * NT, kr = e / RV, rv = e % RV;
         ra[i] = F::load(op.a_kptr(k0 + kr, fr0 + rv * VEC, fcw));
       }
     } else {
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
     if constexpr (AK) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, kr = e / RV, rv = e % RV;
+        const int e = tid + i * NT, kr = e / RV, rv = e % RV;
         *reinterpret_cast<V*>(As + kr * LDA + rv * VEC) = ra[i];
       }
     } else {
@@ -178,7 +187,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   fetch(0);
   [[maybe_unused]] typename EpiTypes<Op>::EpiConst econst{};
   if constexpr (Op::TILE_EPI) econst = op.epi_const(tid);
-  for (int t = ft; t < n_tiles; t += gridDim.x) {
+  for (int t = ft; t < n_tiles; t += vgrid) {
     const int cr0 = fr0, cc0 = fc0;  // coordinates of tile t (the fetch cursor is on it)
     // the epilogue's global reads, issued now so they land under the K loop
     [[maybe_unused]] typename EpiTypes<Op>::Epi ep[TRW][TCW];
@@ -202,8 +211,8 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
       __syncthreads();
       if (kc + 1 < NK) {
         fetch((kc + 1) * BK);
-      } else if (t + (int)gridDim.x < n_tiles) {
-        set_ctx(t + gridDim.x);  // prefetch the next tile's first chunk under this compute
+      } else if (t + vgrid < n_tiles) {
+        set_ctx(t + vgrid);  // prefetch the next tile's first chunk under this compute
         fetch(0);
       }
       const T* As = smem + buf * (ASZ + BC * LD);
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
     }
     if constexpr (Op::TILE_EPI) {
       // workgroup epilogue: fp32 tile [BC][BR+4] in (reused) LDS, then op.tile_epilogue
-      static_assert((size_t)BC * (BR + 4) * sizeof(float) <= sizeof(smem), "epilogue tile");
+      static_assert((size_t)BC * (BR + 4) * sizeof(float) <= SMEM * sizeof(T), "epilogue tile");
       __syncthreads();  // all waves are done reading the staging buffers
       float* et = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -260,6 +269,12 @@ __global__ __launch_bounds__(256) void gemm_tile(const Op op, int n_rtiles) {
   }
 }
 
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
+__global__ __launch_bounds__(64 * WR * WC) void gemm_tile(const Op op, int n_rtiles) {
+  __shared__ __attribute__((aligned(16))) T smem[gemm_tile_smem<T, BR, BC, BK, WR, WC, Op>()];
+  gemm_tile_body<T, BR, BC, BK, WR, WC, Op>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
+}
+
 // Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split
 // blockIdx.z.  X is a row-major [M][x_ld] matrix (the channels-last output gradient); Y is a
 // gather (im2col of the layer input) given as element offsets y_roff(m) + y_coff(c) of 16-byte
@@ -279,10 +294,16 @@ template <class Op, class = void> struct wg_direct { static constexpr bool value
 template <class Op> struct wg_direct<Op, decltype(void(Op::DIRECT))> {
   static constexpr bool value = Op::DIRECT;
 };
+// The body runs as virtual workgroup `lin` of a gx x gy x gz grid on 256 * G threads, with the
+// LDS passed in (gemm_wg_smem elements).
+template <typename T, int BR, int BC, int BM, int G>
+constexpr int gemm_wg_smem() {
+  constexpr int VEC = 16 / (int)sizeof(T);
+  return (BM * (BR + VEC) + BM * (BC + VEC)) * 2 * G;
+}
 template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op, int PD = 2>
-__global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restrict__ slab,
-                                                   float* __restrict__ slab_bias,
-                                                   int m_per_split) {
+DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict__ slab_bias,
+                      int m_per_split, int lin, int gx, int gy, int gz, T* __restrict__ smem) {
   using F = Frag<T>;
   typedef typename F::vec V;  // 16 bytes of T
   constexpr int VEC = 16 / (int)sizeof(T);
@@ -307,12 +328,12 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
   static_assert(PD >= 1, "prefetch depth");
   static_assert((size_t)STAGE * 2 * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
                 "LDS reuse for the group reduction");
-  __shared__ __attribute__((aligned(16))) T smem[STAGE * 2 * G];
+  static_assert(STAGE * 2 * G == gemm_wg_smem<T, BR, BC, BM, G>(), "LDS size");
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   // work item (column tile fastest) from the XCD-swizzled dispatch id
-  const int nwg = gridDim.x * gridDim.y * gridDim.z;
-  const int wid = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
-  const int bx = wid % gridDim.x, by = (wid / gridDim.x) % gridDim.y, split = wid / (gridDim.x * gridDim.y);
+  const int nwg = gx * gy * gz;
+  const int wid = xcd_swizzle(lin, nwg);
+  const int bx = wid % gx, by = (wid / gx) % gy, split = wid / (gx * gy);
   const int c0 = bx * BC, r0 = by * BR;
   const int m_beg = split * m_per_split;
   const int m_end = min(op.M, m_beg + m_per_split);
@@ -491,9 +512,7 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
     float* redq = reinterpret_cast<float*>(smem);
     if (grp == 0 && lane == 0) redq[wave] = sq;
     __syncthreads();
-    if (threadIdx.x == 0)
-      op.sumsq[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] =
-          (redq[0] + redq[1]) + (redq[2] + redq[3]);
+    if (threadIdx.x == 0) op.sumsq[lin] = (redq[0] + redq[1]) + (redq[2] + redq[3]);
     return;
   }
   if (grp != 0) return;
@@ -510,4 +529,15 @@ __global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restric
         slab[((size_t)split * op.R + r + q) * op.C + c] = acc[i][j][q] * sc;
     }
   }
+}
+
+template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op, int PD = 2>
+__global__ __launch_bounds__(256 * G) void gemm_wg(const Op op, float* __restrict__ slab,
+                                                   float* __restrict__ slab_bias,
+                                                   int m_per_split) {
+  __shared__ __attribute__((aligned(16))) T smem[gemm_wg_smem<T, BR, BC, BM, G>()];
+  gemm_wg_body<T, BR, BC, WR, WC, BM, G, Op, PD>(
+      op, slab, slab_bias, m_per_split,
+      (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)), (int)gridDim.x,
+      (int)gridDim.y, (int)gridDim.z, smem);
 }

@@ -91,12 +91,12 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 enum KernelId {
   K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
   K_LN_BWD, K_CONV3_DGRAD, K_LNC3_BWD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
-  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_COUNT
+  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
     "ln_bwd", "conv3_dgrad", "ln_bwd_conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
-    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam"};
+    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam", "fc_wgrad_fc_dgrad"};
 
 struct impala_learner {
   impala_config cfg;
@@ -122,6 +122,7 @@ struct impala_learner {
   int64_t* step;
   FusedSync fsync{};  // reduce_adam_kernel's granules, epoch counter and fault word
   bool fused_update = false;  // world_size 1: slab reduction + clip + Adam in one launch
+  bool fc_merged = true;      // FC weight + input gradients in one launch (fc_bwd_kernel)
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   // FC weight gradient in one split written straight into the canonical gradient (gemm_wg
@@ -304,6 +305,8 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     CK(hipStreamWaitEvent(ss, h->ev_fork[i], 0));
     return 0;
   };
+  // FC weight and input gradients in one launch (single stream, slab FC weight gradient)
+  const bool fc_merged = h->fc_merged && !h->fc_direct && !h->use_side && h->red_mode != 1;
   if (part == 1 || part == 4) goto part1;
   if (part == 3) goto stage_b;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
@@ -328,7 +331,18 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
       return r;
   }
   if (int r = fork(1)) return r;  // dz ready
-  if (h->fc_direct) {
+  if (fc_merged) {
+    FcWgrad<T> ow{};
+    ow.M = N; ow.x = (const T*)h->dz; ow.y = (const T*)h->y;
+    FcDgrad<T> od{N, sw + sh.wfc, (const T*)h->dz, h->dy};
+    using C = FcBwdCfg<T, WG2>;
+    const int gx = FLAT / 256, gy = HID / 64, gz = h->spfc.S;
+    const int n_rt = FLAT / C::DR, n_dt = n_rt * cdiv(N, 64);
+    if (int r = klaunch(h, K_FC_BWD, "fc_wgrad_fc_dgrad", fc_bwd_kernel<T, WG2>,
+                        dim3(gx * gy * gz + n_dt), dim3(256 * WG2), st, ow, h->s_fc, h->s_bfc,
+                        h->spfc.mps, gx, gy, gz, od, n_rt))
+      return r;
+  } else if (h->fc_direct) {
     FcWgradDirect<T> op{};
     op.M = N; op.x = (const T*)h->dz; op.y = (const T*)h->y;
     op.grads = h->grads; op.wcanon = (long long)h->cn.wfc; op.sumsq = h->sumsq_part + h->n_red_wg;
@@ -350,7 +364,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     if (h->red_mode == 1)
       if (int r = reduce_segments(h, RS_FC, RS_END, ss, 0)) return r;  // fc + heads slabs
   }
-  {
+  if (!fc_merged) {
     FcDgrad<T> op{N, sw + sh.wfc, (const T*)h->dz, h->dy};
     if (int r = klaunch(h, K_FC_DGRAD, "fc_dgrad", gemm_tile<T, 64, 64, BK(128), 2, 2, FcDgrad<T>>,
                         dim3(persist_grid(h, (long)cdiv(N, 64) * (FLAT / 64))), dim3(256), st, op,
@@ -697,6 +711,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->fsync.fault = (unsigned*)(w + o_fsync + 4);
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
+  if (const char* e = std::getenv("IMPALA_FC_MERGED")) h->fc_merged = e[0] != '0';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default

@@ -268,3 +268,31 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
   DEV int y_bytes() const { return (M / P2) * (H1 * H1 * OC1) * (int)sizeof(T); }
   DEV const T* ybase() const { return in; }
 };
+
+// FC weight gradient and FC input gradient in ONE launch.  Both read only dz (with y / Wfc), so
+// they are independent: blocks [0, gx*gy*gz) run the split weight-gradient body (gemm_wg, G
+// 4-wave groups) and the rest run the input-gradient tiles (gemm_tile with 4*G waves: 64 x 64
+// tiles for G = 1, 128 x 64 for G = 2).  The weight gradient's 96 workgroups leave most CUs
+// idle for its ~7 us; the dgrad tiles fill them instead of running after it.  Same per-tile
+// arithmetic as the two separate kernels (same tile shapes for the weight gradient).
+template <typename T, int G> struct FcBwdCfg {
+  static constexpr int DR = G == 2 ? 128 : 64, DWR = G == 2 ? 4 : 2, DBK = sizeof(T) == 2 ? 128 : 32;
+  static constexpr int SW = gemm_wg_smem<T, 64, 256, 32, G>();
+  static constexpr int SD = gemm_tile_smem<T, DR, 64, DBK, DWR, 2, FcDgrad<T>>();
+  static constexpr int SMEM = SW > SD ? SW : SD;
+};
+template <typename T, int G>
+__global__ __launch_bounds__(256 * G) void fc_bwd_kernel(const FcWgrad<T> ow, float* __restrict__ slab,
+                                                         float* __restrict__ slab_bias, int mps,
+                                                         int gx, int gy, int gz,
+                                                         const FcDgrad<T> od, int n_rtiles) {
+  using C = FcBwdCfg<T, G>;
+  __shared__ __attribute__((aligned(16))) T smem[C::SMEM];
+  const int nw = gx * gy * gz;
+  if ((int)blockIdx.x < nw)
+    gemm_wg_body<T, 64, 256, 1, 4, 32, G, FcWgrad<T>>(ow, slab, slab_bias, mps, (int)blockIdx.x,
+                                                      gx, gy, gz, smem);
+  else
+    gemm_tile_body<T, C::DR, 64, C::DBK, C::DWR, 2, FcDgrad<T>>(od, n_rtiles, (int)blockIdx.x - nw,
+                                                                (int)gridDim.x - nw, smem);
+}

@@ -25,6 +25,8 @@ def short(name):
             return tag
     if "reduce_adam_kernel" in n:
         return "reduce_adam"
+    if "fc_bwd_kernel" in n:
+        return "FcBwd"
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
     if "conv12_bwd_s2d" in n:
