@@ -69,6 +69,7 @@ def kernel_work(es):
         "fc_wgrad_fc_dgrad": (2 * 2 * 256 * 1024, 256 * es + a3 + 1024 * 4, 256 * 1024 * es),
         "conv3_wgrad": (2 * 16 * 64 * 576, a3 + a2, 0),
         "conv2_wgrad": (2 * 36 * 64 * 512, a2 + a1, 0),
+        "conv3_wgrad_conv2_wgrad": (2 * 16 * 64 * 576 + 2 * 36 * 64 * 512, a3 + 2 * a2 + a1, 0),
         # per-parameter traffic: grads, m, v, params read + written, shadow weight written
         "adam": (0, 0, 344_496 * (8 * 4 + es)),
         "reduce_grads": (0, 0, 0),
@@ -226,7 +227,7 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
                  "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "ln_bwd_conv3_dgrad": "LnConv3Bwd", "fc_wgrad": "FcWgrad",
                  "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
                  "reduce_grads": "reduce_grads", "adam": "adam", "reduce_grads_adam": "reduce_adam",
-                 "fc_wgrad_fc_dgrad": "FcBwd"}
+                 "fc_wgrad_fc_dgrad": "FcBwd", "conv3_wgrad_conv2_wgrad": "Wgrad23"}
 
 
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}

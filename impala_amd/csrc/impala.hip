@@ -91,12 +91,13 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 enum KernelId {
   K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
   K_LN_BWD, K_CONV3_DGRAD, K_LNC3_BWD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
-  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_COUNT
+  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_WGRAD23, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
     "ln_bwd", "conv3_dgrad", "ln_bwd_conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
-    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam", "fc_wgrad_fc_dgrad"};
+    "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam", "fc_wgrad_fc_dgrad",
+    "conv3_wgrad_conv2_wgrad"};
 
 struct impala_learner {
   impala_config cfg;
@@ -123,6 +124,7 @@ struct impala_learner {
   FusedSync fsync{};  // reduce_adam_kernel's granules, epoch counter and fault word
   bool fused_update = false;  // world_size 1: slab reduction + clip + Adam in one launch
   bool fc_merged = true;      // FC weight + input gradients in one launch (fc_bwd_kernel)
+  bool wg23_merged = true;    // conv3 + conv2 weight gradients in one launch (wgrad23_kernel)
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   // FC weight gradient in one split written straight into the canonical gradient (gemm_wg
@@ -307,6 +309,9 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   };
   // FC weight and input gradients in one launch (single stream, slab FC weight gradient)
   const bool fc_merged = h->fc_merged && !h->fc_direct && !h->use_side && h->red_mode != 1;
+  // conv3 + conv2 weight gradients in one launch (whole backward only: the data-parallel parts
+  // end a gradient bucket between them)
+  const bool wg23 = h->wg23_merged && (part == -1 || part == 5) && !h->use_side && h->red_mode == 0;
   if (part == 1 || part == 4) goto part1;
   if (part == 3) goto stage_b;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
@@ -392,6 +397,24 @@ stage_b:
       return r;
   }
   if (int r = fork(2)) return r;  // dact3 ready
+  if (wg23) {
+    Conv3Wgrad<T> o3{};
+    o3.M = N * P3; o3.x = (const T*)h->dact3; o3.in = (const T*)h->act2;
+    Conv2Wgrad<T> o2{};
+    o2.M = N * P2; o2.x = (const T*)h->dact2; o2.in = (const T*)h->act1;
+    if (!h->lnc3_fused) {  // dact2 comes from the separate conv3 dgrad
+      Conv3Dgrad<T> op{N * P2, sw + sh.w3, (const T*)h->dact3, (const T*)h->act2, (T*)h->dact2};
+      if (int r = klaunch(h, K_CONV3_DGRAD, "conv3_dgrad", gemm_tile<T, 64, 128, BK(64), 1, 4, Conv3Dgrad<T>>,
+                          dim3(persist_grid(h, cdiv((long)N * P2, 128))), dim3(256), st, op, 1))
+        return r;
+    }
+    const int g3x = K3 / 64, g3z = h->sp3.S, g2x = K2 / 128, g2z = h->sp2.S;
+    if (int r = klaunch(h, K_WGRAD23, "conv3_wgrad_conv2_wgrad", wgrad23_kernel<T, WG4>,
+                        dim3(g3x * g3z + g2x * g2z), dim3(256 * WG4), st, o3, h->s_w3, h->s_b3,
+                        h->sp3.mps, g3x, g3z, o2, h->s_w2, h->s_b2, h->sp2.mps, g2x, g2z))
+      return r;
+    goto conv12b;
+  }
   {
     Conv3Wgrad<T> op{};
     op.M = N * P3; op.x = (const T*)h->dact3; op.in = (const T*)h->act2;
@@ -434,6 +457,7 @@ part1:
       if (int r = reduce_segments(h, RS_CONV2, RS_END, ss, 0)) return r;
     }
   }
+conv12b:
   // conv2 input gradient (ReLU-masked) + conv1 weight gradient, fused per frame
   if (int r = klaunch(h, K_CONV12_BWD, "conv2_dgrad_conv1_wgrad", conv12_bwd_s2d<T>,
                       dim3(h->c1_wg), dim3(256 * c12_groups<T>()), st, b->obs, sw + sh.w2,
@@ -712,6 +736,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
   if (const char* e = std::getenv("IMPALA_FC_MERGED")) h->fc_merged = e[0] != '0';
+  if (const char* e = std::getenv("IMPALA_WG23_MERGED")) h->wg23_merged = e[0] != '0';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default

@@ -296,3 +296,26 @@ __global__ __launch_bounds__(256 * G) void fc_bwd_kernel(const FcWgrad<T> ow, fl
     gemm_tile_body<T, C::DR, 64, C::DBK, C::DWR, 2, FcDgrad<T>>(od, n_rtiles, (int)blockIdx.x - nw,
                                                                 (int)gridDim.x - nw, smem);
 }
+
+// conv3 and conv2 weight gradients in ONE launch (both depend only on the LayerNorm backward's
+// outputs): blocks [0, n3) run the conv3 split weight-gradient body, the rest conv2's -- the
+// same tiles, splits and group order as the two separate launches (bitwise-equal slabs), with
+// one kernel boundary fewer and conv3's tail overlapping conv2's ramp.
+template <typename T, int G> struct Wg23Cfg {
+  static constexpr int S3 = gemm_wg_smem<T, 64, 64, 32, G>(), S2 = gemm_wg_smem<T, 64, 128, 32, G>();
+  static constexpr int SMEM = S3 > S2 ? S3 : S2;
+};
+template <typename T, int G>
+__global__ __launch_bounds__(256 * G) void wgrad23_kernel(const Conv3Wgrad<T> o3, float* __restrict__ s_w3,
+                                                          float* __restrict__ s_b3, int mps3, int g3x, int g3z,
+                                                          const Conv2Wgrad<T> o2, float* __restrict__ s_w2,
+                                                          float* __restrict__ s_b2, int mps2, int g2x, int g2z) {
+  __shared__ __attribute__((aligned(16))) T smem[Wg23Cfg<T, G>::SMEM];
+  const int n3 = g3x * g3z;
+  if ((int)blockIdx.x < n3)
+    gemm_wg_body<T, 64, 64, 2, 2, 32, G, Conv3Wgrad<T>>(o3, s_w3, s_b3, mps3, (int)blockIdx.x, g3x, 1,
+                                                        g3z, smem);
+  else
+    gemm_wg_body<T, 64, 128, 1, 4, 32, G, Conv2Wgrad<T>>(o2, s_w2, s_b2, mps2, (int)blockIdx.x - n3,
+                                                         g2x, 1, g2z, smem);
+}

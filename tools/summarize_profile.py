@@ -27,6 +27,8 @@ def short(name):
         return "reduce_adam"
     if "fc_bwd_kernel" in n:
         return "FcBwd"
+    if "wgrad23_kernel" in n:
+        return "Wgrad23"
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
     if "conv12_bwd_s2d" in n:
