@@ -54,6 +54,10 @@ def kernel_work(es):
         "conv1_fwd_conv2_fwd": (2 * 225 * 32 * 192 + 2 * 36 * 64 * 512, obs + a1 + m1 + a2,
                                 (32 * 192 + 64 * 512) * es),
         "conv3_fwd": (2 * 16 * 64 * 576, a2 + 2 * a3 + 8, 64 * 576 * es + 2 * 1024 * 4),
+        # the fused trunk forward: conv1 + conv2 per frame, conv3 + LayerNorm as its tail
+        "conv1_conv2_conv3_fwd": (2 * 225 * 32 * 192 + 2 * 36 * 64 * 512 + 2 * 16 * 64 * 576,
+                                  obs + a1 + m1 + a2 + 2 * a3 + 8,
+                                  (32 * 192 + 64 * 512 + 64 * 576) * es + 2 * 1024 * 4),
         "fc_fwd": (2 * 256 * 1024, a3 + 256 * 4 + 256 * es, 256 * 1024 * es),
         "head_step": (2 * 3 * 16 * 256, 256 * es + 256 * 4 + 8 + 4 + 4 + 15 * 4 + 256 * es,
                       2 * 16 * 256 * es),
@@ -64,6 +68,11 @@ def kernel_work(es):
                                64 * 576 * es + 1024 * 4 * 2),
         "conv2_dgrad_conv1_wgrad": (2 * 36 * 64 * 512 + 2 * 225 * 32 * 192, obs + a2 + m1,
                                     64 * 512 * es),
+        # the two per-frame backward chains in one launch (dact2 written once, re-read once)
+        "ln_conv3_conv2_dgrad_conv1_wgrad": (2 * 16 * 64 * 576 + 10 * 1024 + 2 * 36 * 64 * 512 +
+                                             2 * 225 * 32 * 192,
+                                             1024 * 4 + 2 * a3 + 8 + 3 * a2 + obs + m1,
+                                             (64 * 576 + 64 * 512) * es + 1024 * 4 * 2),
         "fc_wgrad": (2 * 256 * 1024, 256 * es + a3, 0),
         # FC weight + input gradient in one launch (dz read once for both)
         "fc_wgrad_fc_dgrad": (2 * 2 * 256 * 1024, 256 * es + a3 + 1024 * 4, 256 * 1024 * es),
@@ -227,7 +236,8 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
                  "conv2_dgrad_conv1_wgrad": "Conv12Bwd", "ln_bwd_conv3_dgrad": "LnConv3Bwd", "fc_wgrad": "FcWgrad",
                  "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
                  "reduce_grads": "reduce_grads", "adam": "adam", "reduce_grads_adam": "reduce_adam",
-                 "fc_wgrad_fc_dgrad": "FcBwd", "conv3_wgrad_conv2_wgrad": "Wgrad23"}
+                 "fc_wgrad_fc_dgrad": "FcBwd", "conv3_wgrad_conv2_wgrad": "Wgrad23",
+                 "conv1_conv2_conv3_fwd": "Conv12Fwd", "ln_conv3_conv2_dgrad_conv1_wgrad": "LnConv12Bwd"}
 
 
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}

@@ -13,6 +13,7 @@
 // ds_read_b64_tr_b16 (bf16) for the weight gradient, where the reduction runs over pixels.
 #pragma once
 #include "gemm.h"
+#include "lnorm.h"
 #include "net.h"
 
 using namespace net;
@@ -197,11 +198,26 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
 // ---------------------------------------------------------------------------------------
 template <typename T> constexpr int c12f_groups() { return sizeof(T) == 2 ? 2 : 1; }
 
+// Optional conv3 + ReLU + LayerNorm tail of the fused forward (bf16): after its frames, the
+// workgroup stages W3 in LDS and computes conv3 for them from act2 kept in LDS, one wave per
+// frame, with the same k-step order and fragment layout as gemm_tile<Conv3LnFwd> and the same
+// ln_frame_epilogue, so act3 / y / stats are bit-identical to the separate conv3 launch.
+constexpr int C3T_FMAX = 6;  // frames per workgroup the tail supports (wave per frame, LDS)
+template <typename T> struct C3Tail {
+  const T* w3;       // kernel-layout W3 [64][576 = tap*64 + ci]
+  const float* b3;
+  const float* gam;  // LayerNorm gamma / beta, p*64+c order
+  const float* bet;
+  T* act3;           // nullptr: no tail (the separate conv3 launch runs)
+  T* y;
+  float* stats;
+};
+
 template <typename T>
 __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
     const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
     const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
-    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw) {
+    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3) {
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
@@ -217,7 +233,12 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
   // (16 act1 rows: wave 3's pad tile oy = 15 writes row 15, read by nobody)
   constexpr int IMGSZ = c1::FROWS * LDI, GSZ = IMGSZ + A1P * 16 * LDA1;
   constexpr bool W2REG = sizeof(T) == 2;             // bf16: conv2 weights in registers
-  __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
+  // conv3 tail (bf16): the frames' act2 in LDS rows of LDA2 elements (144 B: fewer conflicts)
+  constexpr int LDA2 = OC2 + VEC;
+  constexpr int A2SZ = W2REG ? C3T_FMAX * P2 * LDA2 : 0;
+  __shared__ __attribute__((aligned(16))) T smem[G * GSZ + A2SZ];
+  T* a2s = smem + G * GSZ;
+  const bool tail = W2REG && c3.act3 != nullptr;
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   T* img = smem + grp * GSZ;
   T* a1s = img + IMGSZ;
@@ -426,10 +447,58 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[pt][q] + bb2[q], 0.f);
           store4(act2 + ((size_t)f * P2 + pc) * OC2 + 16 * wave + 4 * (lane >> 4), v);
+          if (tail) store4(a2s + ((f - f0) * P2 + pc) * LDA2 + 16 * wave + 4 * (lane >> 4), v);
         }
       }
     }
     __syncthreads();  // the image holds the next frame; the act1 tile is free
+  }
+  if constexpr (W2REG) {
+    if (tail) {
+      // ---- conv3 + ReLU + LayerNorm of this workgroup's frames (the frame loop ended with a
+      // barrier: the image / act1 areas are free, act2 is in a2s) ----
+      constexpr int LDW3 = K3 + VEC, LDE = OC3 + 4, NT = 256 * G;
+      constexpr int NV3 = OC3 * K3 / VEC, NPT3 = (NV3 + NT - 1) / NT;
+      static_assert(OC3 * LDW3 + C3T_FMAX * P3 * LDE * 2 <= G * GSZ, "conv3 tail LDS");
+      static_assert(C3T_FMAX <= 4 * G, "one wave per frame");
+      T* w3s = smem;
+      float* ets = reinterpret_cast<float*>(smem + OC3 * LDW3);
+      V wv3[NPT3];
+#pragma unroll
+      for (int i = 0; i < NPT3; ++i) {
+        const int e = min((int)threadIdx.x + i * NT, NV3 - 1);
+        wv3[i] = *reinterpret_cast<const V*>(c3.w3 + (size_t)e * VEC);
+      }
+      const int gw = (int)threadIdx.x >> 6, nF = f1 - f0;
+      const LnLane lk = ln_lane_consts(lane, c3.b3, c3.gam, c3.bet);
+#pragma unroll
+      for (int i = 0; i < NPT3; ++i) {
+        const int e = (int)threadIdx.x + i * NT;
+        if (e < NV3) *reinterpret_cast<V*>(w3s + (e / (K3 / VEC)) * LDW3 + (e % (K3 / VEC)) * VEC) = wv3[i];
+      }
+      __syncthreads();
+      if (gw < nF) {
+        const int p = lane & 15, oy = p >> 2, ox = p & 3;
+        const T* a2f = a2s + (gw * P2 + oy * H2 + ox) * LDA2 + kl;
+        f32x4 acc3[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                         f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < K3 / KS; ++ks) {  // k = ks*32 + kl: tap = k / 64, ci = k % 64
+          const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
+          const V b = *reinterpret_cast<const V*>(a2f + (kh * H2 + kw) * LDA2 + (k & 63));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const V a = *reinterpret_cast<const V*>(w3s + (16 * i + (lane & 15)) * LDW3 + k + kl);
+            acc3[i] = F::mma(a, b, acc3[i]);
+          }
+        }
+        float* et = ets + gw * P3 * LDE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<f32x4*>(et + p * LDE + 16 * i + 4 * (lane >> 4)) = acc3[i];
+        ln_frame_epilogue<T>(et, LDE, f0 + gw, lane, lk, c3.act3, c3.y, c3.stats);
+      }
+    }
   }
 }
 
@@ -479,14 +548,23 @@ constexpr int NCELL = QG * QG;
 // on top of the one-frame register prefetch); their partials are summed in a fixed order.
 template <typename T> constexpr int c12_groups() { return sizeof(T) == 2 ? 2 : 1; }
 
+// LDS of the body (bytes): per-group image / dY1 / dY2 tiles, the ReLU mask words, bias sums
+template <typename T> struct C12BLds {
+  static constexpr int VEC = 16 / (int)sizeof(T), LDX = OC1 + VEC, LD2 = OC2 + VEC;
+  static constexpr int IMGSZ = c1::GRID * c1::GRID * c1::L<T>::LDI, DYSZ = c1::NPAD * LDX;
+  static constexpr int G = c12_groups<T>();
+  static constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;
+  static constexpr int MSK = (G * GSZ * (int)sizeof(T) + 15) / 16 * 16;
+  static constexpr int BRED = MSK + (G * c1::NPIX * 4 + 15) / 16 * 16;
+  static constexpr int BYTES = BRED + 4 * G * OC1 * 4;
+};
+
+// The kernel body, on workgroup `wg` with the LDS passed in (C12BLds<T>::BYTES)
 template <typename T>
-__global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const uint8_t* __restrict__ x,
-                                                      const T* __restrict__ w2,     // [64][512]
-                                                      const T* __restrict__ dy2,    // [N][36][64]
-                                                      const uint32_t* __restrict__ mask1,  // [N][225]
-                                                      float* __restrict__ slab,
-                                                      float* __restrict__ slab_bias, int N,
-                                                      int fpw) {
+DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2,
+                         const T* __restrict__ dy2, const uint32_t* __restrict__ mask1,
+                         float* __restrict__ slab, float* __restrict__ slab_bias, int N, int fpw,
+                         int wg, char* __restrict__ lds) {
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
@@ -500,15 +578,16 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
   constexpr int NOK = OC2 / KS;                       // k-steps per tap
   constexpr int G = c12_groups<T>();
   constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;  // elements of one group's tiles
-  __shared__ __attribute__((aligned(16))) T smem[G * GSZ];
-  __shared__ uint32_t msk_all[G][c1::NPIX];
-  __shared__ float bred[4 * G * OC1];
+  static_assert(GSZ == C12BLds<T>::GSZ, "LDS layout");
+  T* smem = reinterpret_cast<T*>(lds);
+  uint32_t (*msk_all)[c1::NPIX] = reinterpret_cast<uint32_t (*)[c1::NPIX]>(lds + C12BLds<T>::MSK);
+  float* bred = reinterpret_cast<float*>(lds + C12BLds<T>::BRED);
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   T* img = smem + grp * GSZ;
   T* dyt = img + IMGSZ;
   T* d2s = dyt + DYSZ;
   uint32_t* msk = msk_all[grp];
-  const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
+  const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   f32x4 acc[2][3];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -753,9 +832,9 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
     float bs = 0.f;
 #pragma unroll
     for (int g = 0; g < 4 * G; ++g) bs += bred[g * OC1 + tid];
-    slab_bias[(size_t)blockIdx.x * OC1 + tid] = bs;
+    slab_bias[(size_t)wg * OC1 + tid] = bs;
   }
-  const size_t so = (size_t)blockIdx.x * OC1 * K1;
+  const size_t so = (size_t)wg * OC1 * K1;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -765,4 +844,16 @@ __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const ui
       for (int q = 0; q < 4; ++q)
         slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const uint8_t* __restrict__ x,
+                                                      const T* __restrict__ w2,     // [64][512]
+                                                      const T* __restrict__ dy2,    // [N][36][64]
+                                                      const uint32_t* __restrict__ mask1,  // [N][225]
+                                                      float* __restrict__ slab,
+                                                      float* __restrict__ slab_bias, int N,
+                                                      int fpw) {
+  __shared__ __attribute__((aligned(16))) char lds[C12BLds<T>::BYTES];
+  conv12_bwd_body<T>(x, w2, dy2, mask1, slab, slab_bias, N, fpw, (int)blockIdx.x, lds);
 }

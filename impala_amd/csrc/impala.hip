@@ -91,13 +91,13 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 enum KernelId {
   K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
   K_LN_BWD, K_CONV3_DGRAD, K_LNC3_BWD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
-  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_WGRAD23, K_COUNT
+  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_WGRAD23, K_CONV123_FWD, K_LNC12_BWD, K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
     "ln_bwd", "conv3_dgrad", "ln_bwd_conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
     "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam", "fc_wgrad_fc_dgrad",
-    "conv3_wgrad_conv2_wgrad"};
+    "conv3_wgrad_conv2_wgrad", "conv1_conv2_conv3_fwd", "ln_conv3_conv2_dgrad_conv1_wgrad"};
 
 struct impala_learner {
   impala_config cfg;
@@ -125,6 +125,8 @@ struct impala_learner {
   bool fused_update = false;  // world_size 1: slab reduction + clip + Adam in one launch
   bool fc_merged = true;      // FC weight + input gradients in one launch (fc_bwd_kernel)
   bool wg23_merged = true;    // conv3 + conv2 weight gradients in one launch (wgrad23_kernel)
+  bool c3_tail = true;        // bf16: conv3 + LayerNorm as the tail of the fused conv1/conv2 forward
+  bool lc12 = true;           // LayerNorm/conv3 dgrad + conv2 dgrad/conv1 wgrad in one launch
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   // FC weight gradient in one split written straight into the canonical gradient (gemm_wg
@@ -231,11 +233,21 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;
+  bool conv3_done = false;
   if (h->fwd_fused) {  // conv1 + conv2 per frame (act1 consumed from LDS)
     const int fpw = h->c12f_fpw > 0 ? h->c12f_fpw : std::max(1, cdiv(n, h->n_cu));
-    if (int r = klaunch(h, K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>, dim3(cdiv(n, fpw)),
-                        dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1, vv + Vecs::b1,
-                        sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1, (T*)h->act2, n, fpw))
+    // bf16 with at most C3T_FMAX frames per workgroup: conv3 + ReLU + LayerNorm run as the
+    // kernel's tail (one launch for the whole conv trunk)
+    C3Tail<T> c3{};
+    if (sizeof(T) == 2 && h->c3_tail && fpw <= C3T_FMAX) {
+      c3.w3 = sw + sh.w3; c3.b3 = vv + Vecs::b3; c3.gam = vv + Vecs::lng; c3.bet = vv + Vecs::lnb;
+      c3.act3 = (T*)h->act3; c3.y = (T*)h->y; c3.stats = h->lnstat;
+      conv3_done = true;
+    }
+    if (int r = klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>,
+                        dim3(cdiv(n, fpw)), dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1,
+                        vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
+                        (T*)h->act2, n, fpw, c3))
       return r;
   } else {
     if (int r = klaunch(h, K_CONV1_FWD, "conv1_fwd", conv1_fwd_s2d<T>, dim3(min(n, h->n_cu * 4)),
@@ -246,7 +258,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
                         dim3(persist_grid(h, cdiv((long)n * P2, 128))), dim3(256), st, op, 1))
       return r;
   }
-  {
+  if (!conv3_done) {
     Conv3LnFwd<T> op{};
     op.C = n * P3; op.w = sw + sh.w3; op.b = vv + Vecs::b3; op.x = (const T*)h->act2;
     op.out = (T*)h->act3; op.gam = vv + Vecs::lng; op.bet = vv + Vecs::lnb; op.y = (T*)h->y;
@@ -312,6 +324,9 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   // conv3 + conv2 weight gradients in one launch (whole backward only: the data-parallel parts
   // end a gradient bucket between them)
   const bool wg23 = h->wg23_merged && (part == -1 || part == 5) && !h->use_side && h->red_mode == 0;
+  // the two per-frame backward chains in one launch (whole backward, same frame runs)
+  const bool lc12 = h->lc12 && h->lnc3_fused && h->ln_fpw == h->c1_fpw && (part == -1 || part == 5) &&
+                    !h->use_side && h->red_mode == 0;
   if (part == 1 || part == 4) goto part1;
   if (part == 3) goto stage_b;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
@@ -384,7 +399,15 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     return reduce_segments(h, RS_FC, RS_END, st, 0);
   }
 stage_b:
-  if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
+  if (lc12) {
+    if (int r = klaunch(h, K_LNC12_BWD, "ln_conv3_conv2_dgrad_conv1_wgrad", lnc3_conv12_bwd<T>,
+                        dim3(h->n_ln_wg), dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy,
+                        (const T*)h->act3, (const float*)h->lnstat,
+                        (const float*)(h->vecs + Vecs::lng), sw + sh.w3, (const T*)h->act2,
+                        (T*)h->dact3, (T*)h->dact2, h->s_ln, b->obs, sw + sh.w2,
+                        (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N, h->ln_fpw))
+      return r;
+  } else if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
     if (int r = klaunch(h, K_LNC3_BWD, "ln_bwd_conv3_dgrad", lnc3_bwd<T>, dim3(h->n_ln_wg),
                         dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy, (const T*)h->act3,
                         (const float*)h->lnstat, (const float*)(h->vecs + Vecs::lng), sw + sh.w3,
@@ -459,11 +482,12 @@ part1:
   }
 conv12b:
   // conv2 input gradient (ReLU-masked) + conv1 weight gradient, fused per frame
-  if (int r = klaunch(h, K_CONV12_BWD, "conv2_dgrad_conv1_wgrad", conv12_bwd_s2d<T>,
-                      dim3(h->c1_wg), dim3(256 * c12_groups<T>()), st, b->obs, sw + sh.w2,
-                      (const T*)h->dact2, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
-                      h->c1_fpw))
-    return r;
+  if (!lc12)
+    if (int r = klaunch(h, K_CONV12_BWD, "conv2_dgrad_conv1_wgrad", conv12_bwd_s2d<T>,
+                        dim3(h->c1_wg), dim3(256 * c12_groups<T>()), st, b->obs, sw + sh.w2,
+                        (const T*)h->dact2, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
+                        h->c1_fpw))
+      return r;
   // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were
   // reduced on the side stream right after their weight gradients ----
   if (part == 1 || part == 4) {
@@ -737,6 +761,8 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
   if (const char* e = std::getenv("IMPALA_FC_MERGED")) h->fc_merged = e[0] != '0';
   if (const char* e = std::getenv("IMPALA_WG23_MERGED")) h->wg23_merged = e[0] != '0';
+  if (const char* e = std::getenv("IMPALA_C3_TAIL")) h->c3_tail = e[0] != '0';
+  if (const char* e = std::getenv("IMPALA_LC12")) h->lc12 = e[0] != '0';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default

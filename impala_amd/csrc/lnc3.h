@@ -17,6 +17,7 @@
 // LN gamma / beta gradient partials are kept per lane and written as one fp32 slab per
 // workgroup (fixed-order combine of the groups), reduced by reduce_grads like the others.
 #pragma once
+#include "conv1.h"
 #include "gemm.h"
 #include "net.h"
 
@@ -28,11 +29,24 @@ constexpr int ZR = 9 * OC2 + 4;  // Z row (fp32): [tap][ci] of one output pixel,
 
 template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 1; }
 
+// LDS of the body (bytes): the W3 staging / per-group Z + dact3 tiles, then red and comb
+template <typename T> struct Lnc3Lds {
+  static constexpr int VEC = 16 / (int)sizeof(T), LD3 = OC3 + VEC, LW = K3 + VEC;
+  static constexpr int G = lnc3_groups<T>();
+  static constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
+  static constexpr bool REG = sizeof(T) == 2;
+  static constexpr int SMEM = (REG && OC3 * LW * (int)sizeof(T) > G * GB) ? OC3 * LW * (int)sizeof(T) : G * GB;
+  static constexpr int RED = SMEM, COMB = RED + G * 4 * 2 * 4, BYTES = COMB + 2 * FLAT * 4;
+};
+
+// The kernel body, on workgroup `wg` (frames wg*fpw ..) with the LDS passed in
+// (Lnc3Lds<T>::BYTES), so a launch can run it ahead of another per-frame body.
 template <typename T>
-__global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
-    const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
-    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ act2,
-    T* __restrict__ dact3, T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw) {
+DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
+                   const float* __restrict__ stats, const float* __restrict__ gam,
+                   const T* __restrict__ w3, const T* __restrict__ act2, T* __restrict__ dact3,
+                   T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw, int wg,
+                   char* __restrict__ lds) {
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
@@ -45,16 +59,15 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
   // one group's LDS: Z (fp32 [16][ZR]) then the dact3 tile (T [16][LD3]), in bytes
   constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
   constexpr bool REG = sizeof(T) == 2;               // bf16: W3 fragments in registers
-  constexpr int SMEM = (REG && OC3 * LW * (int)sizeof(T) > G * GB) ? OC3 * LW * (int)sizeof(T) : G * GB;
-  static_assert(GB % 16 == 0, "group alignment");
-  __shared__ __attribute__((aligned(16))) char smem_b[SMEM];
-  __shared__ float red[G][4][2];
-  __shared__ float comb[2 * FLAT];
+  static_assert(GB % 16 == 0 && Lnc3Lds<T>::SMEM % 16 == 0, "group alignment");
+  char* smem_b = lds;
+  float (*red)[4][2] = reinterpret_cast<float (*)[4][2]>(lds + Lnc3Lds<T>::RED);
+  float* comb = reinterpret_cast<float*>(lds + Lnc3Lds<T>::COMB);
   T* smem = reinterpret_cast<T*>(smem_b);
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   float* zs = reinterpret_cast<float*>(smem_b + grp * GB);
   T* d3s = reinterpret_cast<T*>(smem_b + grp * GB + ZB);
-  const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
+  const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = KPL * (lane >> 4);
   // this lane's LN features j = 256 w + 4 lane + q  (pixel p = j / 64, channel c = j % 64)
   const int j0 = 256 * wave + 4 * lane, p0 = j0 >> 6, c0 = j0 & 63;
@@ -217,6 +230,36 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
   }
   __syncthreads();
   for (int e = (int)threadIdx.x; e < 2 * FLAT / 4; e += 256 * G)
-    *reinterpret_cast<f32x4*>(slab + (size_t)blockIdx.x * 2 * FLAT + 4 * e) =
+    *reinterpret_cast<f32x4*>(slab + (size_t)wg * 2 * FLAT + 4 * e) =
         *reinterpret_cast<const f32x4*>(comb + 4 * e);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
+    const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
+    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ act2,
+    T* __restrict__ dact3, T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw) {
+  __shared__ __attribute__((aligned(16))) char lds[Lnc3Lds<T>::BYTES];
+  lnc3_body<T>(dy, act3, stats, gam, w3, act2, dact3, dact2, slab, N, fpw, (int)blockIdx.x, lds);
+}
+
+// LayerNorm backward + conv3 input gradient, then conv2 input gradient + conv1 weight gradient,
+// in ONE launch: both are per-frame chains over the same run of frames per workgroup, so the
+// workgroup runs lnc3_body on its frames, then conv12_bwd_body on the same frames (dact2 comes
+// back from the workgroup's own global stores, ordered by the barrier between the bodies).
+// The two bodies share the LDS (its size is the larger of theirs).  The conv3 / conv2 weight
+// gradients, which need dact3 / dact2 of all frames, run after it.
+template <typename T>
+__global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_conv12_bwd(
+    const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
+    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ act2,
+    T* __restrict__ dact3, T* __restrict__ dact2, float* __restrict__ ln_slab,
+    const uint8_t* __restrict__ x, const T* __restrict__ w2, const uint32_t* __restrict__ mask1,
+    float* __restrict__ c1_slab, float* __restrict__ c1_slab_bias, int N, int fpw) {
+  static_assert(lnc3_groups<T>() == c12_groups<T>(), "one block shape for both bodies");
+  constexpr int B1 = Lnc3Lds<T>::BYTES, B2 = C12BLds<T>::BYTES;
+  __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
+  lnc3_body<T>(dy, act3, stats, gam, w3, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
+  __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
+  conv12_bwd_body<T>(x, w2, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds);
 }

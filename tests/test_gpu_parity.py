@@ -278,6 +278,8 @@ def test_fused_update_matches_reduce_then_adam(dtype, monkeypatch):
                                        ({"IMPALA_FC_DIRECT": "1"}, False),
                                        ({"IMPALA_FC_MERGED": "0"}, True),
                                        ({"IMPALA_WG23_MERGED": "0"}, True),
+                                       ({"IMPALA_C3_TAIL": "0"}, True),
+                                       ({"IMPALA_LC12": "0"}, True),
                                        ({"IMPALA_SIDE_STREAM": "1"}, True),
                                        ({"IMPALA_FWD_FUSED": "0"}, True),
                                        ({"IMPALA_LNC3_FUSED": "0"}, False)])

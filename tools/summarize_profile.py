@@ -29,6 +29,8 @@ def short(name):
         return "FcBwd"
     if "wgrad23_kernel" in n:
         return "Wgrad23"
+    if "lnc3_conv12_bwd" in n:
+        return "LnConv12Bwd"
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
     if "conv12_bwd_s2d" in n:
