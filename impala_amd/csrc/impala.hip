@@ -323,12 +323,13 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   const bool fc_merged = h->fc_merged && !h->fc_direct && !h->use_side && h->red_mode != 1;
   // conv3 + conv2 weight gradients in one launch (whole backward only: the data-parallel parts
   // end a gradient bucket between them)
-  const bool wg23 = h->wg23_merged && (part == -1 || part == 5) && !h->use_side && h->red_mode == 0;
+  const bool whole = part == -1 || part == 5 || part == 6;  // the backward after the FC bucket
+  const bool wg23 = h->wg23_merged && whole && !h->use_side && h->red_mode == 0;
   // the two per-frame backward chains in one launch (whole backward, same frame runs)
-  const bool lc12 = h->lc12 && h->lnc3_fused && h->ln_fpw == h->c1_fpw && (part == -1 || part == 5) &&
+  const bool lc12 = h->lc12 && h->lnc3_fused && h->ln_fpw == h->c1_fpw && whole &&
                     !h->use_side && h->red_mode == 0;
   if (part == 1 || part == 4) goto part1;
-  if (part == 3) goto stage_b;
+  if (part == 3 || part == 6) goto stage_b;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
   {
     HeadArgs ha{};
@@ -490,6 +491,13 @@ conv12b:
       return r;
   // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were
   // reduced on the side stream right after their weight gradients ----
+  if (part == 6) {  // the conv + LayerNorm bucket [0, cn.wfc) + loss metrics + step
+    if (h->use_side) {
+      CK(hipEventRecord(h->ev_join, ss));
+      CK(hipStreamWaitEvent(st, h->ev_join, 0));
+    }
+    return reduce_segments(h, RS_CONV1, RS_FC, st, 1);
+  }
   if (part == 1 || part == 4) {
     if (h->use_side) {
       CK(hipEventRecord(h->ev_join, ss));
@@ -954,7 +962,7 @@ int impala_act(impala_learner* h, const uint8_t* obs, int n, const uint8_t* dete
 extern "C++" {
 namespace {
 int enqueue_grads(impala_learner* h, const impala_batch* b, hipStream_t st, int part = -1) {
-  if (part == -1 || part == 0 || part == 2 || part == 5) {
+  if (part == -1 || part == 0 || part == 2 || part == 5) {  // (parts 1, 3, 4, 6 continue a backward)
     int r = h->bf16 ? launch_forward<__bf16>(h, b->obs, h->N, st, false)
                     : launch_forward<float>(h, b->obs, h->N, st, false);
     if (r) return r;
@@ -1025,7 +1033,7 @@ int impala_compute_grads(impala_learner* h, const impala_batch* b, void* stream)
 }
 
 int impala_compute_grads_part(impala_learner* h, const impala_batch* b, int part, void* stream) {
-  if (part < 0 || part > 4) return fail(IMPALA_E_INVALID, "part must be 0..4");
+  if (part < 0 || part > 6 || part == 5) return fail(IMPALA_E_INVALID, "part must be 0..4 or 6");
   if (int r = check_bound(h)) return r;
   if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));

@@ -2,9 +2,9 @@
 
 Trajectories are independent and every loss term is a mean over (B, T-1) or (B, T), so with
 equal shards the mean of the replicas' gradients IS the full-batch gradient.  Each replica:
-``impala_compute_grads_part`` 2 / 3 / 4, each followed by an async ``all_reduce(sum)`` of the
-gradient bucket it finalised (FC + heads, conv3 + LayerNorm, conv1 + conv2), so the larger
-buckets travel while the backward continues -> ``impala_apply_update`` (x 1/world, global-norm clip on the reduced
+``impala_compute_grads_part`` 2 / 6, each followed by an async ``all_reduce(sum)`` of the
+gradient bucket it finalised (FC + heads, then conv1 .. LayerNorm), so the larger bucket
+travels while the backward continues -> ``impala_apply_update`` (x 1/world, global-norm clip on the reduced
 gradient -- identical on every replica -- and Adam).  Weights therefore stay bit-identical
 across replicas (checked by ``params_checksum``).
 """
@@ -51,18 +51,27 @@ def allreduce_grads(flat_grad: torch.Tensor, group=None) -> None:
     dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
 
 
-def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None) -> None:
-    """Local gradients of `batch` summed over replicas, in three buckets, each all-reduced as
-    soon as the backward has finalised it so that it runs on the collective stream beside the
-    rest of the backward: FC + heads (1.07 MB, after part 2: heads step, FC weight gradient and
-    dgrad) overlaps parts 3 and 4; conv3 + LayerNorm (156 KB, after part 3) overlaps part 4
-    (conv2 weight gradient, conv2 dgrad + conv1 weight gradient); conv1 + conv2 (157 KB)
-    follows part 4.  The caller's stream waits for all three before it continues
-    (apply_update)."""
+def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None,
+                             buckets: int = 2) -> None:
+    """Local gradients of `batch` summed over replicas, in buckets, each all-reduced as soon as
+    the backward has finalised it so that it runs on the collective stream beside the rest of
+    the backward.  Two buckets (default): FC + heads (1.07 MB, after part 2: heads step, FC
+    weight and input gradients) overlaps part 6 (the fused per-frame LayerNorm / conv3 / conv2
+    backward and the conv3 + conv2 weight gradients, ~60 us); conv1 .. LayerNorm (0.31 MB)
+    follows it.  Three buckets (the unfused kernels): FC + heads after part 2, conv3 +
+    LayerNorm after part 3, conv1 + conv2 after part 4.  The caller's stream waits for all of
+    them before it continues (apply_update)."""
     import torch.distributed as dist
     engine.compute_grads_part(2, *batch)
     off_fc, off = engine.bucket_offset_fc, engine.bucket_offset
     w_fc = dist.all_reduce(flat_grad[off_fc:], op=dist.ReduceOp.SUM, group=group, async_op=True)
+    if buckets == 2:
+        engine.compute_grads_part(6, *batch)
+        w_rest = dist.all_reduce(flat_grad[:off_fc], op=dist.ReduceOp.SUM, group=group,
+                                 async_op=True)
+        w_fc.wait()
+        w_rest.wait()
+        return
     engine.compute_grads_part(3, *batch)
     w_c3 = dist.all_reduce(flat_grad[off:off_fc], op=dist.ReduceOp.SUM, group=group,
                            async_op=True)

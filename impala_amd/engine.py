@@ -233,7 +233,8 @@ class Engine:
         """A piece of compute_grads.  Two buckets: part 0 finishes grads[bucket_offset:]
         (conv3 .. heads), part 1 (same batch) grads[:bucket_offset] (conv1, conv2) and the
         metrics.  Three buckets: part 2 finishes grads[bucket_offset_fc:] (FC, heads), part 3
-        grads[bucket_offset:bucket_offset_fc] (conv3, LayerNorm), part 4 = part 1."""
+        grads[bucket_offset:bucket_offset_fc] (conv3, LayerNorm), part 4 = part 1.  Two buckets
+        on the fused per-frame backward: part 2, then part 6 grads[:bucket_offset_fc] + metrics."""
         b = self._batch(*batch)
         if part in (0, 2):
             self._sync_weights(stream)

@@ -171,7 +171,11 @@ size_t impala_grad_bucket_offset(const impala_learner* h);
  * gradient, FC dgrad) leaves grads[impala_grad_bucket_offset_fc(h) ..] -- FC and heads, 1.07 MB
  * of the 1.38 MB -- final; part 3 (same batch: LayerNorm backward, conv3 dgrad and weight
  * gradient) finalises [impala_grad_bucket_offset(h), impala_grad_bucket_offset_fc(h)); part 4
- * = part 1.  Parts 2, 3, 4 give bit-identical grads to impala_compute_grads. */
+ * = part 1.  Parts 2, 3, 4 give bit-identical grads to impala_compute_grads.
+ * Two buckets with the fused per-frame backward: part 2, then part 6 (same batch: the fused
+ * LayerNorm / conv3 / conv2 input gradients + conv1 weight gradient, the conv3 + conv2 weight
+ * gradients) finalises [0, impala_grad_bucket_offset_fc(h)) and the metrics.  Parts 2, 6 give
+ * bit-identical grads to impala_compute_grads. */
 size_t impala_grad_bucket_offset_fc(const impala_learner* h);
 
 /* Replay gather (agents/impala/builder.py:30-36 UniformSampler.sample + learning.py:121-123

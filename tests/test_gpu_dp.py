@@ -72,6 +72,13 @@ def test_grad_parts_match_whole_backward(dtype):
     np.testing.assert_array_equal(m3.flat_grad.cpu().numpy(), g_whole)
     np.testing.assert_array_equal(e3.metrics.cpu().numpy(), met_whole)
     assert off_fc == off + 36864 + 64 + 2 * 1024  # + conv3 + LayerNorm
+    # two buckets on the fused per-frame backward: part 2, then part 6 finishes the rest
+    m4, e4 = _setup(dev, 8, dtype=dtype)
+    e4.compute_grads_part(2, *batch)
+    e4.compute_grads_part(6, *batch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m4.flat_grad.cpu().numpy(), g_whole)
+    np.testing.assert_array_equal(e4.metrics.cpu().numpy(), met_whole)
 
 
 def _free_port():
