@@ -13,6 +13,10 @@ using namespace net;
 // over __shfl_down: after the step with offset d every lane holds the composition of the maps
 // t .. t+2d-1, so log2(S) shuffle rounds give e_t on every lane (S = segment size <= 64).
 // (rlax/rlego vtrace_td_error_and_advantage; agents/impala/learning.py:15-26,150-153.)
+// Return order (pg_advantage, td_error, q_estimate): taken from the reference's unpacking
+// `adv, err, _ =` (learning.py:150); rlax's published VTraceOutput lists (errors,
+// pg_advantage, q_estimate).  rlego itself is absent, so this order is an unpinned assumption
+// pinned only by the reference's own call sites.
 // =========================================================================================
 DEV float seg_rev_scan(float a, float b, int t, int L, int S) {
   for (int d = 1; d < S; d <<= 1) {
