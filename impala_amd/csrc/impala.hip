@@ -127,6 +127,10 @@ struct impala_learner {
   bool wg23_merged = true;    // conv3 + conv2 weight gradients in one launch (wgrad23_kernel)
   bool c3_tail = true;        // bf16: conv3 + LayerNorm as the tail of the fused conv1/conv2 forward
   bool lc12 = true;           // LayerNorm/conv3 dgrad + conv2 dgrad/conv1 wgrad in one launch
+  // the already-final slabs reduced inside the conv wgrad launch (opt-in IMPALA_EARLY_RED=1):
+  // bitwise equal, but the merged launch grew by 5.5 us and reduce_grads shrank by only 2 us
+  // (0.1214 / 0.1225 vs 0.1195 ms, reduction blocks last / first)
+  bool early_red = false;
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   // FC weight gradient in one split written straight into the canonical gradient (gemm_wg
@@ -286,7 +290,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
 }
 
 // slab-reduction segment groups (indices into RedArgs::seg, in the order create() adds them)
-enum { RS_CONV1 = 0, RS_CONV2 = 2, RS_CONV3 = 4, RS_FC = 7, RS_END = 11 };
+enum { RS_CONV1 = 0, RS_CONV2 = 2, RS_CONV3 = 4, RS_LN = 6, RS_FC = 7, RS_END = 11 };
 
 int reduce_segments(impala_learner* h, int s_lo, int s_hi, hipStream_t st, int fin) {
   const int n = h->red.wg_start[s_hi] - h->red.wg_start[s_lo];
@@ -329,6 +333,10 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   // the two per-frame backward chains in one launch (whole backward, same frame runs)
   const bool lc12 = h->lc12 && h->lnc3_fused && h->ln_fpw == h->c1_fpw && whole &&
                     !h->use_side && h->red_mode == 0;
+  // with the per-frame backward fused ahead of the merged conv weight gradients, every slab
+  // but conv2 / conv3 is final when the latter start: reduce those inside that launch
+  // (not for part 5: the fused reduce + Adam reduces every unit itself)
+  const bool early = h->early_red && lc12 && wg23 && part != 5;
   if (part == 1 || part == 4) goto part1;
   if (part == 3 || part == 6) goto stage_b;
   // ---- fused head: heads fwd, log-softmax / V-trace / loss, dz, heads weight gradient ----
@@ -434,10 +442,22 @@ stage_b:
         return r;
     }
     const int g3x = K3 / 64, g3z = h->sp3.S, g2x = K2 / 128, g2z = h->sp2.S;
-    if (int r = klaunch(h, K_WGRAD23, "conv3_wgrad_conv2_wgrad", wgrad23_kernel<T, WG4>,
-                        dim3(g3x * g3z + g2x * g2z), dim3(256 * WG4), st, o3, h->s_w3, h->s_b3,
-                        h->sp3.mps, g3x, g3z, o2, h->s_w2, h->s_b2, h->sp2.mps, g2x, g2z))
+    if (early) {
+      // conv1 + b1 and LayerNorm (+ FC and heads unless part 2 reduced them) units ride along
+      const int* ws = h->red.wg_start;
+      const int u0 = ws[RS_CONV1], n0 = ws[RS_CONV2] - ws[RS_CONV1];
+      const int u1 = ws[RS_LN], n1 = (part == 6 ? ws[RS_FC] : ws[RS_END]) - ws[RS_LN];
+      if (int r = klaunch(h, K_WGRAD23, "conv3_wgrad_conv2_wgrad", wgrad23r_kernel<T, WG4>,
+                          dim3(g3x * g3z + g2x * g2z + cdiv(n0 + n1, WG4)), dim3(256 * WG4), st,
+                          o3, h->s_w3, h->s_b3, h->sp3.mps, g3x, g3z, o2, h->s_w2, h->s_b2,
+                          h->sp2.mps, g2x, g2z, h->red, u0, n0, u1, n1))
+        return r;
+    } else if (int r = klaunch(h, K_WGRAD23, "conv3_wgrad_conv2_wgrad", wgrad23_kernel<T, WG4>,
+                               dim3(g3x * g3z + g2x * g2z), dim3(256 * WG4), st, o3, h->s_w3,
+                               h->s_b3, h->sp3.mps, g3x, g3z, o2, h->s_w2, h->s_b2, h->sp2.mps,
+                               g2x, g2z)) {
       return r;
+    }
     goto conv12b;
   }
   {
@@ -497,7 +517,7 @@ conv12b:
       CK(hipEventRecord(h->ev_join, ss));
       CK(hipStreamWaitEvent(st, h->ev_join, 0));
     }
-    return reduce_segments(h, RS_CONV1, RS_FC, st, 1);
+    return early ? reduce_segments(h, RS_CONV2, RS_LN, st, 1) : reduce_segments(h, RS_CONV1, RS_FC, st, 1);
   }
   if (part == 1 || part == 4) {
     if (h->use_side) {
@@ -512,7 +532,11 @@ conv12b:
       CK(hipStreamWaitEvent(st, h->ev_join, 0));
     }
     if (part == 5) return 0;  // the fused update kernel reduces the slabs
-    if (int r = reduce_segments(h, RS_CONV1, RS_END, st, 1)) return r;
+    if (early) {  // conv1, LayerNorm, FC and heads were reduced beside the conv weight gradients
+      if (int r = reduce_segments(h, RS_CONV2, RS_LN, st, 1)) return r;
+    } else if (int r = reduce_segments(h, RS_CONV1, RS_END, st, 1)) {
+      return r;
+    }
   } else {
     if (int r = reduce_segments(h, RS_CONV1, RS_CONV2, st, 1)) return r;
     if (h->use_side) {  // join
@@ -772,6 +796,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   if (const char* e = std::getenv("IMPALA_WG23_MERGED")) h->wg23_merged = e[0] != '0';
   if (const char* e = std::getenv("IMPALA_C3_TAIL")) h->c3_tail = e[0] != '0';
   if (const char* e = std::getenv("IMPALA_LC12")) h->lc12 = e[0] != '0';
+  if (const char* e = std::getenv("IMPALA_EARLY_RED")) h->early_red = e[0] == '1';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default

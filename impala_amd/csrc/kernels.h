@@ -4,6 +4,7 @@
 #include "common.h"
 #include "conv1.h"
 #include "net.h"
+#include "ops.h"
 
 using namespace net;
 
@@ -575,41 +576,92 @@ DEV void adam_scalars(const RedArgs& a, int64_t t, float& step_size, float& bc2s
   bc2s = (float)sqrt(bc2);
 }
 
-// One reduction unit = one workgroup of reduce_grads_kernel (global index `wg`): the SG split
-// groups' sums are combined in LDS; threads of split group 0 whose column is in range get the 4
-// reduced values and their canonical indices (-1: padding / out of range).  Returns the
-// thread's sum-of-squares contribution (in element order).
-DEV float reduce_unit(const RedArgs& a, int wg, f32x4* part, f32x4& acc, long long (&ci)[4]) {
-  int s = 0;
-  while (wg >= a.wg_start[s + 1]) ++s;
-  const RedSeg& sg = a.seg[s];
-  const int SG = sg.sg, cols = 256 / SG;
-  const int col = threadIdx.x % cols, grp = threadIdx.x / cols;
-  const int v4 = (wg - a.wg_start[s]) * cols + col;  // float4 index in the segment
-  const bool in = v4 * 4 < sg.count;
-  acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (in) {
+// One reduction unit = one workgroup of reduce_grads_kernel (global index `u`), on 256 threads
+// (`tid`): reduce_unit_sum gives each thread the sum of its split group, which the caller puts
+// in part[tid]; after a barrier reduce_unit_finish combines the SG split groups from LDS --
+// threads of split group 0 whose column is in range get the 4 reduced values and their
+// canonical indices (-1: padding / out of range) -- and returns the thread's sum of squares.
+struct RedUnit {
+  int s, SG, cols, col, grp, v4;
+  bool in;
+};
+DEV RedUnit reduce_unit_at(const RedArgs& a, int u, int tid) {
+  RedUnit r;
+  r.s = 0;
+  while (u >= a.wg_start[r.s + 1]) ++r.s;
+  const RedSeg& sg = a.seg[r.s];
+  r.SG = sg.sg;
+  r.cols = 256 / r.SG;
+  r.col = tid % r.cols;
+  r.grp = tid / r.cols;
+  r.v4 = (u - a.wg_start[r.s]) * r.cols + r.col;  // float4 index in the segment
+  r.in = r.v4 * 4 < sg.count;
+  return r;
+}
+DEV f32x4 reduce_unit_sum(const RedArgs& a, const RedUnit& r) {
+  const RedSeg& sg = a.seg[r.s];
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (r.in) {
     // R split loads in flight per round, R = 8 or 16 by the splits this thread sums (one
     // round for every segment at the default split-group rule)
-    const float* p = sg.slab + (size_t)v4 * 4;
-    acc = (sg.S + SG - 1) / SG <= 8 ? sum_splits<8>(p, grp, SG, sg.S, sg.count)
-                                    : sum_splits<16>(p, grp, SG, sg.S, sg.count);
+    const float* p = sg.slab + (size_t)r.v4 * 4;
+    acc = (sg.S + r.SG - 1) / r.SG <= 8 ? sum_splits<8>(p, r.grp, r.SG, sg.S, sg.count)
+                                        : sum_splits<16>(p, r.grp, r.SG, sg.S, sg.count);
   }
-  part[threadIdx.x] = acc;
-  __syncthreads();
+  return acc;
+}
+DEV float reduce_unit_finish(const RedArgs& a, const RedUnit& r, const f32x4* part, f32x4& acc,
+                             long long (&ci)[4]) {
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) ci[i] = -1;
-  if (grp == 0 && in) {
-    for (int g2 = 1; g2 < SG; ++g2) acc += part[g2 * cols + col];
-    const int k = v4 * 4;
+  if (r.grp == 0 && r.in) {
+    for (int g2 = 1; g2 < r.SG; ++g2) acc += part[g2 * r.cols + r.col];
+    const int k = r.v4 * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ci[i] = canon_index(a, sg, k + i);
+      ci[i] = canon_index(a, a.seg[r.s], k + i);
       if (ci[i] >= 0) sq += acc[i] * acc[i];
     }
   }
   return sq;
+}
+DEV float reduce_unit(const RedArgs& a, int wg, f32x4* part, f32x4& acc, long long (&ci)[4]) {
+  const RedUnit r = reduce_unit_at(a, wg, (int)threadIdx.x);
+  acc = reduce_unit_sum(a, r);
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  return reduce_unit_finish(a, r, part, acc, ci);
+}
+
+// Reduction units run by extra blocks of another launch (one unit per 256-thread quarter of a
+// 256*Q-thread block; u < 0: the quarter has none but still takes part in the barriers).  Same
+// arithmetic and sum-of-squares slot (the unit's global index) as reduce_grads_kernel.
+template <int Q>
+DEV void reduce_units_quarters(const RedArgs& a, int u, f32x4* part_all, float* red_all) {
+  const int q = (int)threadIdx.x >> 8, tid = (int)threadIdx.x & 255;
+  f32x4* part = part_all + q * 256;
+  float* red = red_all + q * 4;
+  RedUnit r{};
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (u >= 0) {
+    r = reduce_unit_at(a, u, tid);
+    acc = reduce_unit_sum(a, r);
+  }
+  part[tid] = acc;
+  __syncthreads();
+  long long ci[4];
+  float sq = 0.f;
+  if (u >= 0) {
+    sq = reduce_unit_finish(a, r, part, acc, ci);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (ci[i] >= 0) a.grads[ci[i]] = acc[i];
+  }
+  sq = wave_sum(sq);
+  if ((tid & 63) == 0) red[tid >> 6] = sq;
+  __syncthreads();
+  if (u >= 0 && tid == 0) a.sumsq_part[u] = red[0] + red[1] + red[2] + red[3];
 }
 
 // Each segment is processed by workgroups of 256 threads = (256/SG) float4 columns x SG
@@ -1035,5 +1087,36 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
     const long long nw = rb >> 2;
     for (long long v = threadIdx.x; v < nw; v += 256)
       reinterpret_cast<float*>(d)[v] = reinterpret_cast<const float*>(s)[v];
+  }
+}
+
+// conv3 + conv2 weight gradients (wgrad23_kernel's blocks) plus the reduction units of the
+// slabs that are already final when they start -- conv1 / LayerNorm (the per-frame backward)
+// and FC / heads -- as extra blocks, one unit per 256-thread quarter: the conv weight
+// gradients' second round of blocks leaves CUs free, and the final reduce_grads launch keeps
+// only the conv2 / conv3 units.  Units are the global indices [u0, u0 + n0) then [u1, u1 + n1).
+template <typename T, int G>
+__global__ __launch_bounds__(256 * G) void wgrad23r_kernel(
+    const Conv3Wgrad<T> o3, float* __restrict__ s_w3, float* __restrict__ s_b3, int mps3, int g3x,
+    int g3z, const Conv2Wgrad<T> o2, float* __restrict__ s_w2, float* __restrict__ s_b2, int mps2,
+    int g2x, int g2z, const RedArgs ra, int u0, int n0, int u1, int n1) {
+  constexpr int SM = Wg23Cfg<T, G>::SMEM * (int)sizeof(T);
+  constexpr int SR = G * 256 * 16 + G * 4 * 4;
+  __shared__ __attribute__((aligned(16))) char lds[SM > SR ? SM : SR];
+  // the reduction blocks first: they are short, and the weight-gradient blocks fill the CUs
+  // they free
+  const int nr = (n0 + n1 + G - 1) / G;
+  const int n3 = g3x * g3z, n2 = g2x * g2z, b = (int)blockIdx.x - nr;
+  if (b < 0) {
+    const int i = (int)blockIdx.x * G + ((int)threadIdx.x >> 8);
+    const int u = i < n0 ? u0 + i : (i - n0 < n1 ? u1 + i - n0 : -1);
+    reduce_units_quarters<G>(ra, u, reinterpret_cast<f32x4*>(lds),
+                             reinterpret_cast<float*>(lds + G * 256 * 16));
+  } else if (b < n3) {
+    gemm_wg_body<T, 64, 64, 2, 2, 32, G, Conv3Wgrad<T>>(o3, s_w3, s_b3, mps3, b, g3x, 1, g3z,
+                                                        reinterpret_cast<T*>(lds));
+  } else if (b < n3 + n2) {
+    gemm_wg_body<T, 64, 128, 1, 4, 32, G, Conv2Wgrad<T>>(o2, s_w2, s_b2, mps2, b - n3, g2x, 1, g2z,
+                                                         reinterpret_cast<T*>(lds));
   }
 }

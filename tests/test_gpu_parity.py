@@ -280,6 +280,7 @@ def test_fused_update_matches_reduce_then_adam(dtype, monkeypatch):
                                        ({"IMPALA_WG23_MERGED": "0"}, True),
                                        ({"IMPALA_C3_TAIL": "0"}, True),
                                        ({"IMPALA_LC12": "0"}, True),
+                                       ({"IMPALA_EARLY_RED": "1"}, True),
                                        ({"IMPALA_SIDE_STREAM": "1"}, True),
                                        ({"IMPALA_FWD_FUSED": "0"}, True),
                                        ({"IMPALA_LNC3_FUSED": "0"}, False)])
