@@ -33,7 +33,13 @@ template <> struct L<float> { static constexpr int LDI = 52; };
 // reach row 256).  With grid-indexed tiles the 16 lanes of a B fragment read 16 consecutive
 // rows, so 96-byte rows (bf16, no padding) make every ds_read_b128 conflict-free
 // (tools/ldsbank.py: 1.00x, against 2.80x for pixel-indexed tiles on 112-byte rows).
+// Backward (conv12_bwd) tile pitches, from tools/ldsbank.py: s2d image rows of 52 bf16 (frame
+// stash 1.00x vs 2.00x at 56), dY1 rows of 36 (its masked stores 1.88x vs 3.75x at 40), dY2
+// cell rows of 80 (its ds_read_b128 2.00x vs 3.00x at 72)
 namespace c1 {
+template <typename T> struct LB;
+template <> struct LB<__bf16> { static constexpr int LDI = 52, LDX = 36, LD2 = 80; };
+template <> struct LB<float> { static constexpr int LDI = 52, LDX = 36, LD2 = 68; };
 template <typename T> struct LF;
 template <> struct LF<__bf16> { static constexpr int LDI = 48; };
 template <> struct LF<float> { static constexpr int LDI = 52; };
@@ -62,9 +68,8 @@ DEV void c1_load_frame(const uint8_t* __restrict__ frame, int tid, uint4 v[3]) {
 #pragma unroll
   for (int i = 0; i < 3; ++i) v[i] = reinterpret_cast<const uint4*>(frame)[tid + i * 256];
 }
-template <typename T>
+template <typename T, int LDI = c1::L<T>::LDI>
 DEV void c1_stash_frame(T* img, int tid, const uint4 v[3]) {
-  constexpr int LDI = c1::L<T>::LDI;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int vi = tid + i * 256, ci = vi >> 8, yy = (vi & 255) >> 2, xq = vi & 3;
@@ -550,8 +555,8 @@ template <typename T> constexpr int c12_groups() { return sizeof(T) == 2 ? 2 : 1
 
 // LDS of the body (bytes): per-group image / dY1 / dY2 tiles, the ReLU mask words, bias sums
 template <typename T> struct C12BLds {
-  static constexpr int VEC = 16 / (int)sizeof(T), LDX = OC1 + VEC, LD2 = OC2 + VEC;
-  static constexpr int IMGSZ = c1::GRID * c1::GRID * c1::L<T>::LDI, DYSZ = c1::NPAD * LDX;
+  static constexpr int VEC = 16 / (int)sizeof(T), LDX = c1::LB<T>::LDX, LD2 = c1::LB<T>::LD2;
+  static constexpr int IMGSZ = c1::GRID * c1::GRID * c1::LB<T>::LDI, DYSZ = c1::NPAD * LDX;
   static constexpr int G = c12_groups<T>();
   static constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;
   static constexpr int MSK = (G * GSZ * (int)sizeof(T) + 15) / 16 * 16;
@@ -568,10 +573,10 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
-  constexpr int LDI = c1::L<T>::LDI;
+  constexpr int LDI = c1::LB<T>::LDI;
   constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int LDX = OC1 + VEC;                      // dY1 tile row (elements)
-  constexpr int LD2 = OC2 + VEC;                      // dY2 cell row (elements)
+  constexpr int LDX = c1::LB<T>::LDX;                 // dY1 tile row (elements)
+  constexpr int LD2 = c1::LB<T>::LD2;                 // dY2 cell row (elements)
   constexpr int IMGSZ = c1::GRID * c1::GRID * LDI, DYSZ = c1::NPAD * LDX;
   constexpr int D2V = P2 * OC2 / VEC;                 // 16-byte vectors of one dY2 frame
   constexpr int ND2 = (D2V + 255) / 256;
@@ -657,11 +662,14 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
         }
     }
   }
-  // zero the dY1 padding rows 225..255 and the dY2 cell grid once (the border stays zero)
-  static_assert((c1::NPAD - c1::NPIX) * LDX % VEC == 0 && c12::NCELL * LD2 % VEC == 0 &&
-                c1::NPIX * LDX % VEC == 0, "16-byte zero fill");
-  for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX / VEC; e += 256)
-    *reinterpret_cast<V*>(dyt + c1::NPIX * LDX + e * VEC) = F::zero();
+  // zero the dY1 padding rows 225..255 and the dY2 cell grid once (the border stays zero);
+  // the dY1 pad rows in 4-element pieces (rows of 36 elements start 8-byte aligned)
+  static_assert((c1::NPAD - c1::NPIX) * LDX % 4 == 0 && c12::NCELL * LD2 % VEC == 0 &&
+                c1::NPIX * LDX % 4 == 0 && LDX % 4 == 0, "zero fill");
+  for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX / 4; e += 256) {
+    const float z[4] = {0.f, 0.f, 0.f, 0.f};
+    store4(dyt + c1::NPIX * LDX + e * 4, z);
+  }
   for (int e = tid; e < c12::NCELL * LD2 / VEC; e += 256)
     *reinterpret_cast<V*>(d2s + e * VEC) = F::zero();
   const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDI;
@@ -672,7 +680,7 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
     const bool active = f < f1;
     __syncthreads();  // the previous frame's readers are done
     if (active) {
-    c1_stash_frame<T>(img, tid, nv);
+    c1_stash_frame<T, LDI>(img, tid, nv);
 #pragma unroll
     for (int i = 0; i < ND2; ++i) {
       const int e = tid + i * 256;
