@@ -54,6 +54,11 @@ def kernel_work(es):
         "conv1_fwd_conv2_fwd": (2 * 225 * 32 * 192 + 2 * 36 * 64 * 512, obs + a1 + m1 + a2,
                                 (32 * 192 + 64 * 512) * es),
         "conv3_fwd": (2 * 16 * 64 * 576, a2 + 2 * a3 + 8, 64 * 576 * es + 2 * 1024 * 4),
+        # the trunk forward and the FC forward in one launch (flag hand-off of y)
+        "conv123_fwd_fc_fwd": (2 * 225 * 32 * 192 + 2 * 36 * 64 * 512 + 2 * 16 * 64 * 576 +
+                               2 * 256 * 1024,
+                               obs + a1 + m1 + a2 + 2 * a3 + 8 + a3 + 256 * 4 + 256 * es,
+                               (32 * 192 + 64 * 512 + 64 * 576 + 256 * 1024) * es + 2 * 1024 * 4),
         # the fused trunk forward: conv1 + conv2 per frame, conv3 + LayerNorm as its tail
         "conv1_conv2_conv3_fwd": (2 * 225 * 32 * 192 + 2 * 36 * 64 * 512 + 2 * 16 * 64 * 576,
                                   obs + a1 + m1 + a2 + 2 * a3 + 8,
@@ -237,7 +242,8 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
                  "conv3_wgrad": "Conv3Wgrad", "conv2_wgrad": "Conv2Wgrad",
                  "reduce_grads": "reduce_grads", "adam": "adam", "reduce_grads_adam": "reduce_adam",
                  "fc_wgrad_fc_dgrad": "FcBwd", "conv3_wgrad_conv2_wgrad": "Wgrad23",
-                 "conv1_conv2_conv3_fwd": "Conv12Fwd", "ln_conv3_conv2_dgrad_conv1_wgrad": "LnConv12Bwd"}
+                 "conv1_conv2_conv3_fwd": "Conv12Fwd", "ln_conv3_conv2_dgrad_conv1_wgrad": "LnConv12Bwd",
+                 "conv123_fwd_fc_fwd": "FwdChain"}
 
 
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}

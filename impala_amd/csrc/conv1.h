@@ -216,13 +216,26 @@ template <typename T> struct C3Tail {
   T* act3;           // nullptr: no tail (the separate conv3 launch runs)
   T* y;
   float* stats;
+  int y_sc1;         // y stored write-through (read by other workgroups of the same launch)
 };
 
+// LDS of the forward body (elements of T)
+template <typename T> struct C12FLds {
+  static constexpr int VEC = 16 / (int)sizeof(T), LDA1 = OC1 + VEC, A1P = 22;
+  static constexpr int IMGSZ = c1::FROWS * c1::LF<T>::LDI, GSZ = IMGSZ + A1P * 16 * LDA1;
+  static constexpr int LDA2 = OC2 + VEC;
+  static constexpr int A2SZ = sizeof(T) == 2 ? C3T_FMAX * P2 * LDA2 : 0;
+  static constexpr int ELEMS = c12f_groups<T>() * GSZ + A2SZ;
+};
+
+// The kernel body on workgroup `wg` (frames wg*fpw ..) with the LDS passed in
+// (C12FLds<T>::ELEMS elements)
 template <typename T>
-__global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
-    const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
-    const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
-    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3) {
+DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1,
+                         const float* __restrict__ b1, const T* __restrict__ w2,
+                         const float* __restrict__ b2, T* __restrict__ act1,
+                         uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw,
+                         const C3Tail<T>& c3, int wg, T* __restrict__ smem) {
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
@@ -241,13 +254,13 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
   // conv3 tail (bf16): the frames' act2 in LDS rows of LDA2 elements (144 B: fewer conflicts)
   constexpr int LDA2 = OC2 + VEC;
   constexpr int A2SZ = W2REG ? C3T_FMAX * P2 * LDA2 : 0;
-  __shared__ __attribute__((aligned(16))) T smem[G * GSZ + A2SZ];
+  static_assert(G * GSZ + A2SZ == C12FLds<T>::ELEMS && GSZ == C12FLds<T>::GSZ, "LDS layout");
   T* a2s = smem + G * GSZ;
   const bool tail = W2REG && c3.act3 != nullptr;
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   T* img = smem + grp * GSZ;
   T* a1s = img + IMGSZ;
-  const int f0 = blockIdx.x * fpw, f1 = min(N, f0 + fpw);
+  const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = KPL * (lane >> 4);
   uint4 nv[3];
   if (f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, tid, nv);
@@ -501,10 +514,22 @@ __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           *reinterpret_cast<f32x4*>(et + p * LDE + 16 * i + 4 * (lane >> 4)) = acc3[i];
-        ln_frame_epilogue<T>(et, LDE, f0 + gw, lane, lk, c3.act3, c3.y, c3.stats);
+        if (c3.y_sc1)
+          ln_frame_epilogue<T, true>(et, LDE, f0 + gw, lane, lk, c3.act3, c3.y, c3.stats);
+        else
+          ln_frame_epilogue<T>(et, LDE, f0 + gw, lane, lk, c3.act3, c3.y, c3.stats);
       }
     }
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
+    const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
+    const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
+    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3) {
+  __shared__ __attribute__((aligned(16))) T smem[C12FLds<T>::ELEMS];
+  conv12_fwd_body<T>(x, w1, b1, w2, b2, act1, mask, act2, N, fpw, c3, (int)blockIdx.x, smem);
 }
 
 // ---------------------------------------------------------------------------------------

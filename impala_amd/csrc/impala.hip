@@ -91,13 +91,15 @@ Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
 enum KernelId {
   K_CONV1_FWD = 0, K_CONV2_FWD, K_CONV12_FWD, K_CONV3_FWD, K_FC_FWD, K_HEADS_FWD, K_HEAD_STEP, K_FC_DGRAD,
   K_LN_BWD, K_CONV3_DGRAD, K_LNC3_BWD, K_FC_WGRAD, K_CONV3_WGRAD, K_CONV2_WGRAD, K_CONV12_BWD, K_REDUCE,
-  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_WGRAD23, K_CONV123_FWD, K_LNC12_BWD, K_COUNT
+  K_SUMSQ, K_ADAM, K_REDUCE_ADAM, K_FC_BWD, K_WGRAD23, K_CONV123_FWD, K_LNC12_BWD, K_FWD_CHAIN,
+  K_COUNT
 };
 const char* const kKernelNames[K_COUNT] = {
     "conv1_fwd", "conv2_fwd", "conv1_fwd_conv2_fwd", "conv3_fwd", "fc_fwd", "heads_fwd", "head_step", "fc_dgrad",
     "ln_bwd", "conv3_dgrad", "ln_bwd_conv3_dgrad", "fc_wgrad", "conv3_wgrad", "conv2_wgrad",
     "conv2_dgrad_conv1_wgrad", "reduce_grads", "sumsq", "adam", "reduce_grads_adam", "fc_wgrad_fc_dgrad",
-    "conv3_wgrad_conv2_wgrad", "conv1_conv2_conv3_fwd", "ln_conv3_conv2_dgrad_conv1_wgrad"};
+    "conv3_wgrad_conv2_wgrad", "conv1_conv2_conv3_fwd", "ln_conv3_conv2_dgrad_conv1_wgrad",
+    "conv123_fwd_fc_fwd"};
 
 struct impala_learner {
   impala_config cfg;
@@ -131,6 +133,12 @@ struct impala_learner {
   // bitwise equal, but the merged launch grew by 5.5 us and reduce_grads shrank by only 2 us
   // (0.1214 / 0.1225 vs 0.1195 ms, reduction blocks last / first)
   bool early_red = false;
+  // trunk forward + FC forward in one launch with per-producer flags (fwd_chain_kernel,
+  // opt-in IMPALA_FWD_CHAIN=1): bitwise equal, but 30.6 us against 22.8 + 5.8 us -- the FC
+  // tiles only start on CUs the conv workgroups free, all at the end (step 0.1202 vs 0.1180 ms)
+  bool fwd_chain = false;
+  unsigned* chain_flags = nullptr;  // [N] one word per conv workgroup
+  unsigned chain_epoch = 0;
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
   // FC weight gradient in one split written straight into the canonical gradient (gemm_wg
@@ -247,6 +255,24 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
       c3.w3 = sw + sh.w3; c3.b3 = vv + Vecs::b3; c3.gam = vv + Vecs::lng; c3.bet = vv + Vecs::lnb;
       c3.act3 = (T*)h->act3; c3.y = (T*)h->y; c3.stats = h->lnstat;
       conv3_done = true;
+    }
+    // training forward (no heads launch after it): the FC forward joins the launch, each FC
+    // tile waiting on flags of the conv workgroups that produce its frames (not under graph
+    // capture: the epoch argument changes every launch)
+    if (conv3_done && !with_heads && h->fwd_chain && !h->use_graph) {
+      if (++h->chain_epoch == 0) h->chain_epoch = 1;
+      c3.y_sc1 = 1;
+      using CC = FwdChainCfg<T>;
+      FcFwd<T> fop{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->zg, (T*)h->h};
+      const int n_conv = cdiv(n, fpw), n_fc = (HID / CC::FR) * cdiv(n, CC::FC);
+      if constexpr (sizeof(T) == 2) {
+        if (int r = klaunch(h, K_FWD_CHAIN, "conv123_fwd_fc_fwd", fwd_chain_kernel<T>,
+                            dim3(n_conv + n_fc), dim3(512), st, obs, sw + sh.w1, vv + Vecs::b1,
+                            sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1, (T*)h->act2, n, fpw,
+                            c3, n_conv, fop, h->chain_flags, h->chain_epoch, h->fsync.fault))
+          return r;
+      }
+      return 0;
     }
     if (int r = klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>,
                         dim3(cdiv(n, fpw)), dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1,
@@ -759,6 +785,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t o_step = take(8);
   const size_t o_gran = take((size_t)h->n_red_wg * 8);  // fused update granules (upper bound)
   const size_t o_fsync = take(16);                       // epoch counter, fault word
+  const size_t o_chain = take((size_t)N * 4);            // forward-chain producer flags
   h->ws_bytes = off;
   hipError_t e = hipMalloc(&h->ws, off);
   if (e != hipSuccess) {
@@ -790,6 +817,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->fsync.gran = (unsigned long long*)(w + o_gran);
   h->fsync.epoch_ctr = (unsigned*)(w + o_fsync);
   h->fsync.fault = (unsigned*)(w + o_fsync + 4);
+  h->chain_flags = (unsigned*)(w + o_chain);
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
   if (const char* e = std::getenv("IMPALA_FC_MERGED")) h->fc_merged = e[0] != '0';
@@ -797,6 +825,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   if (const char* e = std::getenv("IMPALA_C3_TAIL")) h->c3_tail = e[0] != '0';
   if (const char* e = std::getenv("IMPALA_LC12")) h->lc12 = e[0] != '0';
   if (const char* e = std::getenv("IMPALA_EARLY_RED")) h->early_red = e[0] == '1';
+  if (const char* e = std::getenv("IMPALA_FWD_CHAIN")) h->fwd_chain = e[0] == '1';
   // hipGraph replay of whole steps (opt-in): it cuts the host enqueue cost of a step ~3x, but
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default

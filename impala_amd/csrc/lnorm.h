@@ -24,7 +24,9 @@ DEV LnLane ln_lane_consts(int lane, const float* b3, const float* gam, const flo
 
 // One wavefront per frame.  et: fp32 conv3 accumulators of the frame, [16 px][ldt]
 // channels-contiguous.  Writes act3 = relu(acc + b3), y = LN(act3) and (mean, rstd).
-template <typename T>
+// Y_SC1 (bf16): y is stored write-through (8-byte agent-scope atomic stores = sc1), the payload
+// form another workgroup of the same launch may read after a flag (fwd_chain_kernel).
+template <typename T, bool Y_SC1 = false>
 DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const LnLane& k,
                            T* act3, T* y, float* stats) {
   using namespace net;
@@ -49,7 +51,14 @@ DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const 
     for (int q = 0; q < 4; ++q)
       yy[q] = (v[i + q] - mean) * rstd * k.g[i + q] + k.e[i + q];
     store4(act3 + o + i, v + i);
-    store4(y + o + i, yy);
+    if constexpr (Y_SC1 && sizeof(T) == 2) {
+      const unsigned long long w = (unsigned long long)(unsigned)pack_bf16x2(yy[0], yy[1]) |
+                                   ((unsigned long long)(unsigned)pack_bf16x2(yy[2], yy[3]) << 32);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(y + o + i), w, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      store4(y + o + i, yy);
+    }
   }
   if (lane == 0) {
     stats[2 * frame] = mean;

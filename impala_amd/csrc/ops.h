@@ -5,6 +5,7 @@
 // Activations are channels-last (pixel-major, channel-contiguous); frame n = b*T + t
 // (batch-major flatten of agents/impala/learning.py:143).
 #pragma once
+#include "conv1.h"
 #include "gemm.h"
 #include "lnorm.h"
 #include "net.h"
@@ -318,4 +319,66 @@ __global__ __launch_bounds__(256 * G) void wgrad23_kernel(const Conv3Wgrad<T> o3
   else
     gemm_wg_body<T, 64, 128, 1, 4, 32, G, Conv2Wgrad<T>>(o2, s_w2, s_b2, mps2, (int)blockIdx.x - n3,
                                                          g2x, 1, g2z, smem);
+}
+
+// The trunk forward and the FC forward in ONE launch (bf16, conv3 tail on): blocks [0, n_conv)
+// run the per-frame conv1 / conv2 / conv3+LayerNorm body and publish a flag each; the FC tile
+// blocks after them (64 hidden units x 32 frames, 8 waves, one tile per block) wait only for
+// the conv blocks that produce their 32 frames of y, then run the FC body.  Hand-off
+// (MI355X_MICROARCH.md, inter-workgroup visibility, R1): the producer stores y write-through
+// (sc1), every storing wave drains, and one lane stores flag = epoch (relaxed, agent); the
+// consumer polls relaxed, acquires at agent scope once, then a barrier, then plain loads.  The FC blocks are dispatched after every
+// conv block, so a waiting block never holds a slot a producer needs; the poll is bounded (a
+// timeout sets *fault and continues).  epoch changes every launch (never 0).
+template <typename T> struct FwdChainCfg {
+  static constexpr int FR = 64, FC = 32, FK = 256, FWR = 4, FWC = 2;  // FC tile, 8 waves
+  static constexpr int SD = gemm_tile_smem<T, FR, FC, FK, FWR, FWC, FcFwd<T>>();
+  static constexpr int SMEM = C12FLds<T>::ELEMS > SD ? C12FLds<T>::ELEMS : SD;
+};
+template <typename T>
+__global__ __launch_bounds__(512) void fwd_chain_kernel(
+    const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
+    const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
+    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3,
+    int n_conv, const FcFwd<T> fc, unsigned* __restrict__ flags, unsigned epoch,
+    unsigned* __restrict__ fault) {
+  static_assert(c12f_groups<T>() == 2, "512-thread conv body (bf16)");
+  using C = FwdChainCfg<T>;
+  __shared__ __attribute__((aligned(16))) T smem[C::SMEM];
+  const int b = (int)blockIdx.x;
+  if (b < n_conv) {
+    // y is the only payload the FC blocks read; c3.y_sc1 stores it write-through, so the
+    // publish is: every storing wave drains, a barrier, one lane stores the flag (R1)
+    conv12_fwd_body<T>(x, w1, b1, w2, b2, act1, mask, act2, N, fpw, c3, b, smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // FC tile of this block (gemm_tile_body's tile order: row tile fastest)
+  const int vb = b - n_conv, vg = (int)gridDim.x - n_conv;
+  const int n_rt = HID / C::FR;
+  const int t = xcd_swizzle(vb, vg);
+  const int c0 = (t / n_rt) * C::FC;
+  if (threadIdx.x < 64) {  // wave 0: lane i polls producer p0 + i
+    const int p0 = c0 / fpw, p1 = (min(N, c0 + C::FC) - 1) / fpw;
+    const int p = p0 + (int)threadIdx.x;
+    bool ok = p > p1 ||
+              __hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+    for (unsigned spins = 0; !__all(ok); ++spins) {
+      if (spins > (1u << 22)) {  // ~0.1 s: a producer never finished; do not hang the GPU
+        if (threadIdx.x == 0) __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      ok = ok || __hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+    }
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  gemm_tile_body<T, C::FR, C::FC, C::FK, C::FWR, C::FWC, FcFwd<T>>(fc, n_rt, vb, vg, smem);
 }

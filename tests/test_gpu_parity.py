@@ -279,6 +279,7 @@ def test_fused_update_matches_reduce_then_adam(dtype, monkeypatch):
                                        ({"IMPALA_FC_MERGED": "0"}, True),
                                        ({"IMPALA_WG23_MERGED": "0"}, True),
                                        ({"IMPALA_C3_TAIL": "0"}, True),
+                                       ({"IMPALA_FWD_CHAIN": "1"}, True),
                                        ({"IMPALA_LC12": "0"}, True),
                                        ({"IMPALA_EARLY_RED": "1"}, True),
                                        ({"IMPALA_SIDE_STREAM": "1"}, True),

@@ -31,6 +31,8 @@ def short(name):
         return "Wgrad23"
     if "lnc3_conv12_bwd" in n:
         return "LnConv12Bwd"
+    if "fwd_chain_kernel" in n:
+        return "FwdChain"
     if "conv1_fwd_s2d" in n:
         return "Conv1Fwd"
     if "conv12_bwd_s2d" in n:
