@@ -200,12 +200,27 @@ __global__ __launch_bounds__(256) void loss_head_kernel(const LossArgs a, TO* __
 }
 
 // metrics[0..5] = loss, entropy, td, pg, kl, ratio from the loss-head partial sums
-DEV void finalize_loss_metrics(const float* part, int nparts, int B, int T, float ent_coef,
-                               float* metrics) {
-  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int p = 0; p < nparts; ++p)
+// Sum the per-workgroup partials [nparts][8] (first K values) across one wavefront: lane l
+// sums partials l, l + 64, ... in order, then a fixed butterfly over the lanes -- every lane
+// ends with the same totals (a one-thread load-add loop would be one L2 round trip per partial).
+template <int K>
+DEV void sum_partials(const float* part, int nparts, int lane, float (&s)[K]) {
+  for (int p = lane; p < nparts; p += 64) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(part + (size_t)p * 8);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(part + (size_t)p * 8 + 4);
 #pragma unroll
-    for (int k = 0; k < 5; ++k) s[k] += part[p * 8 + k];
+    for (int k = 0; k < K; ++k) s[k] += k < 4 ? a[k] : b[k - 4];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) s[k] = wave_sum(s[k]);
+}
+
+// (called by a whole wavefront; lane 0 writes the metrics)
+DEV void finalize_loss_metrics(const float* part, int nparts, int B, int T, float ent_coef,
+                               float* metrics, int lane) {
+  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  sum_partials<5>(part, nparts, lane, s);
+  if (lane != 0) return;
   const float c_pg = 1.f / (float)(B * (T - 1)), c_ent = 1.f / (float)(B * T);
   const float pg = s[0] * c_pg, td = s[1] * c_pg, ent = s[2] * c_ent;
   metrics[0] = -pg + td - ent_coef * ent;
@@ -218,7 +233,7 @@ DEV void finalize_loss_metrics(const float* part, int nparts, int B, int T, floa
 
 __global__ void finalize_loss_kernel(const float* part, int nparts, int B, int T, float ent_coef,
                                      float* metrics) {
-  if (threadIdx.x == 0) finalize_loss_metrics(part, nparts, B, T, ent_coef, metrics);
+  if (threadIdx.x < 64) finalize_loss_metrics(part, nparts, B, T, ent_coef, metrics, (int)threadIdx.x);
 }
 
 // =========================================================================================
@@ -244,11 +259,10 @@ DEV PpoFrame ppo_frame(float r, float v, float tgt, float lo, float hi) {
 // metrics from PPO partial sums (pg_l, adv^2, H, KL, r, target): slots 0..5 as IMPALA
 // (loss, entropy, td, pg, kl, ratio) and slot 8 = train/target; kl is clamp_min(0)'d
 DEV void finalize_ppo_metrics(const float* part, int nparts, int N, float ent_coef,
-                              float* metrics) {
+                              float* metrics, int lane) {
   float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int p = 0; p < nparts; ++p)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s[k] += part[p * 8 + k];
+  sum_partials<6>(part, nparts, lane, s);
+  if (lane != 0) return;
   const float c = 1.f / (float)N;
   const float pg = s[0] * c, td = 0.5f * (s[1] * c), ent = s[2] * c;
   metrics[0] = pg + td - ent_coef * ent;
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(256) void ppo_loss_head_kernel(
 
 __global__ void finalize_ppo_kernel(const float* part, int nparts, int N, float ent_coef,
                                     float* metrics9) {
-  if (threadIdx.x == 0) finalize_ppo_metrics(part, nparts, N, ent_coef, metrics9);
+  if (threadIdx.x < 64) finalize_ppo_metrics(part, nparts, N, ent_coef, metrics9, (int)threadIdx.x);
 }
 
 
@@ -685,11 +699,11 @@ __global__ __launch_bounds__(256) void reduce_grads_kernel(const RedArgs a, int 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
   __syncthreads();
   if (threadIdx.x == 0) a.sumsq_part[wg] = red[0] + red[1] + red[2] + red[3];
-  if (fin && blockIdx.x == 0 && threadIdx.x == 64) {
+  if (fin && blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {  // wave 1
     if (a.algo == 1)
-      finalize_ppo_metrics(a.loss_part, a.n_loss_part, a.B * a.T, a.ent_coef, a.metrics);
+      finalize_ppo_metrics(a.loss_part, a.n_loss_part, a.B * a.T, a.ent_coef, a.metrics, threadIdx.x & 63);
     else
-      finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
+      finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics, threadIdx.x & 63);
   }
   if (fin && blockIdx.x == 0 && threadIdx.x == 128) {  // step += 1 and its bias corrections
     const int64_t t = *a.step + 1;
@@ -894,11 +908,11 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const RedArgs a, const
   }
   const unsigned epoch = s_epoch;
   const int64_t t = (int64_t)s_step + 1;
-  if (blockIdx.x == 0 && threadIdx.x == 64) {
+  if (blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {  // wave 1
     if (a.algo == 1)
-      finalize_ppo_metrics(a.loss_part, a.n_loss_part, a.B * a.T, a.ent_coef, a.metrics);
+      finalize_ppo_metrics(a.loss_part, a.n_loss_part, a.B * a.T, a.ent_coef, a.metrics, threadIdx.x & 63);
     else
-      finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics);
+      finalize_loss_metrics(a.loss_part, a.n_loss_part, a.B, a.T, a.ent_coef, a.metrics, threadIdx.x & 63);
   }
   // step size and bias correction (double pow) by one lane, while the others start sweeping
   __shared__ float s_sc[2];
