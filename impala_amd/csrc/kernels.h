@@ -786,6 +786,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     }
   }
   const float step_size = a.sc[0], bc2s = a.sc[1];
+  const int64_t step = a.step[0];  // for metrics[7] (block 0), loaded with everything else
   float sq = 0.f;  // partials are zero-padded to a multiple of 4 (see impala_create)
   // 4 float4 partial loads in flight per thread (unconditional, clamped; out-of-range ones
   // dropped by a select), same summation order as one at a time
@@ -804,7 +805,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.f);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.metrics[6] = norm;
-    a.metrics[7] = (float)*a.step;
+    a.metrics[7] = (float)step;
   }
   if (n == 0) return;
   const float gscale = a.inv_world * coef;
