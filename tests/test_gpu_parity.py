@@ -318,6 +318,31 @@ def test_launch_modes_agree(env, exact, monkeypatch):
         np.testing.assert_allclose(base[1], alt[1], rtol=1e-2, atol=3e-3)
 
 
+@pytest.mark.parametrize("B,T", [(24, 64), (160, 20)])
+def test_merged_launches_at_other_frame_runs(B, T, monkeypatch):
+    """The merged / fused launches against the separate ones, bitwise, where the per-workgroup
+    frame run differs from C2's 5: N = 1536 (6 frames per workgroup, the conv3 tail's limit)
+    and N = 3200 (13: the tail is off, the fused backward and merged GEMMs stay on)."""
+    dev = _dev()
+    batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(B, T, 15, seed=77)]
+
+    def run():
+        m = _model(dev, "bf16", seed=0)
+        e = _engine(m, B, T)
+        for _ in range(2):
+            e.train_step(*batch)
+        torch.cuda.synchronize()
+        return m.flat.cpu().numpy().copy(), e.metrics.cpu().numpy().copy()
+
+    base = run()
+    for k in ("IMPALA_C3_TAIL", "IMPALA_LC12", "IMPALA_WG23_MERGED", "IMPALA_FC_MERGED"):
+        monkeypatch.setenv(k, "0")
+    alt = run()
+    np.testing.assert_array_equal(base[0], alt[0])
+    np.testing.assert_array_equal(base[1], alt[1])
+    assert np.isfinite(base[1]).all()
+
+
 def test_full_size_bf16_step_properties():
     """B=64, T=20 (BASELINE config 2): finite, loss decreases on a repeated batch,
     grad norm positive, params move by <= ~lr per step (Adam bound)."""
