@@ -9,9 +9,7 @@ d = json.loads(open("gpurun_out/envab.json").read().strip().splitlines()[-1])
 print(f"{sys.argv[1]:40s} {d['ms_per_step']:.4f} ms  " + " ".join(f"{a}={b}" for a, b in d["kernel_us"].items()))
 PY
 }
+SETS=${ENV_SETS:-"X=base HIP_FORCE_DEV_KERNARG=0 IMPALA_GRAPH=1"}
 for r in 1 2; do
-  run X=base
-  run HIP_FORCE_DEV_KERNARG=1
-  run HIP_FORCE_DEV_KERNARG=0
-  run IMPALA_GRAPH=1
+  for e in $SETS; do run $e; done
 done
