@@ -77,6 +77,24 @@ DEV Frag<float>::vec lds_frag_k(const float* tile, int ld, int lane) {
   const float* a0 = tile + 4 * (lane >> 4) * ld + (lane & 15);
   return f32x4{a0[0], a0[ld], a0[2 * ld], a0[3 * ld]};
 }
+// The same fragment from a tile whose rows are stored bit-2 / bit-3 swapped (wg_row): the
+// 32 lanes of one transposing read then cover physical rows 0..7 (logical 0..3 and 8..11),
+// and with a row pitch of 16 k + 16 elements, k even (row step = 8 mod 16 dwords), their
+// 8-dword pieces tile the 64 banks (tools/ldsbank.py: 2.0x -> 1.0x).  A plain pitch cannot:
+// rows r and r + 8 of the read are 8 pitches apart, which is 0 or 32 dwords mod 64 and
+// either lands on the same banks or breaks the 8-dword alignment of the other rows.
+DEV int wg_row(int r) { return (r & ~12) | ((r >> 2) & 1) << 3 | ((r >> 3) & 1) << 2; }
+DEV Frag<__bf16>::vec lds_frag_k_sw(const __bf16* tile, int ld, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const __bf16* a0 = tile + (q + 4 * (g & 1) + 16 * (g >> 1)) * ld + 4 * pp;
+  const bf16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+  const bf16x4_t y = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0 + 8 * ld));
+  Frag<__bf16>::vec v;
+  v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+  v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
+  return v;
+}
+DEV Frag<float>::vec lds_frag_k_sw(const float* tile, int ld, int lane) { return lds_frag_k(tile, ld, lane); }
 
 // epilogue operand types of a gemm_tile op: per-tile Epi for store(), or per-workgroup
 // EpiConst for a TILE_EPI tile_epilogue()
@@ -296,10 +314,13 @@ template <class Op> struct wg_direct<Op, decltype(void(Op::DIRECT))> {
 };
 // The body runs as virtual workgroup `lin` of a gx x gy x gz grid on 256 * G threads, with the
 // LDS passed in (gemm_wg_smem elements).
+// bf16 rows are stored bit-2/3 swapped (wg_row) at a pitch of BR / BC + 16 (conflict-free
+// transposing fragment reads); fp32 rows in order at + 4.
+template <typename T> constexpr int wg_pad() { return sizeof(T) == 2 ? 16 : 4; }
+template <typename T> DEV int wg_prow(int r) { if constexpr (sizeof(T) == 2) return wg_row(r); else return r; }
 template <typename T, int BR, int BC, int BM, int G>
 constexpr int gemm_wg_smem() {
-  constexpr int VEC = 16 / (int)sizeof(T);
-  return (BM * (BR + VEC) + BM * (BC + VEC)) * 2 * G;
+  return (BM * (BR + wg_pad<T>()) + BM * (BC + wg_pad<T>())) * 2 * G;
 }
 template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op, int PD = 2>
 DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict__ slab_bias,
@@ -307,7 +328,7 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
   using F = Frag<T>;
   typedef typename F::vec V;  // 16 bytes of T
   constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int LDX = BR + VEC, LDY = BC + VEC;
+  constexpr int LDX = BR + wg_pad<T>(), LDY = BC + wg_pad<T>();
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NACC = TRW * TCW * 4;
   constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per buffer
@@ -384,12 +405,12 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       const int e = tid + i * 256, mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
-      if (e < NXV) *reinterpret_cast<V*>(Xs + mm * LDX + rr) = rx[d][i];
+      if (e < NXV) *reinterpret_cast<V*>(Xs + wg_prow<T>(mm) * LDX + rr) = rx[d][i];
     }
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
       const int v = tid + i * 256;
-      if (v < NYV) *reinterpret_cast<V*>(Ys + (v / YV) * LDY + (v % YV) * VEC) = ry[d][i];
+      if (v < NYV) *reinterpret_cast<V*>(Ys + wg_prow<T>(v / YV) * LDY + (v % YV) * VEC) = ry[d][i];
     }
   };
   const int n_it = (m_end - m_beg + BM * G - 1) / (BM * G);
@@ -422,7 +443,7 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
           const int rch = tid % BR, rg = tid / BR;
           float s0 = 0.f;
 #pragma unroll
-          for (int mm = rg; mm < BM; mm += RG) s0 += (float)Xs[mm * LDX + rch];
+          for (int mm = rg; mm < BM; mm += RG) s0 += (float)Xs[wg_prow<T>(mm) * LDX + rch];
           bias_acc += s0;
         }
 #pragma unroll
@@ -430,10 +451,10 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
           V a[TRW], b[TCW];
 #pragma unroll
           for (int i = 0; i < TRW; ++i)
-            a[i] = lds_frag_k(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
+            a[i] = lds_frag_k_sw(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
 #pragma unroll
           for (int j = 0; j < TCW; ++j)
-            b[j] = lds_frag_k(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
+            b[j] = lds_frag_k_sw(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
 #pragma unroll
           for (int i = 0; i < TRW; ++i)
 #pragma unroll
