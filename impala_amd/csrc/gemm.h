@@ -121,10 +121,15 @@ template <class Op> struct EpiTypes<Op, true> {
 // Requires K % BK == 0, R % BR == 0 and no A dependence on columns inside one BC tile.
 // The body runs on NT = 64 * WR * WC threads as virtual workgroup `vbid` of `vgrid`, with the
 // LDS passed in (gemm_tile_smem elements), so a launch can host it beside another body.
+// bf16 rows are padded by 16 elements: the k-contiguous ds_read_b128 fragment reads are then
+// conflict-free (row step 8 mod 64 dwords; + 8 is 2.0x by tools/ldsbank.py), and the k-major
+// A tile also stores its rows bit-2/3 swapped for the transposing read (wg_row).
+template <typename T> DEV int wg_prow(int r) { if constexpr (sizeof(T) == 2) return wg_row(r); else return r; }
+template <typename T> constexpr int tile_pad() { return sizeof(T) == 2 ? 16 : 4; }
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
 constexpr int gemm_tile_smem() {
-  constexpr int VEC = 16 / (int)sizeof(T), LD = BK + VEC;
-  constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + VEC) : BR * LD;
+  constexpr int LD = BK + tile_pad<T>();
+  constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + tile_pad<T>()) : BR * LD;
   return 2 * (ASZ + BC * LD);
 }
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
@@ -135,11 +140,11 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   typedef typename F::vec V;
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int KV = BK / VEC;            // 16-byte vectors per tile row per chunk
-  constexpr int LD = BK + VEC;            // padded row (elements)
+  constexpr int LD = BK + tile_pad<T>();  // padded row (elements)
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NA = BR * KV / NT, NB = BC * KV / NT;
   constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
-  constexpr int LDA = AK ? BR + VEC : LD; // A tile row length (elements)
+  constexpr int LDA = AK ? BR + tile_pad<T>() : LD;  // A tile row length (elements)
   constexpr int ASZ = AK ? BK * LDA : BR * LD;
   constexpr int NK = Op::K / BK;
   static_assert((WR * WC == 4 || (WR * WC == 8 && !Op::TILE_EPI)) && TRW >= 1 && TCW >= 1, "tile");
@@ -191,7 +196,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int e = tid + i * NT, kr = e / RV, rv = e % RV;
-        *reinterpret_cast<V*>(As + kr * LDA + rv * VEC) = ra[i];
+        *reinterpret_cast<V*>(As + wg_prow<T>(kr) * LDA + rv * VEC) = ra[i];
       }
     } else {
 #pragma unroll
@@ -241,7 +246,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 #pragma unroll
         for (int i = 0; i < TRW; ++i) {
           if constexpr (AK)
-            a[i] = lds_frag_k(As + kk * LDA + (wr * TRW + i) * 16, LDA, lane);
+            a[i] = lds_frag_k_sw(As + kk * LDA + (wr * TRW + i) * 16, LDA, lane);
           else
             a[i] = *reinterpret_cast<const V*>(As + ((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl);
         }
@@ -317,7 +322,6 @@ template <class Op> struct wg_direct<Op, decltype(void(Op::DIRECT))> {
 // bf16 rows are stored bit-2/3 swapped (wg_row) at a pitch of BR / BC + 16 (conflict-free
 // transposing fragment reads); fp32 rows in order at + 4.
 template <typename T> constexpr int wg_pad() { return sizeof(T) == 2 ? 16 : 4; }
-template <typename T> DEV int wg_prow(int r) { if constexpr (sizeof(T) == 2) return wg_row(r); else return r; }
 template <typename T, int BR, int BC, int BM, int G>
 constexpr int gemm_wg_smem() {
   return (BM * (BR + wg_pad<T>()) + BM * (BC + wg_pad<T>())) * 2 * G;
