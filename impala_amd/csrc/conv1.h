@@ -475,7 +475,9 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
     if (tail) {
       // ---- conv3 + ReLU + LayerNorm of this workgroup's frames (the frame loop ended with a
       // barrier: the image / act1 areas are free, act2 is in a2s) ----
-      constexpr int LDW3 = K3 + VEC, LDE = OC3 + 4, NT = 256 * G;
+      // W3 rows of 592 (row step 8 mod 64 dwords: the k-contiguous b128 reads are conflict-free
+      // by tools/ldsbank.py; 584 is 2.0x)
+      constexpr int LDW3 = K3 + 2 * VEC, LDE = OC3 + 4, NT = 256 * G;
       constexpr int NV3 = OC3 * K3 / VEC, NPT3 = (NV3 + NT - 1) / NT;
       static_assert(OC3 * LDW3 + C3T_FMAX * P3 * LDE * 2 <= G * GSZ, "conv3 tail LDS");
       static_assert(C3T_FMAX <= 4 * G, "one wave per frame");

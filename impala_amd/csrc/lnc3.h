@@ -31,7 +31,7 @@ template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 
 
 // LDS of the body (bytes): the W3 staging / per-group Z + dact3 tiles, then red and comb
 template <typename T> struct Lnc3Lds {
-  static constexpr int VEC = 16 / (int)sizeof(T), LD3 = OC3 + VEC, LW = K3 + VEC;
+  static constexpr int VEC = 16 / (int)sizeof(T), LD3 = OC3 + 2 * VEC, LW = K3 + VEC;
   static constexpr int G = lnc3_groups<T>();
   static constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
   static constexpr bool REG = sizeof(T) == 2;
@@ -51,7 +51,7 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
   constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int LD3 = OC3 + VEC;                     // dact3 row (elements)
+  constexpr int LD3 = OC3 + 2 * VEC;                 // dact3 row (80 bf16: conflict-free b128 reads)
   constexpr int LW = K3 + VEC;                       // staged W3 row
   constexpr int NKS = K3 / KS;
   constexpr int NKO = OC3 / KS;                      // k-steps per tap (K = oc)
