@@ -14,10 +14,13 @@ replicas, B=64 per GPU (weak scaling), one flat fp32 gradient bucket all-reduced
 Also reported, all from the same run:
 * ``roofline`` / ``roofline_top2``: the two kernels with algorithmic work that take longest
   (chosen from every kernel's average over --steps untimed steps, ``kernel_us``), each timed
-  live over the timed steps by hipExtLaunchKernel start/stop events (the kernel's own begin /
-  end stamps, the duration rocprofv3's kernel trace reports): algorithmic FLOPs or bytes /
-  that duration vs the dense MFMA or HBM peak, plus the PMC-measured HBM traffic per launch
-  from the newest matching profiles/*/summary.json;
+  live by hipExtLaunchKernel start/stop events (the kernel's own begin / end stamps, the
+  duration rocprofv3's kernel trace reports) over a second run of --steps steps right after
+  the timed region: algorithmic FLOPs or bytes / that duration vs the dense MFMA or HBM peak,
+  plus the PMC-measured HBM traffic per launch from the newest matching
+  profiles/*/summary.json.  The stamped run is separate because an event pair on a launch
+  costs the step ≈4.7 µs (tools/stamp_cost.py: 105 µs unstamped, 115 µs with two kernels
+  stamped, 143 µs with all eight); its step time is reported as ``ms_per_step_stamped``;
 * ``step_roofline``: SURVEY.md §8(d)'s step-level figure, frames/s x 17.74 MFLOP/frame vs
   the dense MFMA peak;
 * ``fp32_parity_mode``: the same workload in fp32 (the reference's arithmetic);
@@ -558,7 +561,8 @@ def main():
     torch.cuda.synchronize()
     work = kernel_work(2 if args.dtype == "bf16" else 4)
     kernel_us, top = select_kernels(eng, step, work, args)
-    elapsed, k_times = timed_steps(eng, step, top, args, dist, dev)
+    elapsed, _ = timed_steps(eng, step, [], args, dist, dev)  # the headline: no stamps
+    elapsed_st, k_times = timed_steps(eng, step, top, args, dist, dev)
     met = eng.metrics.cpu().numpy()
     if not np.all(np.isfinite(met)):
         raise RuntimeError(f"non-finite metrics {met}")
@@ -588,6 +592,7 @@ def main():
         "roofline_top2": rooflines,
         "step_roofline": step_roofline(value / world, step_flops_pf, args.dtype),
         "kernel_us": kernel_us,
+        "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
     }
     if not args.no_fp32_line and args.dtype == "bf16":
         out["fp32_parity_mode"] = fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo)
@@ -703,10 +708,12 @@ def fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo):
     work = kernel_work(4)
     table, top = select_kernels(e, step, work, argparse.Namespace(steps=args.steps,
                                                                    roofline_kernel=None))
-    elapsed, k_times = timed_steps(e, step, top[:1], args, dist, dev)
+    elapsed, _ = timed_steps(e, step, [], args, dist, dev)
+    elapsed_st, k_times = timed_steps(e, step, top[:1], args, dist, dev)
     value = world * B * T * args.steps / elapsed
     out = {"dtype": "fp32", "value": round(value, 1), "unit": "env-frames/s",
            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+           "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
            "step_roofline": step_roofline(value / world, STEP_FLOPS_PER_FRAME if not ppo
                                           else STEP_FLOPS_PER_FRAME_PPO, "fp32"),
            "roofline": kernel_roofline(top[0], k_times[top[0]], work, B * T, "fp32", args.algo),

@@ -285,7 +285,8 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
   V wa2[W2REG ? NKS2 : 1];
   if constexpr (W2REG) {
-    constexpr int LW1 = K1 + VEC, LW2 = K2 + VEC, NT = 256 * G;
+    // rows padded by 16 (row step 8 mod 32 dwords): conflict-free b128 fragment reads
+    constexpr int LW1 = K1 + 2 * VEC, LW2 = K2 + 2 * VEC, NT = 256 * G;
     constexpr int NV1 = OC1 * K1 / VEC, NV2 = OC2 * K2 / VEC;
     static_assert(OC1 * LW1 + OC2 * LW2 <= G * GSZ, "weight staging");
     T* w1s = smem;
@@ -645,9 +646,10 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
   const int py = wave >> 1, px = wave & 1;
   V wa[4][2][NOK];  // [tap j1*2+j2][ci tile][k-step]: A[ci][oc] = W2[oc][kh][kw][ci]
   if constexpr (sizeof(T) == 2) {
-    // bf16: W2 [64][512] staged through LDS with 16-byte loads (rows padded to 520), the
-    // fragments (k = oc along the lane's 8 values) read with the transposing LDS read
-    constexpr int LDW = K2 + VEC, NWV = OC2 * K2 / VEC, NT = 256 * G, NPT = NWV / NT;
+    // bf16: W2 [64][512] staged through LDS with 16-byte loads (rows padded to 528 and stored
+    // bit-2/3 swapped, wg_row), the fragments (k = oc along the lane's 8 values) read with the
+    // transposing LDS read, conflict-free
+    constexpr int LDW = K2 + 2 * VEC, NWV = OC2 * K2 / VEC, NT = 256 * G, NPT = NWV / NT;
     static_assert(NWV % NT == 0 && OC2 * LDW <= G * GSZ, "w2 staging");
     T* w2s = smem;
     V wv[NPT];
@@ -659,7 +661,7 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int e = (int)threadIdx.x + i * NT, row = e / (K2 / VEC), c = (e % (K2 / VEC)) * VEC;
-      *reinterpret_cast<V*>(w2s + row * LDW + c) = wv[i];
+      *reinterpret_cast<V*>(w2s + wg_row(row) * LDW + c) = wv[i];
     }
     __syncthreads();
 #pragma unroll
@@ -669,7 +671,7 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int ks = 0; ks < NOK; ++ks)
-          wa[t][i][ks] = lds_frag_k(w2s + ks * KS * LDW + (kh * KS2 + kw) * OC1 + 16 * i, LDW, lane);
+          wa[t][i][ks] = lds_frag_k_sw(w2s + ks * KS * LDW + (kh * KS2 + kw) * OC1 + 16 * i, LDW, lane);
     }
     __syncthreads();  // the staging area becomes the frame tiles
   } else {

@@ -31,7 +31,7 @@ template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 
 
 // LDS of the body (bytes): the W3 staging / per-group Z + dact3 tiles, then red and comb
 template <typename T> struct Lnc3Lds {
-  static constexpr int VEC = 16 / (int)sizeof(T), LD3 = OC3 + 2 * VEC, LW = K3 + VEC;
+  static constexpr int VEC = 16 / (int)sizeof(T), LD3 = OC3 + 2 * VEC, LW = K3 + 2 * VEC;
   static constexpr int G = lnc3_groups<T>();
   static constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
   static constexpr bool REG = sizeof(T) == 2;
@@ -52,7 +52,7 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
   constexpr int KPL = F::KPL, KS = F::KSTEP;
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int LD3 = OC3 + 2 * VEC;                 // dact3 row (80 bf16: conflict-free b128 reads)
-  constexpr int LW = K3 + VEC;                       // staged W3 row
+  constexpr int LW = K3 + 2 * VEC;                   // staged W3 row (bit-2/3 swapped rows)
   constexpr int NKS = K3 / KS;
   constexpr int NKO = OC3 / KS;                      // k-steps per tap (K = oc)
   constexpr int G = lnc3_groups<T>();
@@ -106,14 +106,14 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
       const int e = (int)threadIdx.x + i * NT;
       if (e < NV) {
         const int r = e / (K3 / VEC), c = (e % (K3 / VEC)) * VEC;
-        *reinterpret_cast<V*>(smem + r * LW + c) = wv[i];
+        *reinterpret_cast<V*>(smem + wg_row(r) * LW + c) = wv[i];
       }
     }
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
-      wa[ks] = lds_frag_k(smem + oc0 * LW + tap * OC2 + 16 * wave, LW, lane);
+      wa[ks] = lds_frag_k_sw(smem + oc0 * LW + tap * OC2 + 16 * wave, LW, lane);
     }
     __syncthreads();  // the staging area becomes the Z / dact3 tiles
   }
