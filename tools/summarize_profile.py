@@ -101,7 +101,8 @@ def main(tag, src_root="gpurun_out", dst_root="profiles"):
               open(os.path.join(dst, "summary.json"), "w"), indent=1)
     with open(os.path.join(dst, "summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary `{tag}`\n\n`tools/profile.sh {tag}` = `rocprofv3 --kernel-trace --stats` "
-                "over `bench.py --steps 20 --warmup 3` (23 learner steps), then separate `--pmc FETCH_SIZE` "
+                "over `bench.py --steps 20 --warmup 3` (every launch of the run: warmup, kernel selection, the "
+                "timed and the stamped steps), then separate `--pmc FETCH_SIZE` "
                 "and `--pmc WRITE_SIZE` passes. HBM bytes per launch: FETCH_SIZE×1024×2 (gfx950 half-count "
                 "correction) + WRITE_SIZE×1024.\n\n")
         f.write("| kernel | calls | avg µs | % time | HBM read MB | HBM write MB |\n|---|---|---|---|---|---|\n")
