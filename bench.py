@@ -525,7 +525,9 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
-    if world > 1:
+    # IMPALA_BENCH_DIST=1: the data-parallel path (RCCL group, bucketed all-reduce, barriers,
+    # max over ranks) also at world size 1, to rehearse the N-GPU code on one GPU
+    if world > 1 or os.environ.get("IMPALA_BENCH_DIST") == "1":
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 

@@ -2,10 +2,9 @@
 
 Trajectories are independent and every loss term is a mean over (B, T-1) or (B, T), so with
 equal shards the mean of the replicas' gradients IS the full-batch gradient.  Each replica:
-``impala_compute_grads_part`` 2 / 6, each followed by an async ``all_reduce(sum)`` of the
-gradient bucket it finalised (FC + heads, then conv1 .. LayerNorm), so the larger bucket
-travels while the backward continues -> ``impala_apply_update`` (x 1/world, global-norm clip on the reduced
-gradient -- identical on every replica -- and Adam).  Weights therefore stay bit-identical
+``impala_compute_grads`` (the whole backward) -> ``all_reduce(sum)`` of the flat fp32 gradient
+(bucketed variants: ``compute_grads_allreduced``) -> ``impala_apply_update`` (x 1/world,
+global-norm clip on the reduced gradient -- identical on every replica -- and Adam).  Weights therefore stay bit-identical
 across replicas (checked by ``params_checksum``).
 """
 from __future__ import annotations
@@ -52,16 +51,28 @@ def allreduce_grads(flat_grad: torch.Tensor, group=None) -> None:
 
 
 def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None,
-                             buckets: int = 2) -> None:
-    """Local gradients of `batch` summed over replicas, in buckets, each all-reduced as soon as
-    the backward has finalised it so that it runs on the collective stream beside the rest of
-    the backward.  Two buckets (default): FC + heads (1.07 MB, after part 2: heads step, FC
-    weight and input gradients) overlaps part 6 (the fused per-frame LayerNorm / conv3 / conv2
-    backward and the conv3 + conv2 weight gradients, ~60 us); conv1 .. LayerNorm (0.31 MB)
-    follows it.  Three buckets (the unfused kernels): FC + heads after part 2, conv3 +
-    LayerNorm after part 3, conv1 + conv2 after part 4.  The caller's stream waits for all of
-    them before it continues (apply_update)."""
+                             buckets: int | None = None) -> None:
+    """Local gradients of `batch` summed over replicas.  The caller's stream waits for the
+    collectives before it continues (apply_update).
+
+    One bucket (default): the whole backward, then one all-reduce of the flat fp32 gradient
+    (1.38 MB).  Measured at world size 1 (RCCL group of one, `tools/dp_hosttime.py`,
+    `profiles/r02j/dp_hosttime.txt`): 114-130 us per step (bench: 0.1132 ms) against 105 us
+    for the fused single-replica step, while every bucketed arrangement costs more than the
+    overlap it can buy: each extra all-reduce adds a pair of cross-stream dependencies (~12 us of GPU idle
+    each pair) and ~15-30 us of host time in c10d, which leaves the GPU waiting on the host.
+    Two buckets (``buckets=2`` or IMPALA_DP_BUCKETS=2): FC + heads (1.07 MB) all-reduced after
+    part 2 while part 6 (the fused per-frame backward and the conv weight gradients) runs,
+    then conv1 .. LayerNorm (0.31 MB): 142 us at world size 1.  Three buckets (the unfused
+    kernels): FC + heads after part 2, conv3 + LayerNorm after part 3, conv1 + conv2 after
+    part 4."""
     import torch.distributed as dist
+    if buckets is None:
+        buckets = int(os.environ.get("IMPALA_DP_BUCKETS", "1"))
+    if buckets == 1:
+        engine.compute_grads(*batch)
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
+        return
     engine.compute_grads_part(2, *batch)
     off_fc, off = engine.bucket_offset_fc, engine.bucket_offset
     w_fc = dist.all_reduce(flat_grad[off_fc:], op=dist.ReduceOp.SUM, group=group, async_op=True)
