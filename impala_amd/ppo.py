@@ -6,7 +6,7 @@ entropy_coeff=0.01, learning_starts=None, model_push_period=8``), ``prepare`` /
 ``train_step/grad_norm``, ``debug/*``).  ``_train_step`` is one HIP call on a PPO handle
 (``impala_ppo_train_step``: the shared CNN forward, the fused PPO head -- clipped surrogate,
 ½·td², entropy, KL -- the shared backward, clip and Adam), or for data-parallel replicas the
-two-bucket gradient path of ``distributed.compute_grads_allreduced``.
+data-parallel gradient path of ``distributed.compute_grads_allreduced``.
 
 The batch is flat transitions ``(s u8 [N,3,64,64], a i64 [N], v_target f32 [N], pi_ref
 logits f32 [N,A])`` -- the order ``_train_step`` unpacks (learning.py:132).  The reference
