@@ -691,13 +691,22 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
         }
     }
   }
-  // zero the dY1 padding rows 225..255 and the dY2 cell grid once (the border stays zero);
-  // the dY1 pad rows in 4-element pieces (rows of 36 elements start 8-byte aligned)
+  // zero the dY1 rows no pixel writes and the dY2 cell grid once (the border stays zero);
+  // the dY1 rows in 4-element pieces (rows of 36 elements start 8-byte aligned).  bf16: dY1
+  // rows are grid rows oy * 16 + ox (the s2d image's), so the pad rows are ox = 15 and
+  // oy = 15; fp32: rows are pixels, pad rows 225..255.
   static_assert((c1::NPAD - c1::NPIX) * LDX % 4 == 0 && c12::NCELL * LD2 % VEC == 0 &&
                 c1::NPIX * LDX % 4 == 0 && LDX % 4 == 0, "zero fill");
+  constexpr bool GR = sizeof(T) == 2;
   for (int e = tid; e < (c1::NPAD - c1::NPIX) * LDX / 4; e += 256) {
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
-    store4(dyt + c1::NPIX * LDX + e * 4, z);
+    if constexpr (GR) {
+      const int rr = e / (LDX / 4), c = (e % (LDX / 4)) * 4;
+      const int row = rr < H1 ? rr * c1::GRID + H1 : c1::GRID * H1 + (rr - H1);
+      store4(dyt + row * LDX + c, z);
+    } else {
+      store4(dyt + c1::NPIX * LDX + e * 4, z);
+    }
   }
   for (int e = tid; e < c12::NCELL * LD2 / VEC; e += 256)
     *reinterpret_cast<V*>(d2s + e * VEC) = F::zero();
@@ -760,7 +769,7 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
         const int cell = nt * 16 + (lane & 15), qy = cell >> 3, qx = cell & 7;
         const int iy = 2 * qy + py, ix = 2 * qx + px;
         if (iy < H1 && ix < H1) {
-          const int p = iy * H1 + ix;
+          const int p = iy * H1 + ix, drow = GR ? iy * c1::GRID + ix : p;
           const uint32_t m = msk[p];
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
@@ -771,7 +780,7 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
               v[q] = (m >> (ci + q)) & 1u ? d[i][q] : 0.f;
               bsum[i][q] += v[q];
             }
-            store4(dyt + p * LDX + ci, v);
+            store4(dyt + drow * LDX + ci, v);
           }
         }
       }
@@ -779,14 +788,29 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
     __syncthreads();  // (every group reaches it: no early exit for an idle group)
     if (!active) continue;
     // ---- conv1 weight gradient: reduction over the frame's (padded) 256 pixels, fragments
-    // software-pipelined one k-step ahead ----
+    // software-pipelined one k-step ahead.  bf16: the k slots of a 32-deep step are the 32
+    // grid rows kk .. kk + 31 taken in the order that gives each 32-lane half of a
+    // transposing read 8 rows R + 4m (m = 0..7): at dY1's 18-dword and the image's 26-dword
+    // row steps those are 8 disjoint 8-dword bank ranges (tools/ldsbank.py: dY1 reads 2.0x ->
+    // 1.0x, image reads 1.88x -> 1.09x).  Rows without a pixel hold dY1 = 0; their image row
+    // is clamped to the last pixel row (238) so that the tap offsets stay inside the stashed image
+    // rows 0..255 (a 0 x NaN from an unwritten row would poison the sum). ----
     auto frag = [&](int kk, V* a, V* b) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
       if constexpr (sizeof(T) == 2) {
         const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
-        const int ra = c1_row(min(kk + 8 * g + q, c1::NPIX - 1), 0) * LDI + tapoff + 4 * pp;
-        const int rb = c1_row(min(kk + 8 * g + 4 + q, c1::NPIX - 1), 0) * LDI + tapoff + 4 * pp;
+        const int r0 = kk + 4 * (q + 4 * (g & 1)) + 2 * (g >> 1);  // rows r0 (k 0..3), r0 + 1
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x4_t u = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(dyt + r0 * LDX + 16 * i + 4 * pp));
+          const bf16x4_t w = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(dyt + (r0 + 1) * LDX + 16 * i + 4 * pp));
+          V v;
+          v[0] = u[0]; v[1] = u[1]; v[2] = u[2]; v[3] = u[3];
+          v[4] = w[0]; v[5] = w[1]; v[6] = w[2]; v[7] = w[3];
+          a[i] = v;
+        }
+        constexpr int RMAX = c1::GRID * (H1 - 1) + H1 - 1;  // 238: the last pixel row (+ 17 < 256)
+        const int ra = min(r0, RMAX) * LDI + tapoff + 4 * pp;
+        const int rb = min(r0 + 1, RMAX) * LDI + tapoff + 4 * pp;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const bf16x4_t u = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + ra + 16 * j));
@@ -797,6 +821,8 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
           b[j] = v;
         }
       } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
         const int g = lane >> 4, col = lane & 15;
         int rr[4];
 #pragma unroll
