@@ -224,7 +224,8 @@ template <typename T> struct C12FLds {
   static constexpr int VEC = 16 / (int)sizeof(T), LDA1 = OC1 + VEC, A1P = 22;
   static constexpr int IMGSZ = c1::FROWS * c1::LF<T>::LDI, GSZ = IMGSZ + A1P * 16 * LDA1;
   static constexpr int LDA2 = OC2 + VEC;
-  static constexpr int A2SZ = sizeof(T) == 2 ? C3T_FMAX * P2 * LDA2 : 0;
+  static constexpr int A2W = H2 + 1;  // act2 tile rows: 6 x 7 cells (one pad column)
+  static constexpr int A2SZ = sizeof(T) == 2 ? C3T_FMAX * H2 * A2W * LDA2 : 0;
   static constexpr int ELEMS = c12f_groups<T>() * GSZ + A2SZ;
 };
 
@@ -251,9 +252,11 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // (16 act1 rows: wave 3's pad tile oy = 15 writes row 15, read by nobody)
   constexpr int IMGSZ = c1::FROWS * LDI, GSZ = IMGSZ + A1P * 16 * LDA1;
   constexpr bool W2REG = sizeof(T) == 2;             // bf16: conv2 weights in registers
-  // conv3 tail (bf16): the frames' act2 in LDS rows of LDA2 elements (144 B: fewer conflicts)
-  constexpr int LDA2 = OC2 + VEC;
-  constexpr int A2SZ = W2REG ? C3T_FMAX * P2 * LDA2 : 0;
+  // conv3 tail (bf16): the frames' act2 in LDS rows of LDA2 elements (144 B), 7 cells per
+  // pixel row (a pad column): the conv3 window reads 2.0x instead of 3.0x, stores 2.0x
+  // instead of 1.67x (tools/ldsbank.py)
+  constexpr int LDA2 = OC2 + VEC, A2W = C12FLds<T>::A2W, A2F = H2 * A2W;
+  constexpr int A2SZ = W2REG ? C3T_FMAX * A2F * LDA2 : 0;
   static_assert(G * GSZ + A2SZ == C12FLds<T>::ELEMS && GSZ == C12FLds<T>::GSZ, "LDS layout");
   T* a2s = smem + G * GSZ;
   const bool tail = W2REG && c3.act3 != nullptr;
@@ -466,7 +469,10 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[pt][q] + bb2[q], 0.f);
           store4(act2 + ((size_t)f * P2 + pc) * OC2 + 16 * wave + 4 * (lane >> 4), v);
-          if (tail) store4(a2s + ((f - f0) * P2 + pc) * LDA2 + 16 * wave + 4 * (lane >> 4), v);
+          if (tail) {
+            const int cy = pc / H2, cx = pc - cy * H2;
+            store4(a2s + ((f - f0) * A2F + cy * A2W + cx) * LDA2 + 16 * wave + 4 * (lane >> 4), v);
+          }
         }
       }
     }
@@ -500,13 +506,13 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       __syncthreads();
       if (gw < nF) {
         const int p = lane & 15, oy = p >> 2, ox = p & 3;
-        const T* a2f = a2s + (gw * P2 + oy * H2 + ox) * LDA2 + kl;
+        const T* a2f = a2s + (gw * A2F + oy * A2W + ox) * LDA2 + kl;
         f32x4 acc3[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                          f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int ks = 0; ks < K3 / KS; ++ks) {  // k = ks*32 + kl: tap = k / 64, ci = k % 64
           const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
-          const V b = *reinterpret_cast<const V*>(a2f + (kh * H2 + kw) * LDA2 + (k & 63));
+          const V b = *reinterpret_cast<const V*>(a2f + (kh * A2W + kw) * LDA2 + (k & 63));
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const V a = *reinterpret_cast<const V*>(w3s + (16 * i + (lane & 15)) * LDW3 + k + kl);
