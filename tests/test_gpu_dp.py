@@ -4,7 +4,8 @@ overlapped all-reduce.
 * impala_compute_grads_part 0 + 1 give bit-identical gradients and metrics to
   impala_compute_grads (same kernels, same fixed-order slab reductions).
 * Two replicas on the box's one GPU (gloo over CUDA tensors: RCCL refuses two ranks on one
-  device) run `compute_grads_allreduced` + `apply_update` on their halves of a B=4 batch; their
+  device) run `compute_grads_allreduced` (one bucket, and two buckets) + `apply_update` on
+  their halves of a B=4 batch; their
   parameters stay bit-identical and match one B=4 learner (mean of shard gradients == full
   batch gradient, up to fp32 summation order amplified by Adam's normalised step).
 """
@@ -119,11 +120,13 @@ dist.destroy_process_group()
 """
 
 
-def test_two_replicas_bucketed_allreduce_match_full_batch(tmp_path):
+@pytest.mark.parametrize("buckets", ["1", "2"])
+def test_two_replicas_bucketed_allreduce_match_full_batch(tmp_path, buckets):
+    """Default one all-reduce after the whole backward, and the two-bucket overlapped path."""
     dev = _dev()
     wf = tmp_path / "worker.py"
     wf.write_text(WORKER)
-    env = dict(os.environ, IMPALA_ROOT=ROOT, OUT=str(tmp_path))
+    env = dict(os.environ, IMPALA_ROOT=ROOT, OUT=str(tmp_path), IMPALA_DP_BUCKETS=buckets)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(wf)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
