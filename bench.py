@@ -2,12 +2,17 @@
 """Learner throughput bench: env-frames/s of the IMPALA learner step on MI355X
 (``--algo ppo`` / ``--algo sac``: the PPO / SAC learner steps of BASELINE configs 4 / 5).
 
-``python bench.py --gpus N --steps K --warmup W``  (N > 1: launched by torch.distributed.run).
+``python bench.py --gpus N --steps K --warmup W``.  N > 1: one rank per GPU.  Under
+torch.distributed.run (WORLD_SIZE set) it must equal --gpus; run directly with --gpus N > 1 it
+starts ``python -m torch.distributed.run --nproc-per-node N`` itself as a child process (before
+anything touches the GPU) and exits with the child's status.
 
 Workload = BASELINE.json configs[1]: IMPALA procgen learner, B=64 trajectories x T=20 steps
-per replica, 15 actions, obs (3,64,64) u8, bf16 operands / fp32 accumulation + fp32 master
-weights.  One step = the full learner update (NatureCNN forward, log-softmax, V-trace, losses,
-backward, [RCCL gradient all-reduce], clip_grad_norm_(0.5), Adam) on a synthetic batch that
+per replica, 15 actions, obs (3,64,64) u8.  The headline (`value`, `dtype`) is the fp32 step --
+the reference learner's own arithmetic (agents/impala/learning.py:140-177 in torch's default
+fp32; MFMA f32-in/f32-accumulate, exact fp32 products); the bf16-operand mode (fp32 accumulation,
+fp32 master weights) is reported beside it as the ``bf16_mode`` sub-record.  One step = the
+full learner update (NatureCNN forward, log-softmax, V-trace, losses, backward, [RCCL gradient all-reduce], clip_grad_norm_(0.5), Adam) on a synthetic batch that
 is resident in HBM before the timed region.  Multi-GPU: data-parallel
 replicas, B=64 per GPU (weak scaling), one flat fp32 gradient bucket all-reduced over RCCL.
 
@@ -23,7 +28,8 @@ Also reported, all from the same run:
   stamped, 143 µs with all eight); its step time is reported as ``ms_per_step_stamped``;
 * ``step_roofline``: SURVEY.md §8(d)'s step-level figure, frames/s x 17.74 MFLOP/frame vs
   the dense MFMA peak;
-* ``fp32_parity_mode``: the same workload in fp32 (the reference's arithmetic);
+* ``bf16_mode`` (``--dtype bf16``: ``fp32_parity_mode``): the same workload in the other
+  operand precision;
 * ``host_staged``: the PCIe-inclusive rate (batches from page-locked host memory), never
   ``value``;
 * ``cpu_baseline``: the reference CPU learner (the oracle's torch-CPU restatement of
@@ -125,9 +131,11 @@ def synthetic_ppo_batch(N, A, seed, device):
     return [torch.from_numpy(x).to(device) for x in (obs, act, tgt, mu)]
 
 
-def cpu_baseline_ppo(N, A, seconds):
+def cpu_baseline_ppo(N, A, seconds, threads=None):
     """The reference PPO learner (oracle port of agents/ppo/learning.py:130-143)."""
     from oracle import ref_cpu
+    if threads:
+        torch.set_num_threads(threads)
     threads = torch.get_num_threads()
     batch = [torch.from_numpy(x) for x in ref_cpu.synthetic_ppo_batch(N, A, seed=4321)]
     model = ref_cpu.make_model(0, A)
@@ -146,18 +154,92 @@ def cpu_baseline_ppo(N, A, seconds):
                       f"{threads} threads) after 2 warm-up; median step {med * 1e3:.1f} ms"}
 
 
+def cgroup_cpu_quota():
+    """The CPU bandwidth quota of this process's cgroup in CPUs (cgroup v2 cpu.max, v1
+    cfs_quota_us / cfs_period_us), or None when unlimited / unreadable."""
+    try:
+        rel = "/"
+        for line in open("/proc/self/cgroup"):
+            parts = line.strip().split(":", 2)
+            if len(parts) == 3 and parts[0] == "0":
+                rel = parts[2]
+        for d in (os.path.join("/sys/fs/cgroup", rel.lstrip("/")), "/sys/fs/cgroup"):
+            p = os.path.join(d, "cpu.max")
+            if os.path.exists(p):
+                q, per = open(p).read().split()[:2]
+                return None if q == "max" else int(q) / int(per)
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except Exception:
+        return None
+
+
+def physical_cores(cpus):
+    """Distinct (package, core) pairs among the logical CPUs `cpus`."""
+    seen = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            seen.add((open(base + "physical_package_id").read().strip(),
+                      open(base + "core_id").read().strip()))
+        except Exception:
+            seen.add(("?", c))
+    return len(seen)
+
+
 def host_cpu_info():
-    """CPU model, the CPUs this process may run on (the box's share) and the machine's total."""
+    """CPU model, the CPUs this process may run on, their physical cores, the cgroup CPU quota,
+    and the CPU budget the baseline uses: the quota when one is set (the box's share of a
+    shared machine), else every physical core of the affinity set."""
     try:
         cpu = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
     except Exception:
         cpu = "unknown"
     try:
-        share = len(os.sched_getaffinity(0))
+        allowed = sorted(os.sched_getaffinity(0))
     except Exception:
-        share = os.cpu_count()
-    return {"cpu": cpu, "cpus_allowed": share, "cpus_machine": os.cpu_count(),
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+        allowed = list(range(os.cpu_count() or 1))
+    phys = physical_cores(allowed)
+    quota = cgroup_cpu_quota()
+    budget = max(1, int(quota)) if quota else phys
+    budget = min(budget, phys)
+    return {"cpu": cpu, "cpus_allowed": len(allowed), "physical_cores_allowed": phys,
+            "cgroup_cpu_quota": quota, "cpus_machine": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "baseline_threads": budget,
+            "budget_rule": "cgroup CPU quota if set, else all physical cores of the affinity set"}
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(nproc, argv, port):
+    """The torch.distributed.run command `bench.py --gpus N` (N > 1, no WORLD_SIZE) runs as its
+    child: one rank per GPU of this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch_ranks(args, argv):
+    """--gpus N > 1 outside torch.distributed.run: start the N ranks as a child process (this
+    process has not touched the GPU) and return its exit status; None = run in this process.
+    Under a launcher WORLD_SIZE must equal --gpus (SystemExit otherwise)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
+        return None
+    if args.gpus <= 1:
+        return None
+    import subprocess
+    cmd = launch_cmd(args.gpus, argv, free_port())
+    print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
 
 
 def cpu_baseline(B, T, A, seconds, threads=None, warmup=2):
@@ -489,13 +571,16 @@ def main():
     ap.add_argument("--batch", type=int, default=64, help="trajectories per GPU")
     ap.add_argument("--rollout", type=int, default=20)
     ap.add_argument("--actions", type=int, default=15)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="operand precision of the headline step (fp32 = the reference's)")
     ap.add_argument("--roofline-kernel", default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-seconds-1t", type=float, default=8.0,
                     help="sample length of the 1-thread CPU baseline leg")
-    ap.add_argument("--no-fp32-line", action="store_true",
-                    help="skip the fp32 parity-mode sub-record of a bf16 run")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: host_cpu_info()['baseline_threads'])")
+    ap.add_argument("--no-alt-line", "--no-fp32-line", dest="no_alt_line", action="store_true",
+                    help="skip the other-precision sub-record (bf16_mode / fp32_parity_mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-staged", action="store_true",
                     help="skip the PCIe-inclusive pass (host batches through impala_stage)")
@@ -507,6 +592,9 @@ def main():
     ap.add_argument("--act-dim", type=int, default=6)
     ap.add_argument("--replay", type=int, default=1_000_000)
     args = ap.parse_args()
+    rc = maybe_launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if args.algo == "sac":
         if args.batch == 64:
             args.batch = 256
@@ -520,8 +608,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
@@ -596,16 +682,20 @@ def main():
         "kernel_us": kernel_us,
         "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
     }
-    if not args.no_fp32_line and args.dtype == "bf16":
-        out["fp32_parity_mode"] = fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo)
+    if not args.no_alt_line:
+        alt = "fp32" if args.dtype == "bf16" else "bf16"
+        out["fp32_parity_mode" if alt == "fp32" else "bf16_mode"] = alt_line(
+            alt, args, B, T, A, dev, dist, world, make_step, ppo)
     if not args.no_host_staged:
         out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if ppo:
-            out["cpu_baseline"] = cpu_baseline_ppo(B, A, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline_ppo(B, A, args.cpu_seconds,
+                                                   args.cpu_threads or host_cpu_info()["baseline_threads"])
         else:
-            cb = cpu_baseline(B, T, A, args.cpu_seconds)
-            cb["host"] = host_cpu_info()
+            host = host_cpu_info()
+            cb = cpu_baseline(B, T, A, args.cpu_seconds, threads=args.cpu_threads or host["baseline_threads"])
+            cb["host"] = host
             cb["single_thread"] = cpu_baseline(B, T, A, args.cpu_seconds_1t, threads=1, warmup=1)
             out["cpu_baseline"] = cb
     if rank == 0:
@@ -692,12 +782,12 @@ def step_roofline(frames_per_s_per_gpu, flops_per_frame, dtype):
             "flops_per_frame": flops_per_frame}
 
 
-def fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo):
-    """The same workload in fp32 parity mode (the reference's arithmetic), in the same run:
-    value, step roofline and the dominant kernel's roofline."""
+def alt_line(dtype, args, B, T, A, dev, dist, world, make_step, ppo):
+    """The same workload in the other operand precision, in the same run: value, step
+    roofline and the dominant kernel's roofline (`bf16_mode` beside an fp32 headline)."""
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
-    m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+    m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=dtype, seed=0)
     e = Engine(m, batch_size=B, rollout_length=T, world_size=world, algo=args.algo)
     m._train_engine = e
     if dist is not None:
@@ -707,18 +797,18 @@ def fp32_line(args, B, T, A, dev, dist, world, batch, make_step, ppo):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    work = kernel_work(4)
+    work = kernel_work(2 if dtype == "bf16" else 4)
     table, top = select_kernels(e, step, work, argparse.Namespace(steps=args.steps,
                                                                    roofline_kernel=None))
     elapsed, _ = timed_steps(e, step, [], args, dist, dev)
     elapsed_st, k_times = timed_steps(e, step, top[:1], args, dist, dev)
     value = world * B * T * args.steps / elapsed
-    out = {"dtype": "fp32", "value": round(value, 1), "unit": "env-frames/s",
+    out = {"dtype": dtype, "value": round(value, 1), "unit": "env-frames/s",
            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
            "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
            "step_roofline": step_roofline(value / world, STEP_FLOPS_PER_FRAME if not ppo
-                                          else STEP_FLOPS_PER_FRAME_PPO, "fp32"),
-           "roofline": kernel_roofline(top[0], k_times[top[0]], work, B * T, "fp32", args.algo),
+                                          else STEP_FLOPS_PER_FRAME_PPO, dtype),
+           "roofline": kernel_roofline(top[0], k_times[top[0]], work, B * T, dtype, args.algo),
            "kernel_us": table}
     e.close()
     return out
