@@ -522,9 +522,9 @@ part1:
       return r;
     if (h->red_mode == 1) {
       if (int r = reduce_segments(h, RS_CONV2, RS_CONV3, ss, 0)) return r;
-    } else if (h->red_mode == 2 && part != 1 && part != 4) {
-      // (parts 1 / 4: conv3 .. heads were reduced by parts 0 / 2-3 and may be in an
-      // all-reduce right now; the final reduction below covers conv1 + conv2)
+    } else if (h->red_mode == 2 && part != 1 && part != 4 && part != 6) {
+      // (parts 1 / 4 / 6: conv3 .. heads, or FC + heads, were reduced by an earlier part and
+      // may be in an all-reduce right now; the final reduction below covers the rest)
       if (int r = reduce_segments(h, RS_CONV2, RS_END, ss, 0)) return r;
     }
   }

@@ -69,6 +69,8 @@ def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None,
     import torch.distributed as dist
     if buckets is None:
         buckets = int(os.environ.get("IMPALA_DP_BUCKETS", "1"))
+    if buckets not in (1, 2, 3):
+        raise ValueError(f"gradient buckets must be 1, 2 or 3 (IMPALA_DP_BUCKETS), got {buckets}")
     if buckets == 1:
         engine.compute_grads(*batch)
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)

@@ -156,20 +156,27 @@ class DeviceReplayBuffer(ReplayBuffer):
             return key
 
     def sample(self, batch_size: int, stream=None):
-        """-> (keys, (obs, act, rew, disc, mu) collated on the device, probs)."""
+        """-> (keys, (obs, act, rew, disc, mu) collated on the device, probs).
+
+        The lock is held from picking the slots until the gather's completion event is
+        published as ``_last_read`` (both are asynchronous enqueues, so this is cheap): an
+        append either lands before -- its H2D event is among the ``pending`` the gather waits
+        for -- or after, and then its copy waits for this gather.  No append can slip between
+        the two and overwrite a slot the gather is reading."""
         from impala_amd.engine import gather_rollouts
+        cur = torch.cuda.current_stream(self.device) if stream is None else stream
         with self._cv:
             idx = self._indices(batch_size)
             keys = self._keys[idx].copy()
             pending, self._pending = self._pending, []
-        cur = torch.cuda.current_stream(self.device) if stream is None else stream
-        for ev in pending:  # the learner's stream waits for every staged H2D
-            cur.wait_event(ev)
-        idx_t = torch.from_numpy(idx.astype(np.int64)).to(self.device, non_blocking=True)
-        batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx_t, stream)
-        read = torch.cuda.Event()
-        read.record(cur)
-        with self._cv:
+            for ev in pending:  # the learner's stream waits for every staged H2D
+                cur.wait_event(ev)
+            idx_t = torch.from_numpy(idx.astype(np.int64)).to(self.device, non_blocking=True)
+            batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx_t,
+                                    stream)
+            read = torch.cuda.Event()
+            read.record(cur)
             self._last_read = read
-        probs = np.full(batch_size, 1.0 / self._size)
+            size = self._size
+        probs = np.full(batch_size, 1.0 / size)
         return keys, batch, probs

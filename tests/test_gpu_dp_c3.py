@@ -1,8 +1,9 @@
 """Data-parallel path at the C3 per-replica shape and through RCCL.
 
-* RCCL is actually issued: a world-size-1 `nccl` (RCCL) process group runs the three-bucket
-  `compute_grads_allreduced` + `impala_apply_update`; a one-rank all-reduce is the identity,
-  so two steps must be bitwise equal to `impala_train_step` on the same batches.
+* RCCL is actually issued: a world-size-1 `nccl` (RCCL) process group runs
+  `compute_grads_allreduced` (one bucket, the default; and the two- and three-bucket
+  arrangements) + `impala_apply_update`; a one-rank all-reduce is the identity, so two steps
+  must be bitwise equal to `impala_train_step` on the same batches.
 * C3's per-replica shape (B=64 per replica, T=20; BASELINE config 3 is 8 replicas x 64): two
   replicas on the box's one GPU over gloo (RCCL refuses two ranks on one device), bf16 and
   fp32, each on its half of a B=128 batch, against one learner on the whole B=128 batch.
@@ -78,7 +79,7 @@ m1, e1 = make()
 m2, e2 = make()
 for b in batches:
     e1.train_step(*b)
-    compute_grads_allreduced(e2, b, m2.flat_grad, group=group)
+    compute_grads_allreduced(e2, b, m2.flat_grad, group=group, buckets=int(os.environ["BUCKETS"]))
     e2.apply_update()
 torch.cuda.synchronize()
 res = {"params_equal": bool(torch.equal(m1.flat, m2.flat)),
@@ -90,10 +91,10 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-def test_rccl_world1_bucketed_step_is_bitwise_train_step(dtype, tmp_path):
+@pytest.mark.parametrize("dtype,buckets", [("bf16", 1), ("fp32", 1), ("fp32", 2), ("fp32", 3)])
+def test_rccl_world1_bucketed_step_is_bitwise_train_step(dtype, buckets, tmp_path):
     _dev()
-    _launch(tmp_path, RCCL_WORKER, 1, {"DTYPE": dtype})
+    _launch(tmp_path, RCCL_WORKER, 1, {"DTYPE": dtype, "BUCKETS": str(buckets)})
     res = json.load(open(tmp_path / "rccl.json"))
     assert res["backend"] == "nccl"
     assert res["params_equal"] and res["metrics_equal"] and res["grads_equal"], res

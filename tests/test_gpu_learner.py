@@ -281,6 +281,57 @@ def test_device_replay_overwrite_waits_for_queued_gather():
         np.testing.assert_array_equal(batch[4][j].cpu().numpy(), old[k][4].numpy())
 
 
+def test_device_replay_append_during_sample_threaded():
+    """appends racing sample() from another thread never tear a trajectory.  Every
+    field of trajectory k encodes k, a capacity-8 ring is overwritten continuously by a writer
+    thread while the main thread samples; each sampled row must be one whole trajectory and the
+    one its returned key names."""
+    import threading
+    dev = _dev()
+    from impala_amd.replay import DeviceReplayBuffer
+    T, A, C = 20, 15, 8
+
+    def item(k):
+        return [torch.full((T, 3, 64, 64), k % 251, dtype=torch.uint8),
+                torch.full((T, 1), k % A, dtype=torch.int64),
+                torch.full((T, 1), float(k)), torch.full((T, 1), 0.5 * k),
+                torch.full((T, A), float(-k))]
+
+    rb = DeviceReplayBuffer(capacity=C, rollout_length=T, num_actions=A, device=dev, seed=3,
+                            staging_slots=4)
+    for k in range(C):
+        rb.append(item(k))
+    stop = threading.Event()
+    errors = []
+
+    def writer():
+        k = C
+        try:
+            while not stop.is_set() and k < 5000:
+                rb.append(item(k))
+                k += 1
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = threading.Thread(target=writer)
+    th.start()
+    try:
+        for _ in range(150):
+            keys, (obs, act, rew, disc, mu), _ = rb.sample(C)
+            torch.cuda.synchronize()
+            r = rew.cpu().numpy()
+            for j, k in enumerate(keys.tolist()):
+                assert np.all(r[j] == float(k)), (j, k, r[j][:3])
+                assert np.all(obs[j].cpu().numpy() == k % 251)
+                assert np.all(act[j].cpu().numpy() == k % A)
+                assert np.all(disc[j].cpu().numpy() == 0.5 * k)
+                assert np.all(mu[j].cpu().numpy() == -float(k))
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors
+
+
 def test_whole_model_checkpoint_after_learner_step(tmp_path):
     """reference main.py:117 torch.save(builder.learner_model, ...) with the learner's engine
     (a native handle) attached: the model pickles, reloads with its parameters and gradients
