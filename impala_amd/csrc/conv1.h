@@ -286,6 +286,9 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // workgroup instead of 8 waves x 28 KB of fragment loads through the CU's L2 port).
   V wa1[2][NKS1];  // conv1: rows oc = 16 i + (lane & 15), all of K
   const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
+  // bf16: this wave's W2 rows in registers for the whole frame run (64 VGPRs).  fp32 reads its
+  // fragments from L2 per k-step: holding all 128 VGPRs of them made the kernel 3.5 us slower
+  // (78.9 -> 82.4 us, r03 q32 run)
   V wa2[W2REG ? NKS2 : 1];
   if constexpr (W2REG) {
     // rows padded by 16 (row step 8 mod 32 dwords): conflict-free b128 fragment reads
@@ -323,6 +326,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       wa2[ks] = *reinterpret_cast<const V*>(w2s + (16 * wave + (lane & 15)) * LW2 + ks * KS + kl);
     __syncthreads();  // the staging area becomes the frame tiles
   } else {
+    // fp32: 16-byte fragment loads straight from L2, issued once for the frame run
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll

@@ -240,8 +240,9 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
                    bool with_heads) {
   using namespace net;
   // K chunk of the LDS-staged tile GEMM: long chunks (few, each a full memory round trip) for
-  // bf16; fp32 (parity mode) keeps 32 for its LDS budget
-#define BK(kb) (sizeof(T) == 4 ? 32 : (kb))
+  // bf16; fp32 at most 64 (tools/var_specs/fp32a.py: 32 -> 64 cut fc_fwd 18.2 -> 14.0 us and
+  // conv3_fwd 28.3 -> 27.0 us; 128 / 256 lost on conv3_fwd's LDS footprint)
+#define BK(kb) (sizeof(T) == 4 ? ((kb) < 64 ? (kb) : 64) : (kb))
   const T* sw = reinterpret_cast<const T*>(h->shadow);
   const Shadow& sh = h->sh;
   const float* vv = h->vecs;

@@ -35,7 +35,10 @@ template <typename T> struct Lnc3Lds {
   static constexpr int G = lnc3_groups<T>();
   static constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
   static constexpr bool REG = sizeof(T) == 2;
-  static constexpr int SMEM = (REG && OC3 * LW * (int)sizeof(T) > G * GB) ? OC3 * LW * (int)sizeof(T) : G * GB;
+  // W3 staging: bf16 all 64 rows at once; fp32 (147 KB) in two passes of 32 rows of K3 + 4
+  static constexpr int LWF = K3 + 4;
+  static constexpr int STG = REG ? OC3 * LW * (int)sizeof(T) : (OC3 / 2) * LWF * 4;
+  static constexpr int SMEM = STG > G * GB ? STG : G * GB;
   static constexpr int RED = SMEM, COMB = RED + G * 4 * 2 * 4, BYTES = COMB + 2 * FLAT * 4;
 };
 
@@ -91,9 +94,41 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 #pragma unroll
   for (int q = 0; q < 4; ++q) gm[q] = gam[j0 + q];
 
-  // ---- W3 fragments: B[k = oc][n = ci] = W3[oc][tap][ci] of every tap (k-major) ----
-  V wa[REG ? NKS : 1];
-  if constexpr (REG) {
+  // ---- W3 fragments: B[k = oc][n = ci] = W3[oc][tap][ci] of every tap (k-major), held in
+  // registers for the whole frame run (bf16 72, fp32 144 VGPRs) ----
+  V wa[NKS];
+  if constexpr (!REG) {
+    // fp32: W3 (147 KB) staged through LDS in two passes of 32 oc rows (coalesced 16-byte
+    // loads, rows of K3 + 4 floats), the fragments of the pass's k-steps read from LDS: rows
+    // 4 apart of one read sit 16 banks apart (conflict-free)
+    constexpr int LWF = Lnc3Lds<T>::LWF, HALF = OC3 / 2, NV = HALF * K3 / 4, NT = 256 * G;
+    constexpr int NPT = NV / NT;
+    static_assert(NV % NT == 0 && HALF * LWF * 4 <= Lnc3Lds<T>::SMEM, "fp32 W3 staging");
+    float* ws = reinterpret_cast<float*>(smem_b);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x4 wv[NPT];
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int e = (int)threadIdx.x + i * NT;
+        wv[i] = *reinterpret_cast<const f32x4*>(w3 + (size_t)(HALF * hh) * K3 + (size_t)e * 4);
+      }
+      if (hh) __syncthreads();  // the first pass's fragment reads are done
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int e = (int)threadIdx.x + i * NT, r = e / (K3 / 4), c = (e % (K3 / 4)) * 4;
+        *reinterpret_cast<f32x4*>(ws + r * LWF + c) = wv[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
+        if ((oc0 >> 5) == hh)
+          wa[ks] = lds_frag_k(ws + (oc0 - HALF * hh) * LWF + tap * OC2 + 16 * wave, LWF, lane);
+      }
+    }
+    __syncthreads();  // the staging area becomes the Z / dact3 tiles
+  } else {
     constexpr int NV = OC3 * K3 / VEC, NT = 256 * G, NPT = (NV + NT - 1) / NT;
     V wv[NPT];  // all loads in flight at once, then the LDS stores
 #pragma unroll
@@ -175,15 +210,7 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 #pragma unroll
         for (int ko = 0; ko < NKO; ++ko) {
           const int ks = tap * NKO + ko;
-          if constexpr (REG) {
-            acc = F::mma(a[ko], wa[ks], acc);
-          } else {  // fp32: the B fragment straight from L2 (parity mode)
-            V b;
-#pragma unroll
-            for (int jj = 0; jj < KPL; ++jj)
-              b[jj] = w3[(size_t)(ko * KS + kl + jj) * K3 + tap * OC2 + 16 * wave + (lane & 15)];
-            acc = F::mma(a[ko], b, acc);
-          }
+          acc = F::mma(a[ko], wa[ks], acc);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)

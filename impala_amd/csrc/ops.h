@@ -277,7 +277,7 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
 // idle for its ~7 us; the dgrad tiles fill them instead of running after it.  Same per-tile
 // arithmetic as the two separate kernels (same tile shapes for the weight gradient).
 template <typename T, int G> struct FcBwdCfg {
-  static constexpr int DR = G == 2 ? 128 : 64, DWR = G == 2 ? 4 : 2, DBK = sizeof(T) == 2 ? 128 : 32;
+  static constexpr int DR = G == 2 ? 128 : 64, DWR = G == 2 ? 4 : 2, DBK = sizeof(T) == 2 ? 128 : 64;
   static constexpr int SW = gemm_wg_smem<T, 64, 256, 32, G>();
   static constexpr int SD = gemm_tile_smem<T, DR, 64, DBK, DWR, 2, FcDgrad<T>>();
   static constexpr int SMEM = SW > SD ? SW : SD;
