@@ -591,6 +591,19 @@ constexpr int NCELL = QG * QG;
 // on top of the one-frame register prefetch); their partials are summed in a fixed order.
 template <typename T> constexpr int c12_groups() { return sizeof(T) == 2 ? 2 : 1; }
 
+// fp32 body (conv12_bwd_body_f32) LDS, in floats: the frame's s2d image, dY1 in pixel rows
+// (240: the conv1 weight gradient's 15 k-steps of 16), dY2 as the scatter GEMM's A rows (48:
+// 3 row tiles), two Z buffers of one stride-parity class, then the mask words
+struct C12B32 {
+  static constexpr int LDI = c1::LB<float>::LDI, LDX = c1::LB<float>::LDX;
+  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = 48, LDZ = 4 * OC1 + 4, ZROWS = P2;
+  static constexpr int IMG = 0, DYT = IMG + c1::GRID * c1::GRID * LDI, D2S = DYT + NROW * LDX;
+  static constexpr int Z0 = D2S + DROWS * LDD, ZSZ = ZROWS * LDZ, MSK = Z0 + 2 * ZSZ;
+  static constexpr int BYTES = (MSK + c1::NPIX) * 4;
+  static constexpr int LDW = K2 + 4;  // W2 staging rows (32 per pass)
+  static_assert(32 * LDW <= MSK, "W2 staging");
+};
+
 // LDS of the body (bytes): per-group image / dY1 / dY2 tiles, the ReLU mask words, bias sums
 template <typename T> struct C12BLds {
   static constexpr int VEC = 16 / (int)sizeof(T), LDX = c1::LB<T>::LDX, LD2 = c1::LB<T>::LD2;
@@ -599,8 +612,234 @@ template <typename T> struct C12BLds {
   static constexpr int GSZ = IMGSZ + DYSZ + c12::NCELL * LD2;
   static constexpr int MSK = (G * GSZ * (int)sizeof(T) + 15) / 16 * 16;
   static constexpr int BRED = MSK + (G * c1::NPIX * 4 + 15) / 16 * 16;
-  static constexpr int BYTES = BRED + 4 * G * OC1 * 4;
+  static constexpr int BYTES = sizeof(T) == 4 ? C12B32::BYTES : BRED + 4 * G * OC1 * 4;
 };
+
+// ---------------------------------------------------------------------------------------
+// fp32 conv2 input gradient + ReLU mask + conv1 weight gradient, per frame, in SCATTER form:
+//
+//   Z[op][t][ci] = sum_oc dY2[op][oc] W2[oc][t][ci]        (36 conv2 output pixels op)
+//   dY1[iy][ix][ci] = [act1 > 0] * sum_{t = (kh, kw): iy = 2 oy + kh, ix = 2 ox + kw} Z[op][t][ci]
+//
+// The 16 taps fall into the four stride-parity classes (kh % 2, kw % 2); a class's 4 taps
+// reach exactly the input pixels of that parity, so the classes run one after another through
+// a double-buffered Z of one class: wave w computes tap w of the class (rows op: 3 tiles of 16,
+// cols ci: 2 tiles, K = 64 oc) with its W2 fragments in registers and the dY2 rows as the A
+// operand (16-byte LDS reads, loaded once per frame), then every thread gathers <= 4 Z terms
+// per (pixel, 4 channels) of the class in a fixed tap order, masks them and writes dY1.  Each
+// class's gather overlaps the next class's MFMAs (different Z buffer; one barrier per class).
+// 384 MFMAs per wave per frame against the gather form's 512 (whose K runs over zero-padded
+// dY2 cells: 56 % useful); the conv1 weight gradient then reduces over 240 pixel rows (225
+// real) instead of 256.  fp32 sums: oc in MFMA order, then taps in a fixed order.
+// ---------------------------------------------------------------------------------------
+DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restrict__ w2,
+                             const float* __restrict__ dy2, const uint32_t* __restrict__ mask1,
+                             float* __restrict__ slab, float* __restrict__ slab_bias, int N,
+                             int fpw, int wg, char* __restrict__ lds) {
+  using F = Frag<float>;
+  typedef F::vec V;
+  using L = C12B32;
+  constexpr int KS = F::KSTEP, LDI = L::LDI, LDX = L::LDX, LDD = L::LDD, LDZ = L::LDZ;
+  constexpr int NKO = OC2 / KS;             // 4 k-steps over oc
+  constexpr int D2V = P2 * OC2 / 4;         // float4 vectors of one dY2 frame (576)
+  constexpr int ND2 = (D2V + 255) / 256;
+  float* smem = reinterpret_cast<float*>(lds);
+  float* img = smem + L::IMG;
+  float* dyt = smem + L::DYT;
+  float* d2s = smem + L::D2S;
+  uint32_t* msk = reinterpret_cast<uint32_t*>(smem + L::MSK);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
+  const int kl = 4 * (lane >> 4);
+  f32x4 acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // conv1 bias partials of this thread's 4 channels
+  uint4 nv[3];
+  f32x4 nd2[ND2];
+  uint32_t nmk = 0;
+  auto fetch = [&](int f) {
+    c1_load_frame<float>(x + (size_t)f * IMG, tid, nv);
+    const float* src = dy2 + (size_t)f * P2 * OC2;
+#pragma unroll
+    for (int i = 0; i < ND2; ++i) {
+      const int e = tid + i * 256;
+      nd2[i] = e < D2V ? *reinterpret_cast<const f32x4*>(src + e * 4) : F::zero();
+    }
+    if (tid < c1::NPIX) nmk = mask1[(size_t)f * c1::NPIX + tid];
+  };
+  if (f0 < f1) fetch(f0);  // the first frame is in flight during the prologue
+  // ---- W2 fragments, B[k = oc][n = ci] = W2[oc][kh][kw][ci] for tap w of every class:
+  // staged through LDS in two passes of 32 oc rows (coalesced 16-byte loads), rows 4 apart of
+  // one fragment read 16 banks apart ----
+  V wb[4][NKO][2];  // [class][k-step][ci tile]
+  {
+    constexpr int NV = 32 * K2 / 4, NPT = NV / 256;
+    static_assert(NV % 256 == 0, "W2 staging");
+    float* ws = smem;
+    const int j1 = wave >> 1, j2 = wave & 1;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x4 wv[NPT];
+#pragma unroll
+      for (int i = 0; i < NPT; ++i)
+        wv[i] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(32 * hh) * K2 + (size_t)(tid + i * 256) * 4);
+      if (hh) __syncthreads();  // the first pass's fragment reads are done
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int e = tid + i * 256, r = e / (K2 / 4), c = (e % (K2 / 4)) * 4;
+        *reinterpret_cast<f32x4*>(ws + r * L::LDW + c) = wv[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int kh = (c >> 1) + 2 * j1, kw = (c & 1) + 2 * j2;
+#pragma unroll
+        for (int ks = 2 * hh; ks < 2 * hh + 2; ++ks)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+            wb[c][ks][ct] = lds_frag_k(ws + (ks * KS - 32 * hh) * L::LDW + (kh * KS2 + kw) * OC1 + 16 * ct,
+                                       L::LDW, lane);
+      }
+    }
+    __syncthreads();  // the staging area becomes the frame tiles
+  }
+  // zero the dY1 rows no pixel writes (225..239) and the dY2 pad rows (36..47) once
+  for (int e = tid; e < (L::NROW - c1::NPIX) * LDX / 4; e += 256)
+    *reinterpret_cast<f32x4*>(dyt + c1::NPIX * LDX + 4 * e) = F::zero();
+  for (int e = tid; e < (L::DROWS - P2) * LDD / 4; e += 256)
+    *reinterpret_cast<f32x4*>(d2s + P2 * LDD + 4 * e) = F::zero();
+  const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDI;
+  // gather item of this thread: channels 4 cg .. 4 cg + 3 of cells s and s + 32 of a class
+  const int cg = tid & 7, sl = tid >> 3;
+  for (int f = f0; f < f1; ++f) {
+    __syncthreads();  // the previous frame's readers are done
+    c1_stash_frame<float, LDI>(img, tid, nv);
+#pragma unroll
+    for (int i = 0; i < ND2; ++i) {
+      const int e = tid + i * 256;
+      if (e < D2V) {
+        const int op = (e * 4) / OC2, oc = (e * 4) % OC2;
+        *reinterpret_cast<f32x4*>(d2s + op * LDD + oc) = nd2[i];
+      }
+    }
+    if (tid < c1::NPIX) msk[tid] = nmk;
+    __syncthreads();
+    if (f + 1 < f1) fetch(f + 1);
+    // ---- conv2 dgrad: the dY2 A fragments of the 3 row tiles, then the four classes ----
+    V a2[3][NKO];
+#pragma unroll
+    for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+      for (int ks = 0; ks < NKO; ++ks)
+        a2[rt][ks] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + ks * KS + kl);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float* zc = smem + L::Z0 + (c & 1) * L::ZSZ;
+      f32x4 z[3][2];
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) z[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKO; ++ks)
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) z[rt][ct] = F::mma(a2[rt][ks], wb[c][ks][ct], z[rt][ct]);
+      // Z[op][w * 32 + ci] (rows op < 36 only)
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int op = 16 * rt + kl + q;
+          if (op < P2) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) zc[op * LDZ + wave * OC1 + 16 * ct + (lane & 15)] = z[rt][ct][q];
+          }
+        }
+      __syncthreads();
+      // ---- col2im of class c = (py, px): input pixel (2 qy + py, 2 qx + px) sums taps
+      // (kh, kw) = (py + 2 j1, px + 2 j2) at dY2 cell (qy - j1, qx - j2), order j1, j2 ----
+      const int py = c >> 1, px = c & 1;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int cell = sl + 32 * h2, qy = cell >> 3, qx = cell & 7;
+        const int iy = 2 * qy + py, ix = 2 * qx + px;
+        if (iy < H1 && ix < H1) {
+          f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int oy = qy - (t >> 1), ox = qx - (t & 1);
+            if (oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
+              sum += *reinterpret_cast<const f32x4*>(zc + (oy * H2 + ox) * LDZ + t * OC1 + 4 * cg);
+          }
+          const int p = iy * H1 + ix;
+          const uint32_t m = msk[p];
+          f32x4 v;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[q] = (m >> (4 * cg + q)) & 1u ? sum[q] : 0.f;
+            bsum[q] += v[q];
+          }
+          *reinterpret_cast<f32x4*>(dyt + p * LDX + 4 * cg) = v;
+        }
+      }
+    }
+    __syncthreads();  // dY1 complete
+    // ---- conv1 weight gradient over the 240 pixel rows (as conv12_bwd_body's fp32 path) ----
+    auto frag = [&](int kk, V* a, V* b) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
+      const int g = lane >> 4, col = lane & 15;
+      int rr[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        rr[jj] = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDI + tapoff + col;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        V v;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[jj] = img[rr[jj] + 16 * j];
+        b[j] = v;
+      }
+    };
+    constexpr int NKK = L::NROW / KS;
+    V fa[2][2], fb[2][3];
+    frag(0, fa[0], fb[0]);
+#pragma unroll
+    for (int s2 = 0; s2 < NKK; ++s2) {
+      if (s2 + 1 < NKK) frag((s2 + 1) * KS, fa[(s2 + 1) & 1], fb[(s2 + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
+    }
+  }
+  // conv1 bias: the 32 threads of each channel group in a fixed order
+  __syncthreads();  // every frame's readers are done: the Z area holds the bias partials
+  float* bred = smem + L::Z0;
+  *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
+  __syncthreads();
+  if (tid < OC1) {
+    float bs = 0.f;
+#pragma unroll 8
+    for (int s = 0; s < 32; ++s) bs += bred[4 * (s * 8 + (tid >> 2)) + (tid & 3)];
+    slab_bias[(size_t)wg * OC1 + tid] = bs;
+  }
+  const size_t so = (size_t)wg * OC1 * K1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int col = wave * c1::CH + 16 * j + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);
+    }
+}
 
 // The kernel body, on workgroup `wg` with the LDS passed in (C12BLds<T>::BYTES)
 template <typename T>
@@ -608,6 +847,11 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
                          const T* __restrict__ dy2, const uint32_t* __restrict__ mask1,
                          float* __restrict__ slab, float* __restrict__ slab_bias, int N, int fpw,
                          int wg, char* __restrict__ lds) {
+  if constexpr (sizeof(T) == 4) {  // fp32: the scatter-form body above
+    conv12_bwd_body_f32(x, reinterpret_cast<const float*>(w2), reinterpret_cast<const float*>(dy2),
+                        mask1, slab, slab_bias, N, fpw, wg, lds);
+    return;
+  }
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
