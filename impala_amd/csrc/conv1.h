@@ -591,17 +591,17 @@ constexpr int NCELL = QG * QG;
 // on top of the one-frame register prefetch); their partials are summed in a fixed order.
 template <typename T> constexpr int c12_groups() { return sizeof(T) == 2 ? 2 : 1; }
 
-// fp32 body (conv12_bwd_body_f32) LDS, in floats: the frame's s2d image, dY1 in pixel rows
-// (240: the conv1 weight gradient's 15 k-steps of 16), dY2 as the scatter GEMM's A rows (48:
-// 3 row tiles), two Z buffers of one stride-parity class, then the mask words
+// fp32 body (conv12_bwd_body_f32) LDS, in 4-byte words: the frame's s2d image as BYTES (the
+// raw 0..255 values, converted when read; 48-byte rows), dY1 in pixel rows (240: the conv1
+// weight gradient's 15 k-steps of 16), dY2 as the scatter GEMM's A rows (48: 3 row tiles), one
+// Z tile per wave (its stride-parity class; row 36 stays zero: the gather's out-of-range taps
+// read it), then the mask words
 struct C12B32 {
-  static constexpr int LDI = c1::LB<float>::LDI, LDX = c1::LB<float>::LDX;
-  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = 48, LDZ = 4 * OC1 + 4, ZROWS = P2;
-  static constexpr int IMG = 0, DYT = IMG + c1::GRID * c1::GRID * LDI, D2S = DYT + NROW * LDX;
-  static constexpr int Z0 = D2S + DROWS * LDD, ZSZ = ZROWS * LDZ, MSK = Z0 + 2 * ZSZ;
+  static constexpr int LDIB = c1::CH, LDX = c1::LB<float>::LDX;  // image row bytes, dY1 row
+  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = 48, LDZ = 4 * OC1 + 4, ZROWS = P2 + 1;
+  static constexpr int IMG = 0, DYT = IMG + c1::GRID * c1::GRID * LDIB / 4, D2S = DYT + NROW * LDX;
+  static constexpr int Z0 = D2S + DROWS * LDD, ZSZ = ZROWS * LDZ, MSK = Z0 + 4 * ZSZ;
   static constexpr int BYTES = (MSK + c1::NPIX) * 4;
-  static constexpr int LDW = K2 + 4;  // W2 staging rows (32 per pass)
-  static_assert(32 * LDW <= MSK, "W2 staging");
 };
 
 // LDS of the body (bytes): per-group image / dY1 / dY2 tiles, the ReLU mask words, bias sums
@@ -621,42 +621,44 @@ template <typename T> struct C12BLds {
 //   Z[op][t][ci] = sum_oc dY2[op][oc] W2[oc][t][ci]        (36 conv2 output pixels op)
 //   dY1[iy][ix][ci] = [act1 > 0] * sum_{t = (kh, kw): iy = 2 oy + kh, ix = 2 ox + kw} Z[op][t][ci]
 //
-// The 16 taps fall into the four stride-parity classes (kh % 2, kw % 2); a class's 4 taps
-// reach exactly the input pixels of that parity, so the classes run one after another through
-// a double-buffered Z of one class: wave w computes tap w of the class (rows op: 3 tiles of 16,
-// cols ci: 2 tiles, K = 64 oc) with its W2 fragments in registers and the dY2 rows as the A
-// operand (16-byte LDS reads, loaded once per frame), then every thread gathers <= 4 Z terms
-// per (pixel, 4 channels) of the class in a fixed tap order, masks them and writes dY1.  Each
-// class's gather overlaps the next class's MFMAs (different Z buffer; one barrier per class).
-// 384 MFMAs per wave per frame against the gather form's 512 (whose K runs over zero-padded
-// dY2 cells: 56 % useful); the conv1 weight gradient then reduces over 240 pixel rows (225
-// real) instead of 256.  fp32 sums: oc in MFMA order, then taps in a fixed order.
+// The 16 taps fall into the four stride-parity classes (kh % 2, kw % 2) and a class's 4 taps
+// reach exactly the input pixels of that parity, so wave w owns class w: it computes Z for its
+// 4 taps (rows op: 3 tiles of 16, cols (tap, ci): 8 tiles, K = 64 oc; its W2 fragments in
+// registers, the dY2 rows as the A operand) into its own LDS tile, then gathers <= 4 Z terms
+// per (pixel, 4 channels) of its class in a fixed tap order, masks them and writes dY1 -- no
+// workgroup barrier between the GEMM and the gather.  384 MFMAs per wave per frame against the
+// gather form's 512 (whose K runs over zero-padded dY2 cells: 56 % useful); the conv1 weight
+// gradient then reduces over 240 pixel rows (225 real) instead of 256.  The image is kept as
+// bytes (12 KB instead of 53 KB of floats) and converted per fragment element, which is what
+// leaves room for the four Z tiles.  fp32 sums: oc in MFMA order, then taps in a fixed order.
 // ---------------------------------------------------------------------------------------
-DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restrict__ w2,
+DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restrict__ w2t,
                              const float* __restrict__ dy2, const uint32_t* __restrict__ mask1,
                              float* __restrict__ slab, float* __restrict__ slab_bias, int N,
                              int fpw, int wg, char* __restrict__ lds) {
   using F = Frag<float>;
   typedef F::vec V;
   using L = C12B32;
-  constexpr int KS = F::KSTEP, LDI = L::LDI, LDX = L::LDX, LDD = L::LDD, LDZ = L::LDZ;
+  constexpr int KS = F::KSTEP, LDIB = L::LDIB, LDX = L::LDX, LDD = L::LDD, LDZ = L::LDZ;
   constexpr int NKO = OC2 / KS;             // 4 k-steps over oc
   constexpr int D2V = P2 * OC2 / 4;         // float4 vectors of one dY2 frame (576)
   constexpr int ND2 = (D2V + 255) / 256;
   float* smem = reinterpret_cast<float*>(lds);
-  float* img = smem + L::IMG;
+  uint8_t* img = reinterpret_cast<uint8_t*>(smem + L::IMG);
   float* dyt = smem + L::DYT;
   float* d2s = smem + L::D2S;
   uint32_t* msk = reinterpret_cast<uint32_t*>(smem + L::MSK);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = 4 * (lane >> 4);
+  const int py = wave >> 1, px = wave & 1;  // this wave's stride-parity class
+  float* zw = smem + L::Z0 + wave * L::ZSZ;
   f32x4 acc[2][3];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // conv1 bias partials of this thread's 4 channels
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // conv1 bias partials of this lane's 4 channels
   uint4 nv[3];
   f32x4 nd2[ND2];
   uint32_t nmk = 0;
@@ -671,52 +673,40 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     if (tid < c1::NPIX) nmk = mask1[(size_t)f * c1::NPIX + tid];
   };
   if (f0 < f1) fetch(f0);  // the first frame is in flight during the prologue
-  // ---- W2 fragments, B[k = oc][n = ci] = W2[oc][kh][kw][ci] for tap w of every class:
-  // staged through LDS in two passes of 32 oc rows (coalesced 16-byte loads), rows 4 apart of
-  // one fragment read 16 banks apart ----
-  V wb[4][NKO][2];  // [class][k-step][ci tile]
-  {
-    constexpr int NV = 32 * K2 / 4, NPT = NV / 256;
-    static_assert(NV % 256 == 0, "W2 staging");
-    float* ws = smem;
-    const int j1 = wave >> 1, j2 = wave & 1;
+  // ---- W2 fragments, B[k = oc][n = ci] = W2[oc][kh][kw][ci] for the class's 4 taps: 16-byte
+  // loads from the transposed copy w2t[(kh*4+kw)*32 + ci][oc] (k = oc contiguous) ----
+  V wb[4][NKO][2];  // [tap j1*2+j2][k-step][ci tile]
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      f32x4 wv[NPT];
+  for (int t = 0; t < 4; ++t) {
+    const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
 #pragma unroll
-      for (int i = 0; i < NPT; ++i)
-        wv[i] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(32 * hh) * K2 + (size_t)(tid + i * 256) * 4);
-      if (hh) __syncthreads();  // the first pass's fragment reads are done
+    for (int ks = 0; ks < NKO; ++ks)
 #pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int e = tid + i * 256, r = e / (K2 / 4), c = (e % (K2 / 4)) * 4;
-        *reinterpret_cast<f32x4*>(ws + r * L::LDW + c) = wv[i];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int kh = (c >> 1) + 2 * j1, kw = (c & 1) + 2 * j2;
-#pragma unroll
-        for (int ks = 2 * hh; ks < 2 * hh + 2; ++ks)
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-            wb[c][ks][ct] = lds_frag_k(ws + (ks * KS - 32 * hh) * L::LDW + (kh * KS2 + kw) * OC1 + 16 * ct,
-                                       L::LDW, lane);
-      }
-    }
-    __syncthreads();  // the staging area becomes the frame tiles
+      for (int ct = 0; ct < 2; ++ct)
+        wb[t][ks][ct] = F::load(w2t + (size_t)((kh * KS2 + kw) * OC1 + 16 * ct + (lane & 15)) * OC2 + ks * KS + kl);
   }
-  // zero the dY1 rows no pixel writes (225..239) and the dY2 pad rows (36..47) once
+  // zero the dY1 rows no pixel writes (225..239), the dY2 pad rows (36..47) and each Z tile's
+  // zero row once
+  if (lane < OC1) *reinterpret_cast<f32x4*>(zw + P2 * LDZ + 4 * lane) = F::zero();
   for (int e = tid; e < (L::NROW - c1::NPIX) * LDX / 4; e += 256)
     *reinterpret_cast<f32x4*>(dyt + c1::NPIX * LDX + 4 * e) = F::zero();
   for (int e = tid; e < (L::DROWS - P2) * LDD / 4; e += 256)
     *reinterpret_cast<f32x4*>(d2s + P2 * LDD + 4 * e) = F::zero();
-  const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDI;
-  // gather item of this thread: channels 4 cg .. 4 cg + 3 of cells s and s + 32 of a class
-  const int cg = tid & 7, sl = tid >> 3;
+  const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDIB;  // conv1 wgrad: tap = wave
+  // gather items of this lane: channels 4 cg .. 4 cg + 3 of class cells (qy = i, qx = slot)
+  const int cg = lane & 7, slot = lane >> 3;
   for (int f = f0; f < f1; ++f) {
     __syncthreads();  // the previous frame's readers are done
-    c1_stash_frame<float, LDI>(img, tid, nv);
+    // frame bytes -> s2d byte rows: the 4 bytes of a 32-bit word are d = 0..3 of one channel row
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int vi = tid + i * 256, ci = vi >> 8, yy = (vi & 255) >> 2, xq = vi & 3;
+      const int Y = yy >> 2, b = yy & 3;
+      const uint32_t w[4] = {nv[i].x, nv[i].y, nv[i].z, nv[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<uint32_t*>(img + (Y * c1::GRID + 4 * xq + q) * LDIB + ci * 16 + b * 4) = w[q];
+    }
 #pragma unroll
     for (int i = 0; i < ND2; ++i) {
       const int e = tid + i * 256;
@@ -728,68 +718,75 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     if (tid < c1::NPIX) msk[tid] = nmk;
     __syncthreads();
     if (f + 1 < f1) fetch(f + 1);
-    // ---- conv2 dgrad: the dY2 A fragments of the 3 row tiles, then the four classes ----
-    V a2[3][NKO];
-#pragma unroll
-    for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-      for (int ks = 0; ks < NKO; ++ks)
-        a2[rt][ks] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + ks * KS + kl);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float* zc = smem + L::Z0 + (c & 1) * L::ZSZ;
-      f32x4 z[3][2];
+    // ---- conv2 dgrad of class `wave`: Z = dY2 rows x W2 (two halves of 2 taps) ----
+    {
+      V a2[3][NKO];
 #pragma unroll
       for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) z[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < NKO; ++ks)
+          a2[rt][ks] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + ks * KS + kl);
 #pragma unroll
-      for (int ks = 0; ks < NKO; ++ks)
+      for (int hf = 0; hf < 2; ++hf) {
+        f32x4 z[3][4];  // [row tile][tap 2 hf + (cc >> 1), ci tile cc & 1]
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
-          for (int ct = 0; ct < 2; ++ct) z[rt][ct] = F::mma(a2[rt][ks], wb[c][ks][ct], z[rt][ct]);
-      // Z[op][w * 32 + ci] (rows op < 36 only)
+          for (int cc = 0; cc < 4; ++cc) z[rt][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int rt = 0; rt < 3; ++rt)
+        for (int ks = 0; ks < NKO; ++ks)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int op = 16 * rt + kl + q;
-          if (op < P2) {
+          for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct) zc[op * LDZ + wave * OC1 + 16 * ct + (lane & 15)] = z[rt][ct][q];
-          }
-        }
-      __syncthreads();
-      // ---- col2im of class c = (py, px): input pixel (2 qy + py, 2 qx + px) sums taps
-      // (kh, kw) = (py + 2 j1, px + 2 j2) at dY2 cell (qy - j1, qx - j2), order j1, j2 ----
-      const int py = c >> 1, px = c & 1;
+            for (int cc = 0; cc < 4; ++cc)
+              z[rt][cc] = F::mma(a2[rt][ks], wb[2 * hf + (cc >> 1)][ks][cc & 1], z[rt][cc]);
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int cell = sl + 32 * h2, qy = cell >> 3, qx = cell & 7;
-        const int iy = 2 * qy + py, ix = 2 * qx + px;
-        if (iy < H1 && ix < H1) {
-          f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int oy = qy - (t >> 1), ox = qx - (t & 1);
-            if (oy >= 0 && oy < H2 && ox >= 0 && ox < H2)
-              sum += *reinterpret_cast<const f32x4*>(zc + (oy * H2 + ox) * LDZ + t * OC1 + 4 * cg);
-          }
-          const int p = iy * H1 + ix;
-          const uint32_t m = msk[p];
-          f32x4 v;
+        for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            v[q] = (m >> (4 * cg + q)) & 1u ? sum[q] : 0.f;
-            bsum[q] += v[q];
+            const int op = 16 * rt + kl + q;
+            if (op < P2) {
+#pragma unroll
+              for (int cc = 0; cc < 4; ++cc)
+                zw[op * LDZ + (2 * hf + (cc >> 1)) * OC1 + 16 * (cc & 1) + (lane & 15)] = z[rt][cc][q];
+            }
           }
-          *reinterpret_cast<f32x4*>(dyt + p * LDX + 4 * cg) = v;
-        }
       }
     }
+    // the wave's own Z stores are done before its gather reads them (LDS is in order per wave;
+    // the wait + clobber keeps the compiler from moving the reads up)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- col2im of class (py, px): input pixel (2 qy + py, 2 qx + px) sums taps
+    // (kh, kw) = (py + 2 j1, px + 2 j2) at dY2 cell (qy - j1, qx - j2), order j1, j2 ----
+    // Branch-free: every term is loaded (an out-of-range tap reads the zero row; + 0 leaves the
+    // sum of the in-range terms unchanged), so all of a lane's reads can be in flight at once.
+#pragma unroll
+    for (int qy = 0; qy < 8; ++qy) {
+      const int qx = slot, iy = 2 * qy + py, ix = 2 * qx + px;
+      const bool pv = iy < H1 && ix < H1;
+      f32x4 zt[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int oy = qy - (t >> 1), ox = qx - (t & 1);
+        const bool ok = pv && oy >= 0 && oy < H2 && ox >= 0 && ox < H2;
+        zt[t] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + t * OC1 + 4 * cg);
+      }
+      f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) sum += zt[t];
+      const int p = pv ? iy * H1 + ix : 0;
+      const uint32_t m = pv ? msk[p] : 0u;
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = (m >> (4 * cg + q)) & 1u ? sum[q] : 0.f;
+        bsum[q] += v[q];
+      }
+      if (pv) *reinterpret_cast<f32x4*>(dyt + p * LDX + 4 * cg) = v;
+    }
     __syncthreads();  // dY1 complete
-    // ---- conv1 weight gradient over the 240 pixel rows (as conv12_bwd_body's fp32 path) ----
+    // ---- conv1 weight gradient over the 240 pixel rows: A = dY1 (k = pixel), B = the s2d
+    // image bytes at row(pixel, tap = wave), converted to fp32 ----
     auto frag = [&](int kk, V* a, V* b) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
@@ -797,12 +794,12 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
       int rr[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
-        rr[jj] = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDI + tapoff + col;
+        rr[jj] = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDIB + tapoff + col;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         V v;
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) v[jj] = img[rr[jj] + 16 * j];
+        for (int jj = 0; jj < 4; ++jj) v[jj] = (float)img[rr[jj] + 16 * j];
         b[j] = v;
       }
     };
@@ -818,7 +815,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
         for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
     }
   }
-  // conv1 bias: the 32 threads of each channel group in a fixed order
+  // conv1 bias: the 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order
   __syncthreads();  // every frame's readers are done: the Z area holds the bias partials
   float* bred = smem + L::Z0;
   *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
@@ -841,14 +838,13 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     }
 }
 
-// The kernel body, on workgroup `wg` with the LDS passed in (C12BLds<T>::BYTES)
 template <typename T>
 DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2,
-                         const T* __restrict__ dy2, const uint32_t* __restrict__ mask1,
+                         const T* __restrict__ w2t, const T* __restrict__ dy2, const uint32_t* __restrict__ mask1,
                          float* __restrict__ slab, float* __restrict__ slab_bias, int N, int fpw,
                          int wg, char* __restrict__ lds) {
   if constexpr (sizeof(T) == 4) {  // fp32: the scatter-form body above
-    conv12_bwd_body_f32(x, reinterpret_cast<const float*>(w2), reinterpret_cast<const float*>(dy2),
+    conv12_bwd_body_f32(x, reinterpret_cast<const float*>(w2t), reinterpret_cast<const float*>(dy2),
                         mask1, slab, slab_bias, N, fpw, wg, lds);
     return;
   }
@@ -1166,11 +1162,12 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
 template <typename T>
 __global__ __launch_bounds__(256 * c12_groups<T>()) void conv12_bwd_s2d(const uint8_t* __restrict__ x,
                                                       const T* __restrict__ w2,     // [64][512]
+                                                      const T* __restrict__ w2t,    // [512][64] (fp32)
                                                       const T* __restrict__ dy2,    // [N][36][64]
                                                       const uint32_t* __restrict__ mask1,  // [N][225]
                                                       float* __restrict__ slab,
                                                       float* __restrict__ slab_bias, int N,
                                                       int fpw) {
   __shared__ __attribute__((aligned(16))) char lds[C12BLds<T>::BYTES];
-  conv12_bwd_body<T>(x, w2, dy2, mask1, slab, slab_bias, N, fpw, (int)blockIdx.x, lds);
+  conv12_bwd_body<T>(x, w2, w2t, dy2, mask1, slab, slab_bias, N, fpw, (int)blockIdx.x, lds);
 }

@@ -440,15 +440,17 @@ stage_b:
     if (int r = klaunch(h, K_LNC12_BWD, "ln_conv3_conv2_dgrad_conv1_wgrad", lnc3_conv12_bwd<T>,
                         dim3(h->n_ln_wg), dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy,
                         (const T*)h->act3, (const float*)h->lnstat,
-                        (const float*)(h->vecs + Vecs::lng), sw + sh.w3, (const T*)h->act2,
-                        (T*)h->dact3, (T*)h->dact2, h->s_ln, b->obs, sw + sh.w2,
-                        (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N, h->ln_fpw))
+                        (const float*)(h->vecs + Vecs::lng), sw + sh.w3, sw + sh.w3t,
+                        (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, b->obs,
+                        sw + sh.w2, sw + sh.w2t, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
+                        h->ln_fpw))
       return r;
   } else if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
     if (int r = klaunch(h, K_LNC3_BWD, "ln_bwd_conv3_dgrad", lnc3_bwd<T>, dim3(h->n_ln_wg),
                         dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy, (const T*)h->act3,
                         (const float*)h->lnstat, (const float*)(h->vecs + Vecs::lng), sw + sh.w3,
-                        (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, N, h->ln_fpw))
+                        sw + sh.w3t, (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, N,
+                        h->ln_fpw))
       return r;
   } else {
     if (int r = klaunch(h, K_LN_BWD, "ln_bwd", ln_bwd_kernel<T>, dim3(h->n_ln_wg), dim3(256), st,
@@ -534,7 +536,7 @@ conv12b:
   if (!lc12)
     if (int r = klaunch(h, K_CONV12_BWD, "conv2_dgrad_conv1_wgrad", conv12_bwd_s2d<T>,
                         dim3(h->c1_wg), dim3(256 * c12_groups<T>()), st, b->obs, sw + sh.w2,
-                        (const T*)h->dact2, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
+                        sw + sh.w2t, (const T*)h->dact2, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
                         h->c1_fpw))
       return r;
   // ---- last slab reduction (conv1) + loss metrics + step += 1; the other branches were

@@ -452,11 +452,13 @@ DEV void write_shadow(const ShadowPtrs& sp, const Canon& cn, const Shadow& sh, s
     const int k = (int)(i - cn.w2), oc = k / K2, rem = k % K2, ci = rem >> 4, kh = (rem >> 2) & 3,
               kw = rem & 3;
     w[sh.w2 + oc * K2 + (kh * 4 + kw) * OC1 + ci] = pt;
+    if constexpr (sizeof(T) == 4) w[sh.w2t + ((kh * 4 + kw) * OC1 + ci) * OC2 + oc] = pt;
   } else if (i < cn.w3) {
     vv[Vecs::b2 + (i - cn.b2)] = p;
   } else if (i < cn.b3) {
     const int k = (int)(i - cn.w3), oc = k / K3, rem = k % K3, ci = rem / 9, tap = rem % 9;
     w[sh.w3 + oc * K3 + tap * OC2 + ci] = pt;
+    if constexpr (sizeof(T) == 4) w[sh.w3t + (tap * OC2 + ci) * OC3 + oc] = pt;
   } else if (i < cn.lng) {
     vv[Vecs::b3 + (i - cn.b3)] = p;
   } else if (i < cn.lnb) {

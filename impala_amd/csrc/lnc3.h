@@ -33,11 +33,10 @@ template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 
 template <typename T> struct Lnc3Lds {
   static constexpr int VEC = 16 / (int)sizeof(T), LD3 = OC3 + 2 * VEC, LW = K3 + 2 * VEC;
   static constexpr int G = lnc3_groups<T>();
-  static constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
+  static constexpr int ZB = (P3 + 1) * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
   static constexpr bool REG = sizeof(T) == 2;
-  // W3 staging: bf16 all 64 rows at once; fp32 (147 KB) in two passes of 32 rows of K3 + 4
-  static constexpr int LWF = K3 + 4;
-  static constexpr int STG = REG ? OC3 * LW * (int)sizeof(T) : (OC3 / 2) * LWF * 4;
+  // W3 staging (bf16; fp32 loads its fragments from the transposed copy)
+  static constexpr int STG = REG ? OC3 * LW * (int)sizeof(T) : 0;
   static constexpr int SMEM = STG > G * GB ? STG : G * GB;
   static constexpr int RED = SMEM, COMB = RED + G * 4 * 2 * 4, BYTES = COMB + 2 * FLAT * 4;
 };
@@ -47,7 +46,8 @@ template <typename T> struct Lnc3Lds {
 template <typename T>
 DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
                    const float* __restrict__ stats, const float* __restrict__ gam,
-                   const T* __restrict__ w3, const T* __restrict__ act2, T* __restrict__ dact3,
+                   const T* __restrict__ w3, const T* __restrict__ w3t,
+                   const T* __restrict__ act2, T* __restrict__ dact3,
                    T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw, int wg,
                    char* __restrict__ lds) {
   using F = Frag<T>;
@@ -59,8 +59,9 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
   constexpr int NKS = K3 / KS;
   constexpr int NKO = OC3 / KS;                      // k-steps per tap (K = oc)
   constexpr int G = lnc3_groups<T>();
-  // one group's LDS: Z (fp32 [16][ZR]) then the dact3 tile (T [16][LD3]), in bytes
-  constexpr int ZB = P3 * lc3::ZR * 4, GB = ZB + P3 * LD3 * (int)sizeof(T);
+  // one group's LDS: Z (fp32 [16 + 1][ZR]: row 16 stays zero, read by the gather's
+  // out-of-range taps) then the dact3 tile (T [16][LD3]), in bytes
+  constexpr int ZB = Lnc3Lds<T>::ZB, GB = Lnc3Lds<T>::GB;
   constexpr bool REG = sizeof(T) == 2;               // bf16: W3 fragments in registers
   static_assert(GB % 16 == 0 && Lnc3Lds<T>::SMEM % 16 == 0, "group alignment");
   char* smem_b = lds;
@@ -98,36 +99,13 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
   // registers for the whole frame run (bf16 72, fp32 144 VGPRs) ----
   V wa[NKS];
   if constexpr (!REG) {
-    // fp32: W3 (147 KB) staged through LDS in two passes of 32 oc rows (coalesced 16-byte
-    // loads, rows of K3 + 4 floats), the fragments of the pass's k-steps read from LDS: rows
-    // 4 apart of one read sit 16 banks apart (conflict-free)
-    constexpr int LWF = Lnc3Lds<T>::LWF, HALF = OC3 / 2, NV = HALF * K3 / 4, NT = 256 * G;
-    constexpr int NPT = NV / NT;
-    static_assert(NV % NT == 0 && HALF * LWF * 4 <= Lnc3Lds<T>::SMEM, "fp32 W3 staging");
-    float* ws = reinterpret_cast<float*>(smem_b);
+    // fp32: 16-byte loads from the transposed copy w3t[tap*64 + ci][oc] (k = oc contiguous),
+    // all 36 in flight at once, consumed in the frame loop
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      f32x4 wv[NPT];
-#pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int e = (int)threadIdx.x + i * NT;
-        wv[i] = *reinterpret_cast<const f32x4*>(w3 + (size_t)(HALF * hh) * K3 + (size_t)e * 4);
-      }
-      if (hh) __syncthreads();  // the first pass's fragment reads are done
-#pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int e = (int)threadIdx.x + i * NT, r = e / (K3 / 4), c = (e % (K3 / 4)) * 4;
-        *reinterpret_cast<f32x4*>(ws + r * LWF + c) = wv[i];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
-        if ((oc0 >> 5) == hh)
-          wa[ks] = lds_frag_k(ws + (oc0 - HALF * hh) * LWF + tap * OC2 + 16 * wave, LWF, lane);
-      }
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int k = ks * KS, tap = k >> 6, oc0 = k & 63;
+      wa[ks] = F::load(w3t + (size_t)(tap * OC2 + 16 * wave + (lane & 15)) * OC3 + oc0 + kl);
     }
-    __syncthreads();  // the staging area becomes the Z / dact3 tiles
   } else {
     constexpr int NV = OC3 * K3 / VEC, NT = 256 * G, NPT = (NV + NT - 1) / NT;
     V wv[NPT];  // all loads in flight at once, then the LDS stores
@@ -156,6 +134,8 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 #pragma unroll
   for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(gm[q]));
 
+  for (int e = tid; e < lc3::ZR / 4; e += 256)  // the zero row of this group's Z tile
+    *reinterpret_cast<f32x4*>(zs + P3 * lc3::ZR + 4 * e) = f32x4{0.f, 0.f, 0.f, 0.f};
   const int n_it = (f1 - f0 + G - 1) / G;
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
@@ -225,15 +205,20 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
         const int e = tid + 256 * r;
         if (e < P2 * 16) {
           const int px = e >> 4, ci = 4 * (e & 15), iy = px / H2, ix = px - iy * H2;
-          f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+          // branch-free: out-of-range taps read the zero row (+ 0 leaves the sum unchanged)
+          f32x4 zt[9];
 #pragma unroll
           for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
               const int oy = iy - kh, ox = ix - kw;
-              if (oy >= 0 && oy < H3 && ox >= 0 && ox < H3)
-                sum += *reinterpret_cast<const f32x4*>(zs + (oy * H3 + ox) * lc3::ZR + (kh * 3 + kw) * OC2 + ci);
+              const bool ok = oy >= 0 && oy < H3 && ox >= 0 && ox < H3;
+              zt[kh * 3 + kw] = *reinterpret_cast<const f32x4*>(
+                  zs + (ok ? oy * H3 + ox : P3) * lc3::ZR + (kh * 3 + kw) * OC2 + ci);
             }
+          f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < 9; ++t) sum += zt[t];
           float o[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) o[q] = am[r][q] > 0.f ? sum[q] : 0.f;
@@ -264,10 +249,11 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 template <typename T>
 __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
     const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
-    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ act2,
-    T* __restrict__ dact3, T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw) {
+    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ w3t,
+    const T* __restrict__ act2, T* __restrict__ dact3, T* __restrict__ dact2,
+    float* __restrict__ slab, int N, int fpw) {
   __shared__ __attribute__((aligned(16))) char lds[Lnc3Lds<T>::BYTES];
-  lnc3_body<T>(dy, act3, stats, gam, w3, act2, dact3, dact2, slab, N, fpw, (int)blockIdx.x, lds);
+  lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, slab, N, fpw, (int)blockIdx.x, lds);
 }
 
 // LayerNorm backward + conv3 input gradient, then conv2 input gradient + conv1 weight gradient,
@@ -279,14 +265,15 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
 template <typename T>
 __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_conv12_bwd(
     const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
-    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ act2,
-    T* __restrict__ dact3, T* __restrict__ dact2, float* __restrict__ ln_slab,
-    const uint8_t* __restrict__ x, const T* __restrict__ w2, const uint32_t* __restrict__ mask1,
+    const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ w3t,
+    const T* __restrict__ act2, T* __restrict__ dact3, T* __restrict__ dact2,
+    float* __restrict__ ln_slab, const uint8_t* __restrict__ x, const T* __restrict__ w2,
+    const T* __restrict__ w2t, const uint32_t* __restrict__ mask1,
     float* __restrict__ c1_slab, float* __restrict__ c1_slab_bias, int N, int fpw) {
   static_assert(lnc3_groups<T>() == c12_groups<T>(), "one block shape for both bodies");
   constexpr int B1 = Lnc3Lds<T>::BYTES, B2 = C12BLds<T>::BYTES;
   __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
-  lnc3_body<T>(dy, act3, stats, gam, w3, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
+  lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
   __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
-  conv12_bwd_body<T>(x, w2, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds);
+  conv12_bwd_body<T>(x, w2, w2t, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds);
 }

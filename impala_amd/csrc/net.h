@@ -12,6 +12,8 @@
 //   wh  [16][256]        rows 0..A-1 actor, row 15 critic, rest 0
 // (the dgrads read w2 / w3 / wfc k-major through LDS: no transposed copies)
 //   wht [256][32]        [j][o'], o' >= 16 zero
+//   w2t [512][64]        [(kh*4+kw)*32 + ci][oc]   (fp32 only: the dgrads' B fragments as one
+//   w3t [576][64]        [(kh*3+kw)*64 + ci][oc]    16-byte load, k = oc contiguous)
 //   f32: b1[32] b2[64] b3[64] lng[1024] lnb[1024] (p*64+c order) bfc[256] bh[16]
 #pragma once
 #include <stddef.h>
@@ -57,7 +59,7 @@ inline Canon canon(int A) {
 
 // shadow-weight element offsets (elements of the compute type T), 64-element aligned
 struct Shadow {
-  size_t w1, w2, w3, wfc, wh, wht, total;
+  size_t w1, w2, w3, wfc, wh, wht, w2t, w3t, total;
 };
 constexpr size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 inline Shadow shadow() {
@@ -69,6 +71,8 @@ inline Shadow shadow() {
   s.wfc = o; o = al64(o + (size_t)HID * FLAT);
   s.wh = o; o = al64(o + (size_t)HEADS * HID);
   s.wht = o; o = al64(o + (size_t)HID * HPAD);
+  s.w2t = o; o = al64(o + (size_t)OC2 * K2);
+  s.w3t = o; o = al64(o + (size_t)OC3 * K3);
   s.total = o;
   return s;
 }
