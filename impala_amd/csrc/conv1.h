@@ -208,6 +208,9 @@ template <typename T> constexpr int c12f_groups() { return sizeof(T) == 2 ? 2 : 
 // frame, with the same k-step order and fragment layout as gemm_tile<Conv3LnFwd> and the same
 // ln_frame_epilogue, so act3 / y / stats are bit-identical to the separate conv3 launch.
 constexpr int C3T_FMAX = 6;  // frames per workgroup the tail supports (wave per frame, LDS)
+// fp32: the frames' act2 tiles (36 cells of 68 floats each) fit beside the image and the act1
+// tile for at most 5 frames (C2's run: 1280 frames / 256 workgroups)
+template <typename T> constexpr int c3t_fmax() { return sizeof(T) == 2 ? C3T_FMAX : 5; }
 template <typename T> struct C3Tail {
   const T* w3;       // kernel-layout W3 [64][576 = tap*64 + ci]
   const float* b3;
@@ -224,8 +227,9 @@ template <typename T> struct C12FLds {
   static constexpr int VEC = 16 / (int)sizeof(T), LDA1 = OC1 + VEC, A1P = 22;
   static constexpr int IMGSZ = c1::FROWS * c1::LF<T>::LDI, GSZ = IMGSZ + A1P * 16 * LDA1;
   static constexpr int LDA2 = OC2 + VEC;
-  static constexpr int A2W = H2 + 1;  // act2 tile rows: 6 x 7 cells (one pad column)
-  static constexpr int A2SZ = sizeof(T) == 2 ? C3T_FMAX * H2 * A2W * LDA2 : 0;
+  // act2 tile rows: bf16 6 x 7 cells (one pad column), fp32 6 x 6 (the LDS budget)
+  static constexpr int A2W = sizeof(T) == 2 ? H2 + 1 : H2;
+  static constexpr int A2SZ = c3t_fmax<T>() * H2 * A2W * LDA2;
   static constexpr int ELEMS = c12f_groups<T>() * GSZ + A2SZ;
 };
 
@@ -256,10 +260,10 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // pixel row (a pad column): the conv3 window reads 2.0x instead of 3.0x, stores 2.0x
   // instead of 1.67x (tools/ldsbank.py)
   constexpr int LDA2 = OC2 + VEC, A2W = C12FLds<T>::A2W, A2F = H2 * A2W;
-  constexpr int A2SZ = W2REG ? C3T_FMAX * A2F * LDA2 : 0;
+  constexpr int A2SZ = c3t_fmax<T>() * A2F * LDA2;
   static_assert(G * GSZ + A2SZ == C12FLds<T>::ELEMS && GSZ == C12FLds<T>::GSZ, "LDS layout");
   T* a2s = smem + G * GSZ;
-  const bool tail = W2REG && c3.act3 != nullptr;
+  const bool tail = c3.act3 != nullptr;
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   T* img = smem + grp * GSZ;
   T* a1s = img + IMGSZ;
@@ -532,6 +536,47 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         else
           ln_frame_epilogue<T>(et, LDE, f0 + gw, lane, lk, c3.act3, c3.y, c3.stats);
       }
+    }
+  }
+  if constexpr (!W2REG) {
+    if (tail) {
+      // ---- fp32 conv3 + ReLU + LayerNorm of this workgroup's frames (the frame loop ended
+      // with a barrier: the image / act1 areas are free, act2 is in a2s).  Wave w computes oc
+      // tile w of every frame: its W3 rows (the A operand, 144 VGPRs) by 16-byte loads, the act2
+      // window of each output pixel from LDS; the same k-step order and fragments as
+      // gemm_tile<Conv3LnFwd> and the same ln_frame_epilogue, so act3 / y / stats are
+      // bit-identical to the separate conv3 launch. ----
+      constexpr int FMAX = c3t_fmax<T>(), NKS3 = K3 / KS, LDE = OC3 + 4;
+      static_assert(FMAX * P3 * LDE <= G * GSZ, "fp32 conv3 tail LDS");
+      V w3a[NKS3];
+#pragma unroll
+      for (int ks = 0; ks < NKS3; ++ks)
+        w3a[ks] = F::load(c3.w3 + (size_t)(16 * wave + (lane & 15)) * K3 + ks * KS + kl);
+      const int nF = f1 - f0;
+      const LnLane lk = ln_lane_consts(lane, c3.b3, c3.gam, c3.bet);
+      const int p = lane & 15, oy = p >> 2, ox = p & 3;
+      const T* a2f = a2s + (oy * A2W + ox) * LDA2 + kl;
+      f32x4 acc3[FMAX];
+#pragma unroll
+      for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS3; ++ks) {  // k = ks*16 + kl: tap = k / 64, ci = k % 64
+        const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+        for (int fr = 0; fr < FMAX; ++fr) {
+          if (fr < nF) {
+            const V b = *reinterpret_cast<const V*>(a2f + (fr * A2F + kh * A2W + kw) * LDA2 + (k & 63));
+            acc3[fr] = F::mma(w3a[ks], b, acc3[fr]);
+          }
+        }
+      }
+      float* ets = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int fr = 0; fr < FMAX; ++fr)
+        if (fr < nF) *reinterpret_cast<f32x4*>(ets + (fr * P3 + p) * LDE + 16 * wave + 4 * (lane >> 4)) = acc3[fr];
+      __syncthreads();
+      for (int fr = wave; fr < nF; fr += 4)
+        ln_frame_epilogue<T>(ets + fr * P3 * LDE, LDE, f0 + fr, lane, lk, c3.act3, c3.y, c3.stats);
     }
   }
 }

@@ -249,10 +249,10 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
   bool conv3_done = false;
   if (h->fwd_fused) {  // conv1 + conv2 per frame (act1 consumed from LDS)
     const int fpw = h->c12f_fpw > 0 ? h->c12f_fpw : std::max(1, cdiv(n, h->n_cu));
-    // bf16 with at most C3T_FMAX frames per workgroup: conv3 + ReLU + LayerNorm run as the
-    // kernel's tail (one launch for the whole conv trunk)
+    // at most c3t_fmax<T>() frames per workgroup (bf16 6, fp32 5): conv3 + ReLU + LayerNorm
+    // run as the kernel's tail (one launch for the whole conv trunk)
     C3Tail<T> c3{};
-    if (sizeof(T) == 2 && h->c3_tail && fpw <= C3T_FMAX) {
+    if (h->c3_tail && fpw <= c3t_fmax<T>()) {
       c3.w3 = sw + sh.w3; c3.b3 = vv + Vecs::b3; c3.gam = vv + Vecs::lng; c3.bet = vv + Vecs::lnb;
       c3.act3 = (T*)h->act3; c3.y = (T*)h->y; c3.stats = h->lnstat;
       conv3_done = true;
@@ -260,7 +260,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     // training forward (no heads launch after it): the FC forward joins the launch, each FC
     // tile waiting on flags of the conv workgroups that produce its frames (not under graph
     // capture: the epoch argument changes every launch)
-    if (conv3_done && !with_heads && h->fwd_chain && !h->use_graph) {
+    if (sizeof(T) == 2 && conv3_done && !with_heads && h->fwd_chain && !h->use_graph) {
       if (++h->chain_epoch == 0) h->chain_epoch = 1;
       c3.y_sc1 = 1;
       using CC = FwdChainCfg<T>;

@@ -318,6 +318,36 @@ def test_launch_modes_agree(env, exact, monkeypatch):
         np.testing.assert_allclose(base[1], alt[1], rtol=1e-2, atol=3e-3)
 
 
+@pytest.mark.parametrize("env", [{"IMPALA_GRAPH": "1"}, {"IMPALA_FC_MERGED": "0"},
+                                 {"IMPALA_WG23_MERGED": "0"}, {"IMPALA_C3_TAIL": "0"},
+                                 {"IMPALA_LC12": "0"}, {"IMPALA_SIDE_STREAM": "1"},
+                                 {"IMPALA_FWD_FUSED": "0"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_launch_modes_agree_fp32(env, monkeypatch):
+    """The fp32 headline path (the reference's arithmetic): every fused / merged launch --
+    the conv3 + LayerNorm tail of the forward, the fused per-frame backward, the merged FC and
+    conv weight-gradient launches -- is bit-identical to the separate kernels it replaces, at
+    C2's frame run (B=64, T=20: 5 frames per workgroup, the fp32 tail's limit)."""
+    dev = _dev()
+    batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(64, 20, 15, seed=16)]
+
+    def run():
+        m = _model(dev, "fp32", seed=0)
+        e = _engine(m, 64, 20)
+        for _ in range(2):
+            e.train_step(*batch)
+        torch.cuda.synchronize()
+        return m.flat.cpu().numpy().copy(), e.metrics.cpu().numpy().copy()
+
+    base = run()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    alt = run()
+    np.testing.assert_array_equal(base[0], alt[0])
+    np.testing.assert_array_equal(base[1], alt[1])
+    assert np.isfinite(base[1]).all()
+
+
 @pytest.mark.parametrize("B,T", [(24, 64), (160, 20)])
 def test_merged_launches_at_other_frame_runs(B, T, monkeypatch):
     """The merged / fused launches against the separate ones, bitwise, where the per-workgroup
