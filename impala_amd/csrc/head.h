@@ -45,7 +45,8 @@ struct HeadArgs {
   float* slab_bh;       // [gridDim.x][16]
   float* heads_out;     // optional [N][16] (logits + value), nullptr = skip
   float* vt_dbg;        // optional debug export (IMPALA only): adv, err, q [3][B][T-1] then
-                        // rho [B][T] -- the step's own V-trace outputs (impala_set_debug_vtrace)
+                        // rho [B][T] and the values v [B][T] the scan ran on -- the step's own
+                        // V-trace inputs / outputs (impala_set_debug_vtrace)
 };
 
 constexpr int HEAD_SPLIT = 4;              // workgroups per trajectory group (hidden-column slices)
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
           a.vt_dbg[2 * BL + o] = qq;
         }
         a.vt_dbg[3 * BL + f0 + fl] = rho;
+        a.vt_dbg[3 * BL + (size_t)a.B * T_ + f0 + fl] = v;
       }
       if (valid) {
         const float c_pg = 1.f / (float)(a.B * L);

@@ -109,7 +109,8 @@ class Engine:
 
     def debug_vtrace(self, enable: bool = True):
         """Export the step's own V-trace from the fused head (impala_set_debug_vtrace): returns a
-        dict of device views ``adv``, ``err``, ``q`` [B,T-1] and ``rho`` [B,T], refilled by every
+        dict of device views ``adv``, ``err``, ``q`` [B,T-1], ``rho`` and the values ``v`` [B,T] the
+        scan ran on, refilled by every
         following training step; ``enable=False`` turns the export off (returns None)."""
         if not enable:
             check(_lib.lib().impala_set_debug_vtrace(self._h, None), "impala_set_debug_vtrace")
@@ -117,12 +118,13 @@ class Engine:
             return None
         B, T = self.batch_size, self.rollout_length
         L = T - 1
-        buf = torch.zeros(3 * B * L + B * T, dtype=torch.float32, device=self.device)
+        buf = torch.zeros(3 * B * L + 2 * B * T, dtype=torch.float32, device=self.device)
         check(_lib.lib().impala_set_debug_vtrace(self._h, ptr(buf)), "impala_set_debug_vtrace")
         self._vt_dbg = buf  # keeps the buffer alive while the library writes into it
         BL = B * L
         return {"adv": buf[:BL].view(B, L), "err": buf[BL:2 * BL].view(B, L),
-                "q": buf[2 * BL:3 * BL].view(B, L), "rho": buf[3 * BL:].view(B, T)}
+                "q": buf[2 * BL:3 * BL].view(B, L), "rho": buf[3 * BL:3 * BL + B * T].view(B, T),
+                "v": buf[3 * BL + B * T:].view(B, T)}
 
     # ------------------------------------------------------------------ compute
     def forward(self, obs: torch.Tensor, stream=None):

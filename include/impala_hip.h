@@ -131,7 +131,8 @@ int impala_set_step(impala_learner* h, int64_t step, void* stream);
 /* Debug export of the step's own V-trace (IMPALA handles): when `out` is non-NULL, every
  * following training step writes the pg_advantage, td_error and q_estimate it computed inside
  * the fused head ([3][B][T-1], learning.py:150-153) and the importance ratio rho ([B][T],
- * learning.py:148) to `out` (3*B*(T-1) + B*T floats, device memory).  NULL disables it. */
+ * learning.py:148), then the values v the scan ran on ([B][T], learning.py:146) to `out`
+ * (3*B*(T-1) + 2*B*T floats, device memory).  NULL disables it. */
 int impala_set_debug_vtrace(impala_learner* h, float* out);
 
 /* Policy/value forward of n frames (n <= B*T): logits [n][A], values [n]. */

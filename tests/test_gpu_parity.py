@@ -396,7 +396,8 @@ def test_bf16_tracks_fp32_over_100_steps_c2():
     """bf16 perf mode (bf16 operands, fp32 accumulation / master weights / Adam) against the
     fp32 parity mode for 100 learner steps at C2 (B=64, T=20) on 4 rotating synthetic batches
     from the same init.  Stated bounds (measured drift in DESIGN.md §2): per-step loss within
-    2 % (+0.02 abs) of fp32's, the final parameters within 2 % relative L2 of fp32's, and both
+    2 % (+0.02 abs) of fp32's, the final parameters within 2 % relative L2 of fp32's, the
+    update (final - initial parameters) within 15 % relative L2 of fp32's update, and both
     runs reduce the loss on their batches by the same amount to within 10 %."""
     dev = _dev()
     batches = [[_t(x, dev) for x in ref_cpu.synthetic_batch(64, 20, 15, seed=3000 + i)]
@@ -425,5 +426,7 @@ def test_bf16_tracks_fp32_over_100_steps_c2():
     assert np.all(np.isfinite(l16))
     assert np.all(dl <= 2e-2 * np.abs(l32) + 2e-2), dl.max()
     assert prl2 < 2e-2, prl2
+    # the update itself (params - init): 7.7e-2 measured (profiles/r03d/parity.log), bound 2x
+    assert upd < 0.15, upd
     drop32, drop16 = l32[:4].mean() - l32[-4:].mean(), l16[:4].mean() - l16[-4:].mean()
     assert drop32 > 0 and abs(drop16 - drop32) <= 0.1 * abs(drop32), (drop32, drop16)

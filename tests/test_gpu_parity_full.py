@@ -13,8 +13,16 @@ Three CPU yardsticks, all the same oracle step:
 
 North_star: "V-trace returns and losses match the reference CPU path within 1e-5 rel fp32".
 * V-trace outputs of the step itself -- pg_advantage, td_error, q_estimate [B,T-1] and rho
-  [B,T], exported from inside the fused head kernel (impala_set_debug_vtrace) -- element-wise
-  within 1e-5 relative to max(|x|, rms(x)) of each yardstick.
+  [B,T], exported from inside the fused head kernel (impala_set_debug_vtrace) -- within a
+  NORMWISE 1e-5: |hip - x| <= 1e-5 * (|x| + rms(x)) per element, rms over the whole output.
+  A pure element-wise relative bound cannot hold at the step level: the values the scan runs on
+  come out of the fp32 trunk forward (~1e-7..1e-6 relative rounding from its convolutions), and
+  advantages / TD errors are differences of such values that cross zero.  The element-wise
+  relative error (with a floor of 1e-3 * rms) is printed beside the bound.
+* The scan itself is element-wise: fed its own exported inputs (the values and rho the fused
+  head used), the fp64 oracle V-trace reproduces the kernel's adv / err / q within 1e-5
+  relative per element (floor: 1e-6 of the terms an output is a difference of), i.e. the step's V-trace deviation from the
+  yardsticks is the forward's rounding propagated, not the scan's.
 * The loss and every metric within 1e-5 relative of fp64 and native (and of fp32, or of
   twice fp32's own error when that is larger: grad_norm at C2).
 * The post-clip gradient within 1e-5 rel-L2 of fp64 and native; parameters after 1 step
@@ -92,7 +100,8 @@ def _run(B, T=20, A=15, seed=1234):
     torch.cuda.synchronize()
     hip = {"met": e.metrics.cpu().numpy().astype(np.float64),
            "vt": {k: v.cpu().numpy().copy() for k, v in dbg.items()},
-           "grad": m.flat_grad.cpu().numpy().copy(), "p": [m.flat.cpu().numpy().copy()]}
+           "grad": m.flat_grad.cpu().numpy().copy(), "p": [m.flat.cpu().numpy().copy()],
+           "batch": batch}
     e.debug_vtrace(False)
     for _ in range(2):
         e.train_step(*db)
@@ -110,7 +119,8 @@ CONFIGS = [pytest.param(8, id="C1_B8_T20"), pytest.param(64, id="C2_B64_T20")]
 def test_step_vtrace_outputs_match_oracle(B):
     """The V-trace the fused head computed inside the step (not a standalone call) against the
     oracle step's batched_vtrace(values[:, :-1], values[:, 1:], r, g, rho) (learning.py:150) and
-    rho (learning.py:148): |hip - x| <= 1e-5 * (|x| + rms(x)) element-wise."""
+    rho (learning.py:148): normwise, |hip - x| <= 1e-5 * (|x| + rms(x)) per element.  The pure
+    element-wise relative error (floor 1e-3 * rms) is printed for the record."""
     hip, ys = _run(B)
     for k in ("adv", "err", "q", "rho"):
         got = hip["vt"][k].astype(np.float64)
@@ -118,8 +128,45 @@ def test_step_vtrace_outputs_match_oracle(B):
             want = y["cap"][k].astype(np.float64)
             rms = float(np.sqrt(np.mean(want ** 2)))
             worst = float(np.max(np.abs(got - want) / (np.abs(want) + rms)))
-            print(f"B={B} {k} vs {name}: max |d| / (|x| + rms) = {worst:.2e}")
+            elem = float(np.max(np.abs(got - want) / np.maximum(np.abs(want), 1e-3 * rms)))
+            print(f"B={B} {k} vs {name}: normwise max |d| / (|x| + rms) = {worst:.2e}; "
+                  f"element-wise max |d| / max(|x|, 1e-3 rms) = {elem:.2e}")
             assert worst <= RTOL, (k, name, worst)
+
+
+@pytest.mark.parametrize("B", CONFIGS)
+def test_step_vtrace_scan_elementwise_on_its_own_inputs(B):
+    """The fused head's V-trace scan against the fp64 oracle scan (oracle/vtrace.py, the rlax
+    equations of learning.py:150-153) run on the values and rho the kernel itself used
+    (exported beside its outputs): element-wise 1e-5 relative, with a floor of 1e-6 of the
+    magnitude of the terms an output is the difference of (fp32 cancellation).  Also prints
+    how far the step's values are from each yardstick's: that forward rounding, propagated
+    through the scan, is the whole step-level V-trace deviation."""
+    from oracle.vtrace import vtrace_numpy
+    hip, ys = _run(B)
+    vt = hip["vt"]
+    v = vt["v"].astype(np.float64)
+    rho = vt["rho"].astype(np.float64)
+    r = np.asarray(hip["batch"][2], dtype=np.float64).reshape(v.shape)
+    g = np.asarray(hip["batch"][3], dtype=np.float64).reshape(v.shape)
+    adv, err, q = vtrace_numpy(v[:, :-1], v[:, 1:], r[:, :-1], g[:, :-1], rho[:, :-1])
+    # the terms each output is a difference of: adv = rho' (q - v), err = (e + v) - v,
+    # q = r + g boot; where they cancel, fp32 itself cannot keep 1e-5 of the (small) result,
+    # so the floor is 1e-6 (~16 fp32 ulp) of the terms' magnitude
+    terms = np.abs(v[:, :-1]) + np.abs(v[:, 1:]) + np.abs(r[:, :-1]) + np.abs(q)
+    for k, want in (("adv", adv), ("err", err), ("q", q)):
+        got = vt[k].astype(np.float64)
+        d = np.abs(got - want)
+        elem = float(np.max(d / np.maximum(np.abs(want), 1e-30)))
+        worst = float(np.max(d / (RTOL * np.abs(want) + 1e-6 * terms)))
+        print(f"B={B} scan {k} on its own inputs: max |d| / (1e-5 |x| + 1e-6 terms) = "
+              f"{worst:.2f}; pure element-wise max rel {elem:.2e}")
+        assert worst <= 1.0, (k, worst, elem)
+    for name, y in ys.items():
+        want = y["cap"]["values"].astype(np.float64)
+        rms = float(np.sqrt(np.mean(want ** 2)))
+        print(f"B={B} values vs {name}: max |d| {np.max(np.abs(v - want)):.2e} "
+              f"(rms {rms:.3e}, max |d| / rms {np.max(np.abs(v - want)) / rms:.2e})")
 
 
 def _rel(a, b):
