@@ -279,7 +279,7 @@ def run_host_staged(eng, batch, args, dist, model, world):
     """The PCIe-inclusive rate (SURVEY.md §8(d) secondary bound; never `value`): every step's
     batch comes from page-locked host memory through the library's staging ring
     (impala_stage, 2 slots), the H2D copies of step k+1 overlapping the update on step k."""
-    from impala_amd.distributed import compute_grads_allreduced
+    from impala_amd.distributed import compute_grads_allreduced, native_dp_buckets
     hosts = [[t.cpu().pin_memory() for t in batch] for _ in range(2)]
     eng.stage_init(2)
 
@@ -292,6 +292,8 @@ def run_host_staged(eng, batch, args, dist, model, world):
             b = eng.slot_batch(s)
             if dist is None:
                 eng.train_step(b)
+            elif getattr(eng, "_dp", False):
+                eng.dp_train_step(b, buckets=native_dp_buckets())
             else:
                 compute_grads_allreduced(eng, (b,), model.flat_grad)
                 eng.apply_update()
@@ -617,7 +619,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from impala_amd.distributed import compute_grads_allreduced
+    from impala_amd.distributed import (compute_grads_allreduced, native_dp_buckets,
+                                        native_dp_enabled)
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
 
@@ -634,10 +637,20 @@ def main():
         dist.broadcast(model.flat, 0)
         model.params_changed()
 
+    # data parallel: the library's own RCCL communicator (impala_dp_train_step) unless
+    # IMPALA_DP_NATIVE=0 selects the torch.distributed all-reduce
+    native_dp = dist is not None and native_dp_enabled()
+    dp_buckets = native_dp_buckets() if native_dp else None
+
     def make_step(e, m):
+        if native_dp:
+            e.dp_init()
+
         def step():
             if dist is None:
                 e.train_step(*batch)
+            elif native_dp:
+                e.dp_train_step(*batch, buckets=dp_buckets)
             else:
                 compute_grads_allreduced(e, batch, m.flat_grad)
                 e.apply_update()
@@ -675,7 +688,10 @@ def main():
         "data": "synthetic rollouts resident in HBM (obs u8 uniform, BASELINE.md §3); "
                 "random-init weights (reference layer_init_truncated, seed 0)",
         "config": {"workload": workload,
-                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                   "allreduce": (None if dist is None else
+                                 f"native RCCL communicator, {dp_buckets} bucket(s)" if native_dp
+                                 else "torch.distributed (c10d) RCCL")},
         "roofline": rooflines[0],
         "roofline_top2": rooflines,
         "step_roofline": step_roofline(value / world, step_flops_pf, args.dtype),

@@ -17,6 +17,7 @@ IMPALA_DTYPE_F32 = 0
 IMPALA_DTYPE_BF16 = 1
 IMPALA_ALGO_IMPALA = 0
 IMPALA_ALGO_PPO = 1
+DP_ID_BYTES = 128  # IMPALA_DP_ID_BYTES (ncclUniqueId)
 ABI_VERSION = 2
 NUM_METRICS = 9  # slots 0-6 METRIC_NAMES, 7 step, 8 PPO train/target
 METRIC_NAMES = ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl",
@@ -37,7 +38,7 @@ EXPORTS = (
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
     "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
     "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
-    "impala_timer_read_kernel",
+    "impala_timer_read_kernel", "impala_dp_unique_id", "impala_dp_init", "impala_dp_train_step",
 )
 # every symbol declared in include/sac_hip.h
 SAC_EXPORTS = (
@@ -129,6 +130,9 @@ def _declare(lib):
     lib.impala_grad_bucket_offset.restype = C.c_size_t
     lib.impala_grad_bucket_offset_fc.argtypes = [_P]
     lib.impala_grad_bucket_offset_fc.restype = C.c_size_t
+    lib.impala_dp_unique_id.argtypes = [_P]
+    lib.impala_dp_init.argtypes = [_P, _P, C.c_int, C.c_int]
+    lib.impala_dp_train_step.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int, _P]
     lib.impala_vtrace.argtypes = [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_float, C.c_float,
                                   C.c_float, _P, _P, _P, _P]
     lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,

@@ -7,6 +7,8 @@
 // tensors (state_dict, checkpoint, RCCL all-reduce) without copies.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <cmath>
 #include <cstdio>
@@ -202,6 +204,13 @@ struct impala_learner {
   int h2d_pull_wg = 0;        // > 0: copy with h2d_pull_kernel on that many workgroups
   int h2d_pull_threads = 256; // threads per pull workgroup (IMPALA_H2D_THREADS)
   hipStream_t h2d = nullptr;  // = h2d_s[0]
+  // native data-parallel step (impala_dp_*): the library's own RCCL communicator, so the
+  // gradient all-reduces are enqueued with no host round trip and no c10d bookkeeping; the FC +
+  // heads bucket is all-reduced on dp_stream while the per-frame backward runs
+  ncclComm_t dp_comm = nullptr;
+  hipStream_t dp_stream = nullptr;
+  hipEvent_t dp_ev[3] = {nullptr, nullptr, nullptr};
+  int dp_nranks = 0, dp_rank = -1;
 };
 
 namespace {
@@ -917,6 +926,57 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   return 0;
 }
 
+extern "C++" {
+namespace {
+// RCCL entry points, resolved by dlopen on first use: the library has no link-time RCCL
+// dependency, and inside a torch process the loader hands back torch's already-loaded copy
+// (same SONAME), so the handle's communicator and torch's live in one RCCL instance.
+struct RcclApi {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string err;
+};
+const RcclApi& rccl() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW);
+    if (!lib) lib = dlopen("librccl.so", RTLD_NOW);
+    if (!lib) {
+      const char* e = dlerror();
+      a.err = std::string("dlopen librccl: ") + (e ? e : "not found");
+      return a;
+    }
+    a.get_unique_id = (decltype(a.get_unique_id))dlsym(lib, "ncclGetUniqueId");
+    a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(lib, "ncclCommInitRank");
+    a.all_reduce = (decltype(a.all_reduce))dlsym(lib, "ncclAllReduce");
+    a.comm_destroy = (decltype(a.comm_destroy))dlsym(lib, "ncclCommDestroy");
+    a.error_string = (decltype(a.error_string))dlsym(lib, "ncclGetErrorString");
+    if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy || !a.error_string)
+      a.err = "librccl lacks an expected entry point";
+    return a;
+  }();
+  return api;
+}
+int rccl_fail(const char* what, ncclResult_t r) {
+  return fail(IMPALA_E_RCCL, std::string(what) + ": " + rccl().error_string(r));
+}
+void dp_release(impala_learner* h) {
+  if (h->dp_comm) (void)rccl().comm_destroy(h->dp_comm);
+  h->dp_comm = nullptr;
+  if (h->dp_stream) (void)hipStreamDestroy(h->dp_stream);
+  h->dp_stream = nullptr;
+  for (auto& e : h->dp_ev)
+    if (e) { (void)hipEventDestroy(e); e = nullptr; }
+  h->dp_nranks = 0;
+  h->dp_rank = -1;
+}
+}  // namespace
+}  // extern "C++"
+
 int impala_destroy(impala_learner* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
@@ -939,6 +999,7 @@ int impala_destroy(impala_learner* h) {
     (void)hipStreamSynchronize(h->side);
     (void)hipStreamDestroy(h->side);
   }
+  dp_release(h);
   if (h->ws) (void)hipFree(h->ws);
   delete h;
   return 0;
@@ -1107,6 +1168,75 @@ int impala_apply_update(impala_learner* h, void* stream) {
   CK(hipSetDevice(h->device));
   return run_graphed(h, G_UPDATE, nullptr, (hipStream_t)stream,
                      [&](hipStream_t s) { return enqueue_update(h, s); });
+}
+
+int impala_dp_unique_id(void* out) {
+  if (!out) return fail(IMPALA_E_INVALID, "null unique-id buffer");
+  const RcclApi& api = rccl();
+  if (!api.err.empty()) return fail(IMPALA_E_RCCL, api.err);
+  ncclUniqueId id;
+  if (ncclResult_t r = api.get_unique_id(&id)) return rccl_fail("ncclGetUniqueId", r);
+  static_assert(sizeof(ncclUniqueId) == IMPALA_DP_ID_BYTES, "unique id size");
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+int impala_dp_init(impala_learner* h, const void* unique_id, int nranks, int rank) {
+  if (!h || !unique_id) return fail(IMPALA_E_INVALID, "null argument");
+  if (nranks != h->cfg.world_size || rank < 0 || rank >= nranks)
+    return fail(IMPALA_E_INVALID, "nranks must equal the handle's world_size and 0 <= rank < nranks");
+  const RcclApi& api = rccl();
+  if (!api.err.empty()) return fail(IMPALA_E_RCCL, api.err);
+  CK(hipSetDevice(h->device));
+  dp_release(h);
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  // collective over the nranks processes (each blocks until all have joined)
+  if (ncclResult_t r = api.comm_init_rank(&h->dp_comm, nranks, id, rank)) {
+    h->dp_comm = nullptr;
+    return rccl_fail("ncclCommInitRank", r);
+  }
+  CK(hipStreamCreateWithFlags(&h->dp_stream, hipStreamNonBlocking));
+  for (auto& e : h->dp_ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  h->dp_nranks = nranks;
+  h->dp_rank = rank;
+  return 0;
+}
+
+int impala_dp_train_step(impala_learner* h, const impala_batch* b, int buckets, void* stream) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (!h->dp_comm) return fail(IMPALA_E_STATE, "impala_dp_init has not run on this handle");
+  if (buckets != 1 && buckets != 2) return fail(IMPALA_E_INVALID, "buckets must be 1 or 2");
+  if (int r = check_bound(h)) return r;
+  if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
+  CK(hipSetDevice(h->device));
+  const hipStream_t st = (hipStream_t)stream;
+  const RcclApi& api = rccl();
+  float* g = h->grads;
+  const size_t n = (size_t)h->cn.total, off_fc = (size_t)h->cn.wfc;
+  if (buckets == 1) {  // the whole backward, one all-reduce on the compute stream, the update
+    if (int r = enqueue_grads(h, b, st)) return r;
+    if (ncclResult_t r = api.all_reduce(g, g, n, ncclFloat32, ncclSum, h->dp_comm, st))
+      return rccl_fail("ncclAllReduce", r);
+    return enqueue_update(h, st);
+  }
+  // two buckets: part 2 (forward, heads step, FC gradients) leaves grads[off_fc ..] final; its
+  // all-reduce runs on dp_stream while part 6 (the per-frame backward, the conv weight
+  // gradients) runs on `st`; then grads[.. off_fc] follow on dp_stream and `st` waits for both
+  if (int r = enqueue_grads(h, b, st, 2)) return r;
+  CK(hipEventRecord(h->dp_ev[0], st));
+  CK(hipStreamWaitEvent(h->dp_stream, h->dp_ev[0], 0));
+  if (ncclResult_t r = api.all_reduce(g + off_fc, g + off_fc, n - off_fc, ncclFloat32, ncclSum,
+                                      h->dp_comm, h->dp_stream))
+    return rccl_fail("ncclAllReduce (FC + heads bucket)", r);
+  if (int r = enqueue_grads(h, b, st, 6)) return r;
+  CK(hipEventRecord(h->dp_ev[1], st));
+  CK(hipStreamWaitEvent(h->dp_stream, h->dp_ev[1], 0));
+  if (ncclResult_t r = api.all_reduce(g, g, off_fc, ncclFloat32, ncclSum, h->dp_comm, h->dp_stream))
+    return rccl_fail("ncclAllReduce (conv + LayerNorm bucket)", r);
+  CK(hipEventRecord(h->dp_ev[2], h->dp_stream));
+  CK(hipStreamWaitEvent(st, h->dp_ev[2], 0));
+  return enqueue_update(h, st);
 }
 
 int impala_ppo_train_step(impala_learner* h, const impala_ppo_batch* pb, void* stream) {

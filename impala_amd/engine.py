@@ -77,6 +77,7 @@ class Engine:
                                       ptr(self.exp_avg_sq), ptr(self.metrics), stream_ptr(None)),
                   "impala_bind_state")
         self._version = model._version
+        self._dp = False  # dp_init ran: the handle has its own RCCL communicator
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -253,6 +254,38 @@ class Engine:
     def bucket_offset_fc(self) -> int:
         """First flat-gradient index of the FC + heads bucket (final after part 2)."""
         return int(_lib.lib().impala_grad_bucket_offset_fc(self._h))
+
+    # ------------------------------------------------------------------ native data parallel
+    def dp_init(self, group=None):
+        """Give the handle its own RCCL communicator over the replicas of ``group`` (collective:
+        every rank calls it).  Rank 0 of the group creates the 128-byte communicator id
+        (impala_dp_unique_id), torch.distributed broadcasts it, every rank runs impala_dp_init."""
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        if world != self.cfg.world_size:
+            raise ValueError(f"group has {world} ranks, the handle was created for "
+                             f"world_size {self.cfg.world_size}")
+        uid = torch.zeros(_lib.DP_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            check(_lib.lib().impala_dp_unique_id(ptr(uid)), "impala_dp_unique_id")
+        on_dev = dist.get_backend(group) == "nccl"
+        t = uid.to(self.device) if on_dev else uid
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast(t, src, group=group)
+        uid = t.cpu() if on_dev else t
+        check(_lib.lib().impala_dp_init(self._h, ptr(uid), world, rank), "impala_dp_init")
+        self._dp = True
+
+    def dp_train_step(self, *batch, buckets: int = 1, stream=None):
+        """The whole data-parallel step on the handle's communicator (impala_dp_train_step):
+        local gradients, in-place RCCL all-reduce (sum) on the compute stream -- ``buckets=2``:
+        the FC + heads bucket on the handle's side stream, overlapped with the per-frame
+        backward -- then clip + Adam on the summed gradient."""
+        b = self._batch(*batch)
+        self._sync_weights(stream)
+        check(_lib.lib().impala_dp_train_step(self._h, C.byref(b), int(buckets),
+                                              stream_ptr(stream)), "impala_dp_train_step")
+        self._updated()
 
     def apply_update(self, stream=None):
         check(_lib.lib().impala_apply_update(self._h, stream_ptr(stream)), "impala_apply_update")

@@ -79,6 +79,7 @@ class ImpalaLearner(Learner):
         self._model_push_period = model_push_period
         self._rollout_length = rollout_length
         self._pg = process_group
+        self._native_dp = None  # decided at the first data-parallel step (distributed.py)
         if world_size is None:
             world_size = 1
             if process_group is not None:
@@ -179,9 +180,17 @@ class ImpalaLearner(Learner):
         if self._world_size == 1:
             e.train_step(*batch)
         else:
-            from .distributed import compute_grads_allreduced
-            compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
-            e.apply_update()
+            from .distributed import (compute_grads_allreduced, native_dp_buckets,
+                                      native_dp_enabled)
+            if self._native_dp is None:
+                self._native_dp = native_dp_enabled(self._pg)
+                if self._native_dp:
+                    e.dp_init(self._pg)
+            if self._native_dp:
+                e.dp_train_step(*batch, buckets=native_dp_buckets())
+            else:
+                compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
+                e.apply_update()
         m = e.metrics.clone()  # device scalars; float(v) synchronises lazily
         return {name: m[i] for i, name in enumerate(_lib.METRIC_NAMES)}
 

@@ -52,6 +52,7 @@ extern "C" {
 #define IMPALA_E_INVALID 1001   /* bad argument / shape */
 #define IMPALA_E_STATE 1002     /* state not bound / wrong call order */
 #define IMPALA_E_UNSUPPORTED 1003
+#define IMPALA_E_RCCL 1004      /* RCCL missing or a collective call failed */
 
 #define IMPALA_DTYPE_F32 0      /* fp32 operands, f32 MFMA (parity mode) */
 #define IMPALA_DTYPE_BF16 1     /* bf16 operands, fp32 accumulate / master weights */
@@ -178,6 +179,24 @@ size_t impala_grad_bucket_offset(const impala_learner* h);
  * gradients) finalises [0, impala_grad_bucket_offset_fc(h)) and the metrics.  Parts 2, 6 give
  * bit-identical grads to impala_compute_grads. */
 size_t impala_grad_bucket_offset_fc(const impala_learner* h);
+
+/* Native data-parallel step (SURVEY.md §8(b) impala_create(..., rccl_comm), §8(e)): the handle
+ * owns an RCCL communicator over the world_size replicas (one process per GPU), so the whole
+ * data-parallel step -- learning.py:141-176 on the local shard, the gradient all-reduce over
+ * xGMI, clip and Adam on the summed gradient -- is enqueued by one call with no host round trip.
+ * impala_dp_unique_id: one rank creates the 128-byte communicator id (ncclGetUniqueId) and the
+ * caller hands it to every rank (torch.distributed.broadcast); impala_dp_init (collective: every
+ * rank calls it, nranks = the handle's world_size) creates the communicator.  RCCL is loaded at
+ * run time (librccl.so.1; inside torch the already-loaded copy). */
+#define IMPALA_DP_ID_BYTES 128
+int impala_dp_unique_id(void* out);
+int impala_dp_init(impala_learner* h, const void* unique_id, int nranks, int rank);
+/* buckets 1: the whole backward, then one in-place ncclAllReduce(sum) of the flat gradient on
+ * `stream`, then the update.  buckets 2: part 2 (forward, heads step, FC gradients), whose FC +
+ * heads gradient (1.07 MB) is all-reduced on the handle's side stream while part 6 (the
+ * per-frame backward, the conv weight gradients) runs on `stream`; then the conv + LayerNorm
+ * bucket; `stream` waits for both before the update.  Both give bit-identical parameters. */
+int impala_dp_train_step(impala_learner* h, const impala_batch* batch, int buckets, void* stream);
 
 /* Replay gather (agents/impala/builder.py:30-36 UniformSampler.sample + learning.py:121-123
  * collate/H2D, done in HBM): for each field f < nfields (<= 8), copy row idx[i] of src[f] to

@@ -100,6 +100,55 @@ def test_rccl_world1_bucketed_step_is_bitwise_train_step(dtype, buckets, tmp_pat
     assert res["params_equal"] and res["metrics_equal"] and res["grads_equal"], res
 
 
+NATIVE_WORKER = r"""
+import os, sys, json, numpy as np, torch
+sys.path.insert(0, os.environ["IMPALA_ROOT"])
+import torch.distributed as dist
+from oracle import ref_cpu
+from impala_amd.distributed import init_process_group, native_dp_enabled
+from impala_amd.engine import Engine
+from impala_amd.model import AtariPPOModel
+group = init_process_group("nccl")
+assert native_dp_enabled(group)
+dev = torch.device("cuda:0")
+dtype, buckets = os.environ["DTYPE"], int(os.environ["BUCKETS"])
+B = 8
+batches = [[torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+            for x in ref_cpu.synthetic_batch(B, 20, 15, seed=80 + s)] for s in range(3)]
+def make():
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype=dtype, seed=0)
+    e = Engine(m, batch_size=B, rollout_length=20)
+    m._train_engine = e
+    return m, e
+m1, e1 = make()
+m2, e2 = make()
+e2.dp_init(group)
+for b in batches:
+    e1.train_step(*b)
+    e2.dp_train_step(*b, buckets=buckets)
+torch.cuda.synchronize()
+res = {"params_equal": bool(torch.equal(m1.flat, m2.flat)),
+       "metrics_equal": bool(torch.equal(e1.metrics, e2.metrics)),
+       "grads_equal": bool(torch.equal(m1.flat_grad, m2.flat_grad)),
+       "moments_equal": bool(torch.equal(e1.exp_avg, e2.exp_avg) and
+                             torch.equal(e1.exp_avg_sq, e2.exp_avg_sq))}
+json.dump(res, open(os.path.join(os.environ["OUT"], "native.json"), "w"))
+e2.close()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("dtype,buckets", [("fp32", 1), ("fp32", 2), ("bf16", 2)])
+def test_native_rccl_world1_step_is_bitwise_train_step(dtype, buckets, tmp_path):
+    """impala_dp_init + impala_dp_train_step (the handle's own RCCL communicator, buckets on its
+    side stream) at world size 1: the in-place all-reduces are the identity, so three steps
+    must equal impala_train_step bit for bit (params, Adam moments, grads, metrics)."""
+    _dev()
+    _launch(tmp_path, NATIVE_WORKER, 1, {"DTYPE": dtype, "BUCKETS": str(buckets)})
+    res = json.load(open(tmp_path / "native.json"))
+    assert all(res.values()), res
+
+
 C3_WORKER = r"""
 import os, sys, numpy as np, torch
 sys.path.insert(0, os.environ["IMPALA_ROOT"])
