@@ -41,6 +41,16 @@ template <> struct Frag<float> {
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
     return c;
   }
+  // MFMA e (0..NE-1) of a k-step alone.  Loops that update several independent accumulators
+  // issue element e of every accumulator before element e + 1 of any: a 16x16x4 f32 MFMA issues
+  // every 32 cycles but one that reads the previous one's result waits 40, so mma()'s chain of
+  // four on one accumulator stalls 3 x 8 cycles per k-step (r03 stamps: conv phases at 82 % of
+  // the MFMA issue rate).  Every accumulator still sees the same MFMAs in the same order, so the
+  // results are bit-identical to mma().
+  static constexpr int NE = 4;
+  static DEV f32x4 mma_e(int e, const vec& a, const vec& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], c, 0, 0, 0);
+  }
   static DEV vec load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
   static DEV vec from_u8(uint32_t w) {  // 4 bytes -> 4 floats (raw 0..255)
     return vec{(float)(w & 255u), (float)((w >> 8) & 255u), (float)((w >> 16) & 255u),
@@ -61,6 +71,8 @@ template <> struct Frag<__bf16> {
   static DEV f32x4 mma(const vec& a, const vec& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
+  static constexpr int NE = 1;  // one MFMA per k-step (see Frag<float>::mma_e)
+  static DEV f32x4 mma_e(int, const vec& a, const vec& b, f32x4 c) { return mma(a, b, c); }
   static DEV vec load(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
   static DEV vec from_u8_2(uint32_t lo, uint32_t hi) {  // 8 bytes -> 8 bf16 (exact: <= 255)
     vec v;

@@ -171,8 +171,11 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
         const int k = ks * F::KSTEP + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
         const int off = ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
         const V b = *reinterpret_cast<const V*>(img + base + off);
-        acc[0] = F::mma(wa[0][ks], b, acc[0]);
-        acc[1] = F::mma(wa[1][ks], b, acc[1]);
+#pragma unroll
+        for (int e = 0; e < F::NE; ++e) {
+          acc[0] = F::mma_e(e, wa[0][ks], b, acc[0]);
+          acc[1] = F::mma_e(e, wa[1][ks], b, acc[1]);
+        }
       }
       const int pc = tile * 16 + (lane & 15);
       uint32_t bits = 0;  // ReLU mask of this pixel's 32 channels (bit oc), for the backward
@@ -387,10 +390,12 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         for (int u = 0; u < 2; ++u) bq[(ks + 1) & 1][u] = *reinterpret_cast<const V*>(img + c1base[t0 + u] + off);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        acc[u][0] = F::mma(wa1[0][ks], bq[ks & 1][u], acc[u][0]);
-        acc[u][1] = F::mma(wa1[1][ks], bq[ks & 1][u], acc[u][1]);
-      }
+      for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          acc[u][0] = F::mma_e(e, wa1[0][ks], bq[ks & 1][u], acc[u][0]);
+          acc[u][1] = F::mma_e(e, wa1[1][ks], bq[ks & 1][u], acc[u][1]);
+        }
     }
   };
   auto c1_epi = [&](const f32x4 (&acc)[2][2], int t0, int f) {
@@ -465,7 +470,9 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         if constexpr (W2REG) a = wa2[ks];
         else a = F::load(w2row + ks * KS);
 #pragma unroll
-        for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma(a, bq[ks & 1][pt], acc[pt]);
+        for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma_e(e, a, bq[ks & 1][pt], acc[pt]);
       }
       if (f + G < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
       if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
@@ -521,11 +528,13 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         for (int ks = 0; ks < K3 / KS; ++ks) {  // k = ks*32 + kl: tap = k / 64, ci = k % 64
           const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
           const V b = *reinterpret_cast<const V*>(a2f + (kh * A2W + kw) * LDA2 + (k & 63));
+          V a[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const V a = *reinterpret_cast<const V*>(w3s + (16 * i + (lane & 15)) * LDW3 + k + kl);
-            acc3[i] = F::mma(a, b, acc3[i]);
-          }
+          for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const V*>(w3s + (16 * i + (lane & 15)) * LDW3 + k + kl);
+#pragma unroll
+          for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc3[i] = F::mma_e(e, a[i], b, acc3[i]);
         }
         float* et = ets + gw * P3 * LDE;
 #pragma unroll
@@ -562,13 +571,16 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
 #pragma unroll
       for (int ks = 0; ks < NKS3; ++ks) {  // k = ks*16 + kl: tap = k / 64, ci = k % 64
         const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
+        // every frame slot runs (a slot past the run re-reads the last frame; its result is
+        // dropped), so the FMAX accumulators interleave (F::mma_e)
+        V b[FMAX];
 #pragma unroll
-        for (int fr = 0; fr < FMAX; ++fr) {
-          if (fr < nF) {
-            const V b = *reinterpret_cast<const V*>(a2f + (fr * A2F + kh * A2W + kw) * LDA2 + (k & 63));
-            acc3[fr] = F::mma(w3a[ks], b, acc3[fr]);
-          }
-        }
+        for (int fr = 0; fr < FMAX; ++fr)
+          b[fr] = *reinterpret_cast<const V*>(a2f + (min(fr, nF - 1) * A2F + kh * A2W + kw) * LDA2 + (k & 63));
+#pragma unroll
+        for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+          for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = F::mma_e(e, w3a[ks], b[fr], acc3[fr]);
       }
       float* ets = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -781,10 +793,12 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
 #pragma unroll
         for (int ks = 0; ks < NKO; ++ks)
 #pragma unroll
-          for (int rt = 0; rt < 3; ++rt)
+          for (int e = 0; e < F::NE; ++e)
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-              z[rt][cc] = F::mma(a2[rt][ks], wb[2 * hf + (cc >> 1)][ks][cc & 1], z[rt][cc]);
+            for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+              for (int cc = 0; cc < 4; ++cc)
+                z[rt][cc] = F::mma_e(e, a2[rt][ks], wb[2 * hf + (cc >> 1)][ks][cc & 1], z[rt][cc]);
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
@@ -855,9 +869,11 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     for (int s2 = 0; s2 < NKK; ++s2) {
       if (s2 + 1 < NKK) frag((s2 + 1) * KS, fa[(s2 + 1) & 1], fb[(s2 + 1) & 1]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int e = 0; e < F::NE; ++e)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
     }
   }
   // conv1 bias: the 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order
@@ -1139,9 +1155,11 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
     for (int s2 = 0; s2 < NKK; ++s2) {
       if (s2 + 1 < NKK) frag((s2 + 1) * KS, fa[(s2 + 1) & 1], fb[(s2 + 1) & 1]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int e = 0; e < F::NE; ++e)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = F::mma(fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
     }
   }
   // conv1 bias: sum each lane's partials over the 16 lanes of its channel group (fixed

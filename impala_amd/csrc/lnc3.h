@@ -184,18 +184,21 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 #pragma unroll
       for (int ko = 0; ko < NKO; ++ko)
         a[ko] = *reinterpret_cast<const V*>(d3s + (lane & 15) * LD3 + ko * KS + kl);
+      // the nine taps' accumulators side by side: MFMA e of every tap before e + 1 (F::mma_e)
+      f32x4 acc[9];
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int tap = 0; tap < 9; ++tap) acc[tap] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ko = 0; ko < NKO; ++ko) {
-          const int ks = tap * NKO + ko;
-          acc = F::mma(a[ko], wa[ks], acc);
-        }
+      for (int ko = 0; ko < NKO; ++ko)
+#pragma unroll
+        for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) acc[tap] = F::mma_e(e, a[ko], wa[tap * NKO + ko], acc[tap]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          zs[(4 * (lane >> 4) + q) * lc3::ZR + tap * OC2 + 16 * wave + (lane & 15)] = acc[q];
-      }
+          zs[(4 * (lane >> 4) + q) * lc3::ZR + tap * OC2 + 16 * wave + (lane & 15)] = acc[tap][q];
     }
     __syncthreads();
     if (active) {
