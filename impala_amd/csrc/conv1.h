@@ -777,39 +777,46 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     if (f + 1 < f1) fetch(f + 1);
     // ---- conv2 dgrad of class `wave`: Z = dY2 rows x W2 (two halves of 2 taps) ----
     {
-      V a2[3][NKO];
-#pragma unroll
-      for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-        for (int ks = 0; ks < NKO; ++ks)
-          a2[rt][ks] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + ks * KS + kl);
+      // Z^T tiles: A = the W2 fragments (rows = ci), B = the dY2 rows (cols = op), so a lane
+      // holds four consecutive channels of one op and stores them as one 16-byte write (the
+      // products and their k order are those of Z = dY2 x W2: bit-identical).  The dY2
+      // fragments are read one k-step ahead instead of all up front (register pressure: the
+      // W2 fragments must stay resident across the frame loop)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        f32x4 z[3][4];  // [row tile][tap 2 hf + (cc >> 1), ci tile cc & 1]
+        f32x4 z[3][4];  // [op tile][tap 2 hf + (cc >> 1), ci tile cc & 1]
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc) z[rt][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+        V a2[2][3];
 #pragma unroll
-        for (int ks = 0; ks < NKO; ++ks)
+        for (int rt = 0; rt < 3; ++rt)
+          a2[0][rt] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + kl);
+#pragma unroll
+        for (int ks = 0; ks < NKO; ++ks) {
+          if (ks + 1 < NKO) {
+#pragma unroll
+            for (int rt = 0; rt < 3; ++rt)
+              a2[(ks + 1) & 1][rt] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + (ks + 1) * KS + kl);
+          }
 #pragma unroll
           for (int e = 0; e < F::NE; ++e)
 #pragma unroll
             for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
               for (int cc = 0; cc < 4; ++cc)
-                z[rt][cc] = F::mma_e(e, a2[rt][ks], wb[2 * hf + (cc >> 1)][ks][cc & 1], z[rt][cc]);
+                z[rt][cc] = F::mma_e(e, wb[2 * hf + (cc >> 1)][ks][cc & 1], a2[ks & 1][rt], z[rt][cc]);
+        }
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
+        for (int rt = 0; rt < 3; ++rt) {
+          const int op = 16 * rt + (lane & 15);
+          if (op < P2) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int op = 16 * rt + kl + q;
-            if (op < P2) {
-#pragma unroll
-              for (int cc = 0; cc < 4; ++cc)
-                zw[op * LDZ + (2 * hf + (cc >> 1)) * OC1 + 16 * (cc & 1) + (lane & 15)] = z[rt][cc][q];
-            }
+            for (int cc = 0; cc < 4; ++cc)
+              *reinterpret_cast<f32x4*>(zw + op * LDZ + (2 * hf + (cc >> 1)) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
           }
+        }
       }
     }
     // the wave's own Z stores are done before its gather reads them (LDS is in order per wave;
@@ -819,61 +826,90 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     // (kh, kw) = (py + 2 j1, px + 2 j2) at dY2 cell (qy - j1, qx - j2), order j1, j2 ----
     // Branch-free: every term is loaded (an out-of-range tap reads the zero row; + 0 leaves the
     // sum of the in-range terms unchanged), so all of a lane's reads can be in flight at once.
-#pragma unroll
-    for (int qy = 0; qy < 8; ++qy) {
+    // Two-stage pipeline pinned by scheduling barriers: row qy + 1's five reads are in flight
+    // while row qy is summed, masked and stored (left alone, every row waited for its own reads
+    // behind an lgkmcnt(0)).
+    f32x4 zt[2][4];
+    uint32_t mk[2];
+    auto gload = [&](int qy, f32x4* z, uint32_t& m) {
       const int qx = slot, iy = 2 * qy + py, ix = 2 * qx + px;
       const bool pv = iy < H1 && ix < H1;
-      f32x4 zt[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int oy = qy - (t >> 1), ox = qx - (t & 1);
         const bool ok = pv && oy >= 0 && oy < H2 && ox >= 0 && ox < H2;
-        zt[t] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + t * OC1 + 4 * cg);
+        z[t] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + t * OC1 + 4 * cg);
       }
+      m = msk[pv ? iy * H1 + ix : 0];
+    };
+    gload(0, zt[0], mk[0]);
+#pragma unroll
+    for (int qy = 0; qy < 8; ++qy) {
+      if (qy + 1 < 8) gload(qy + 1, zt[(qy + 1) & 1], mk[(qy + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const int qx = slot, iy = 2 * qy + py, ix = 2 * qx + px;
+      const bool pv = iy < H1 && ix < H1;
       f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < 4; ++t) sum += zt[t];
-      const int p = pv ? iy * H1 + ix : 0;
-      const uint32_t m = pv ? msk[p] : 0u;
+      for (int t = 0; t < 4; ++t) sum += zt[qy & 1][t];
+      const uint32_t m = pv ? mk[qy & 1] : 0u;
       f32x4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         v[q] = (m >> (4 * cg + q)) & 1u ? sum[q] : 0.f;
         bsum[q] += v[q];
       }
-      if (pv) *reinterpret_cast<f32x4*>(dyt + p * LDX + 4 * cg) = v;
+      if (pv) *reinterpret_cast<f32x4*>(dyt + (iy * H1 + ix) * LDX + 4 * cg) = v;
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // dY1 complete
     // ---- conv1 weight gradient over the 240 pixel rows: A = dY1 (k = pixel), B = the s2d
     // image bytes at row(pixel, tap = wave), converted to fp32 ----
-    auto frag = [&](int kk, V* a, V* b) {
+    // The software pipeline is pinned with scheduling barriers: the LDS reads of k-step s + 1
+    // are issued ahead of the MFMAs of step s, and the bytes are converted at the top of the
+    // step that uses them.  Left alone, the scheduler (at this kernel's register pressure) sinks
+    // every read down to its use behind an lgkmcnt(0): 6 MFMAs per LDS round trip, the loop at
+    // 75 % of the MFMA issue rate (r03 stamps).
+    auto load_a = [&](int kk, V* a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
+    };
+    auto load_b = [&](int kk, uint32_t* raw) {
       const int g = lane >> 4, col = lane & 15;
-      int rr[4];
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        rr[jj] = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDIB + tapoff + col;
+      for (int jj = 0; jj < 4; ++jj) {
+        const int rr = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDIB + tapoff + col;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        V v;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) v[jj] = (float)img[rr[jj] + 16 * j];
-        b[j] = v;
+        for (int j = 0; j < 3; ++j) raw[4 * j + jj] = img[rr + 16 * j];
       }
     };
     constexpr int NKK = L::NROW / KS;
-    V fa[2][2], fb[2][3];
-    frag(0, fa[0], fb[0]);
+    V fa[2][2];
+    uint32_t raw[2][12];
+    load_a(0, fa[0]);
+    load_b(0, raw[0]);
 #pragma unroll
     for (int s2 = 0; s2 < NKK; ++s2) {
-      if (s2 + 1 < NKK) frag((s2 + 1) * KS, fa[(s2 + 1) & 1], fb[(s2 + 1) & 1]);
+      // step s + 1's dY1 reads, then this step's bytes converted (their wait covers only the
+      // reads issued before those four), then step s + 1's byte reads, then the MFMAs: at most
+      // 12 LDS reads newer than any operand an MFMA waits for (lgkmcnt counts to 15)
+      if (s2 + 1 < NKK) load_a((s2 + 1) * KS, fa[(s2 + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      V fb[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        fb[j] = V{(float)raw[s2 & 1][4 * j], (float)raw[s2 & 1][4 * j + 1],
+                  (float)raw[s2 & 1][4 * j + 2], (float)raw[s2 & 1][4 * j + 3]};
+      __builtin_amdgcn_sched_barrier(0);
+      if (s2 + 1 < NKK) load_b((s2 + 1) * KS, raw[(s2 + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int e = 0; e < F::NE; ++e)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);
+          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // conv1 bias: the 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order

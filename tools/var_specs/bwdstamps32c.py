@@ -27,8 +27,8 @@ VARIANTS = {
         (C, '    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");\n    // ---- col2im of class',
             '    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");\n    ' + S("25 + 5 * (f - f0)") + '\n    // ---- col2im of class'),
         (C, "    __syncthreads();  // dY1 complete\n", "    " + S("26 + 5 * (f - f0)") + "\n    __syncthreads();  // dY1 complete\n"),
-        (C, "          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);\n    }\n  }\n  // conv1 bias",
-            "          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[s2 & 1][j], acc[i][j]);\n    }\n    " + S("27 + 5 * (f - f0)") + "\n  }\n  // conv1 bias"),
+        (C, "          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);\n      __builtin_amdgcn_sched_barrier(0);\n    }\n  }\n  // conv1 bias",
+            "          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);\n      __builtin_amdgcn_sched_barrier(0);\n    }\n    " + S("27 + 5 * (f - f0)") + "\n  }\n  // conv1 bias"),
         (C, "        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n    }\n}",
             "        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n    }\n  " + S(50) + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("B32"); for (int q = 1; q < 51; ++q) if (q < 22 || (q >= 22 && q < 48) || q == 50) printf(" %lld", g_st32[q] ? g_st32[q] - g_st32[0] : -1); printf("\\n"); }\n}'),
     ],
