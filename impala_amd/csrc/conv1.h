@@ -459,8 +459,19 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       V bq[2][3];
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt) bq[0][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + c2_off(0));
+      // fp32: the W2 fragments stream from L2 in a ring PD2 k-steps ahead of their MFMAs (the
+      // order pinned by scheduling barriers; the compiler kept them one step ahead)
+      constexpr int PD2 = W2REG ? 1 : 4;
+      V ar[PD2];
+      if constexpr (!W2REG) {
+#pragma unroll
+        for (int d = 0; d < PD2 - 1; ++d) ar[d] = F::load(w2row + d * KS);
+      }
 #pragma unroll
       for (int ks = 0; ks < NKS2; ++ks) {
+        if constexpr (!W2REG) {
+          if (ks + PD2 - 1 < NKS2) ar[(ks + PD2 - 1) % PD2] = F::load(w2row + (ks + PD2 - 1) * KS);
+        }
         if (ks + 1 < NKS2) {
           const int off = c2_off(ks + 1);
 #pragma unroll
@@ -468,11 +479,13 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         }
         V a;
         if constexpr (W2REG) a = wa2[ks];
-        else a = F::load(w2row + ks * KS);
+        else a = ar[ks % PD2];
+        if constexpr (!W2REG) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int e = 0; e < F::NE; ++e)
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma_e(e, a, bq[ks & 1][pt], acc[pt]);
+        if constexpr (!W2REG) __builtin_amdgcn_sched_barrier(0);
       }
       if (f + G < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
       if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
@@ -557,10 +570,15 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       // bit-identical to the separate conv3 launch. ----
       constexpr int FMAX = c3t_fmax<T>(), NKS3 = K3 / KS, LDE = OC3 + 4;
       static_assert(FMAX * P3 * LDE <= G * GSZ, "fp32 conv3 tail LDS");
+      // The 36 fragment loads are issued PD3 k-steps ahead of the MFMAs that use them, inside
+      // the k-loop: issued all at once, the burst of every CU's 147 KB of W3 stalls the load
+      // issue itself (per-CU load bandwidth, ~17 B/clk) for ~7k cycles before the first MFMA
+      // (r03 stamps)
+      constexpr int PD3 = 8;
       V w3a[NKS3];
+      const T* w3row = c3.w3 + (size_t)(16 * wave + (lane & 15)) * K3 + kl;
 #pragma unroll
-      for (int ks = 0; ks < NKS3; ++ks)
-        w3a[ks] = F::load(c3.w3 + (size_t)(16 * wave + (lane & 15)) * K3 + ks * KS + kl);
+      for (int ks = 0; ks < PD3; ++ks) w3a[ks] = F::load(w3row + ks * KS);
       const int nF = f1 - f0;
       const LnLane lk = ln_lane_consts(lane, c3.b3, c3.gam, c3.bet);
       const int p = lane & 15, oy = p >> 2, ox = p & 3;
@@ -568,19 +586,27 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       f32x4 acc3[FMAX];
 #pragma unroll
       for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < NKS3; ++ks) {  // k = ks*16 + kl: tap = k / 64, ci = k % 64
+      // every frame slot runs (a slot past the run re-reads the last frame; its result is
+      // dropped), so the FMAX accumulators interleave (F::mma_e); the act2 window reads run one
+      // k-step ahead (k = ks*16 + kl: tap = k / 64, ci = k % 64)
+      auto bload = [&](int ks, V* b) {
         const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
-        // every frame slot runs (a slot past the run re-reads the last frame; its result is
-        // dropped), so the FMAX accumulators interleave (F::mma_e)
-        V b[FMAX];
 #pragma unroll
         for (int fr = 0; fr < FMAX; ++fr)
           b[fr] = *reinterpret_cast<const V*>(a2f + (min(fr, nF - 1) * A2F + kh * A2W + kw) * LDA2 + (k & 63));
+      };
+      V b[2][FMAX];
+      bload(0, b[0]);
+#pragma unroll
+      for (int ks = 0; ks < NKS3; ++ks) {
+        if (ks + PD3 < NKS3) w3a[ks + PD3] = F::load(w3row + (ks + PD3) * KS);
+        if (ks + 1 < NKS3) bload(ks + 1, b[(ks + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int e = 0; e < F::NE; ++e)
 #pragma unroll
-          for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = F::mma_e(e, w3a[ks], b[fr], acc3[fr]);
+          for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = F::mma_e(e, w3a[ks], b[ks & 1][fr], acc3[fr]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       float* ets = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -890,25 +916,37 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     load_b(0, raw[0]);
 #pragma unroll
     for (int s2 = 0; s2 < NKK; ++s2) {
-      // step s + 1's dY1 reads, then this step's bytes converted (their wait covers only the
-      // reads issued before those four), then step s + 1's byte reads, then the MFMAs: at most
-      // 12 LDS reads newer than any operand an MFMA waits for (lgkmcnt counts to 15)
-      if (s2 + 1 < NKK) load_a((s2 + 1) * KS, fa[(s2 + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
+      // One scheduling region per k-step, its order pinned with group barriers: the j = 0
+      // bytes converted first, the j = 1, 2 conversions in the gaps of the first eight MFMAs
+      // (j = 0), step s + 1's sixteen LDS reads in the gaps of the next sixteen (j = 1, 2), so
+      // the MFMA pipe never drains between k-steps (32-cycle issue: room for one other
+      // instruction per gap).  MFMA order (j, e, i): acc[i][j] still sees e = 0..3 in turn.
       V fb[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         fb[j] = V{(float)raw[s2 & 1][4 * j], (float)raw[s2 & 1][4 * j + 1],
                   (float)raw[s2 & 1][4 * j + 2], (float)raw[s2 & 1][4 * j + 3]};
-      __builtin_amdgcn_sched_barrier(0);
-      if (s2 + 1 < NKK) load_b((s2 + 1) * KS, raw[(s2 + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
+      if (s2 + 1 < NKK) {
+        load_a((s2 + 1) * KS, fa[(s2 + 1) & 1]);
+        load_b((s2 + 1) * KS, raw[(s2 + 1) & 1]);
+      }
 #pragma unroll
-      for (int e = 0; e < F::NE; ++e)
+      for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int e = 0; e < F::NE; ++e)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
+          for (int i = 0; i < 2; ++i) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU: the j = 0 conversions
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   }

@@ -184,7 +184,10 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 #pragma unroll
       for (int ko = 0; ko < NKO; ++ko)
         a[ko] = *reinterpret_cast<const V*>(d3s + (lane & 15) * LD3 + ko * KS + kl);
-      // the nine taps' accumulators side by side: MFMA e of every tap before e + 1 (F::mma_e)
+      // the nine taps' accumulators side by side: MFMA e of every tap before e + 1 (F::mma_e).
+      // Z^T tiles (A = the W3 fragments, rows = ci; B = the dact3 rows, cols = p): a lane holds
+      // four consecutive channels of one pixel and stores them with one 16-byte write (the
+      // products and their k order are those of Z = dact3 x W3)
       f32x4 acc[9];
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) acc[tap] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -193,12 +196,10 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
 #pragma unroll
         for (int e = 0; e < F::NE; ++e)
 #pragma unroll
-          for (int tap = 0; tap < 9; ++tap) acc[tap] = F::mma_e(e, a[ko], wa[tap * NKO + ko], acc[tap]);
+          for (int tap = 0; tap < 9; ++tap) acc[tap] = F::mma_e(e, wa[tap * NKO + ko], a[ko], acc[tap]);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          zs[(4 * (lane >> 4) + q) * lc3::ZR + tap * OC2 + 16 * wave + (lane & 15)] = acc[tap][q];
+        *reinterpret_cast<f32x4*>(zs + (lane & 15) * lc3::ZR + tap * OC2 + 16 * wave + 4 * (lane >> 4)) = acc[tap];
     }
     __syncthreads();
     if (active) {

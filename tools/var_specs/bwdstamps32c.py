@@ -4,9 +4,16 @@
 L = "lnc3.h"
 C = "conv1.h"
 def S(i):
-    return f"if (blockIdx.x == 0 && threadIdx.x == 0) g_st32[{i}] = __builtin_amdgcn_s_memtime(); "
+    return (f"__builtin_amdgcn_sched_barrier(0); if (blockIdx.x == 0 && threadIdx.x == 0) g_st32[{i}] = "
+            "__builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); ")
 VARIANTS = {
     "b32st": [
+        (L, "  // ---- gamma / beta partials: fixed-order combine of the groups -> slab [2][1024] ----",
+            "  " + S(56) + "\n  // ---- gamma / beta partials: fixed-order combine of the groups -> slab [2][1024] ----"),
+        (C, "  if (f0 < f1) fetch(f0);  // the first frame is in flight during the prologue",
+            "  " + S(57) + "\n  if (f0 < f1) fetch(f0);  // the first frame is in flight during the prologue"),
+        (C, "  // zero the dY1 rows no pixel writes (225..239), the dY2 pad rows (36..47) and each Z tile's",
+            "  " + S(58) + "\n  // zero the dY1 rows no pixel writes (225..239), the dY2 pad rows (36..47) and each Z tile's"),
         (C, "namespace c1 {\nconstexpr int GRID", "__device__ long long g_st32[64];\nnamespace c1 {\nconstexpr int GRID"),
         (L, "  lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);\n  __syncthreads();  // this workgroup's dact2",
             "  " + S(0) + "\n  lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);\n  " + S(21) + "\n  __syncthreads();  // this workgroup's dact2"),
@@ -26,10 +33,10 @@ VARIANTS = {
             "    " + S("23 + 5 * (f - f0)") + "\n    if (tid < c1::NPIX) msk[tid] = nmk;\n    __syncthreads();\n    " + S("24 + 5 * (f - f0)") + "\n    if (f + 1 < f1) fetch(f + 1);"),
         (C, '    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");\n    // ---- col2im of class',
             '    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");\n    ' + S("25 + 5 * (f - f0)") + '\n    // ---- col2im of class'),
-        (C, "    __syncthreads();  // dY1 complete\n", "    " + S("26 + 5 * (f - f0)") + "\n    __syncthreads();  // dY1 complete\n"),
-        (C, "          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);\n      __builtin_amdgcn_sched_barrier(0);\n    }\n  }\n  // conv1 bias",
-            "          for (int j = 0; j < 3; ++j) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);\n      __builtin_amdgcn_sched_barrier(0);\n    }\n    " + S("27 + 5 * (f - f0)") + "\n  }\n  // conv1 bias"),
+        (C, "    __syncthreads();  // dY1 complete\n", "    " + S("26 + 5 * (f - f0)") + "\n    __syncthreads();  // dY1 complete\n    " + S("51 + (f - f0)") + "\n"),
+        (C, "      __builtin_amdgcn_sched_barrier(0);\n    }\n  }\n  // conv1 bias",
+            "      __builtin_amdgcn_sched_barrier(0);\n    }\n    " + S("27 + 5 * (f - f0)") + "\n  }\n  // conv1 bias"),
         (C, "        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n    }\n}",
-            "        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n    }\n  " + S(50) + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("B32"); for (int q = 1; q < 51; ++q) if (q < 22 || (q >= 22 && q < 48) || q == 50) printf(" %lld", g_st32[q] ? g_st32[q] - g_st32[0] : -1); printf("\\n"); }\n}'),
+            "        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n    }\n  " + S(50) + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("B32"); for (int q = 1; q < 59; ++q) if (q < 48 || q >= 50) printf(" %lld", g_st32[q] ? g_st32[q] - g_st32[0] : -1); printf("\\n"); }\n}'),
     ],
 }

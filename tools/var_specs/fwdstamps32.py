@@ -3,14 +3,16 @@
 # (W3 loads, MFMAs, LN epilogue).  Printed once per launch ("F32F" lines; tools/run_stamps.sh).
 F = "conv1.h"
 def S(i):
-    return f"if (blockIdx.x == 0 && threadIdx.x == 0) stl[{i}] = __builtin_amdgcn_s_memtime(); "
+    return (f"__builtin_amdgcn_sched_barrier(0); if (blockIdx.x == 0 && threadIdx.x == 0) stl[{i}] = "
+            "__builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); ")
 VARIANTS = {
     "f32fst": [
         (F, "  const int kl = KPL * (lane >> 4);\n  uint4 nv[3];",
-            "  const int kl = KPL * (lane >> 4);\n  __shared__ long long stl[40];\n  " + S(0) + "\n  uint4 nv[3];"),
+            "  const int kl = KPL * (lane >> 4);\n  __shared__ long long stl[64];\n  " + S(0) + "\n  uint4 nv[3];"),
         (F, "  const int n_it = (f1 - f0 + G - 1) / G;\n  // conv1 pixel tiles",
             "  " + S(1) + "\n  const int n_it = (f1 - f0 + G - 1) / G;\n  // conv1 pixel tiles"),
-        (F, "      c1_mma(accA, 0);\n", "      " + S("2 + 5 * it") + "\n      c1_mma(accA, 0);\n"),
+        (F, "      c1_mma(accA, 0);\n      c1_mma(accB, 2);\n      c1_epi(accA, 0, f);\n      c1_epi(accB, 2, f);\n",
+            "      " + S("2 + 5 * it") + "\n      c1_mma(accA, 0);\n      " + S("40 + 4 * it") + "\n      c1_mma(accB, 2);\n      " + S("41 + 4 * it") + "\n      c1_epi(accA, 0, f);\n      " + S("42 + 4 * it") + "\n      c1_epi(accB, 2, f);\n"),
         (F, "    __syncthreads();  // the act1 tile is complete; the image is free",
             "    " + S("3 + 5 * it") + "\n    __syncthreads();  // the act1 tile is complete; the image is free\n    " + S("4 + 5 * it")),
         (F, "      if (f + G < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);",
@@ -21,6 +23,6 @@ VARIANTS = {
         (F, "      float* ets = reinterpret_cast<float*>(smem);\n#pragma unroll\n      for (int fr = 0; fr < FMAX; ++fr)\n        if (fr < nF)",
             "      " + S(31) + "\n      float* ets = reinterpret_cast<float*>(smem);\n#pragma unroll\n      for (int fr = 0; fr < FMAX; ++fr)\n        if (fr < nF)"),
         (F, "      for (int fr = wave; fr < nF; fr += 4)\n        ln_frame_epilogue<T>(ets + fr * P3 * LDE, LDE, f0 + fr, lane, lk, c3.act3, c3.y, c3.stats);\n    }",
-            "      " + S(32) + "\n      for (int fr = wave; fr < nF; fr += 4)\n        ln_frame_epilogue<T>(ets + fr * P3 * LDE, LDE, f0 + fr, lane, lk, c3.act3, c3.y, c3.stats);\n      " + S(33) + '\n      if (blockIdx.x == 0 && threadIdx.x == 0) { printf("F32F"); for (int q = 1; q < 34; ++q) if (q < 27 || q >= 30) printf(" %lld", stl[q] - stl[0]); printf("\\n"); }\n    }'),
+            "      " + S(32) + "\n      for (int fr = wave; fr < nF; fr += 4)\n        ln_frame_epilogue<T>(ets + fr * P3 * LDE, LDE, f0 + fr, lane, lk, c3.act3, c3.y, c3.stats);\n      " + S(33) + '\n      if (blockIdx.x == 0 && threadIdx.x == 0) { printf("F32F"); for (int q = 1; q < 60; ++q) if (q < 27 || (q >= 30 && q < 34) || q >= 40) printf(" %lld", stl[q] - stl[0]); printf("\\n"); }\n    }'),
     ],
 }
