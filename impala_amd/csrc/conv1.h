@@ -805,43 +805,64 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     {
       // Z^T tiles: A = the W2 fragments (rows = ci), B = the dY2 rows (cols = op), so a lane
       // holds four consecutive channels of one op and stores them as one 16-byte write (the
-      // products and their k order are those of Z = dY2 x W2: bit-identical).  The dY2
-      // fragments are read one k-step ahead instead of all up front (register pressure: the
-      // W2 fragments must stay resident across the frame loop)
+      // products and their k order are those of Z = dY2 x W2).  The dY2 fragments are read one
+      // k-step ahead instead of all up front (register pressure: the W2 fragments must stay
+      // resident across the frame loop).
+      // ops 0..31 are two 16-wide MFMA tiles; the last 4 (32..35) would fill a third tile 25 %
+      // (64 of the 192 MFMAs per half).  They run on v_mfma_f32_4x4x1_16b_f32 instead: block b
+      // = 4 g + og (lane 16 g + 4 og + j) takes rows 4 og .. 4 og + 3 (ci) of the same W2
+      // fragment element e and k-phase g = lane >> 4, op 32 + j: one 4x4x1 per (k-step, e, ci
+      // tile) instead of four 16x16x4 (tools/probe/mfma4x4.hip: lane map and 9.2 cycles each).
+      // The four k-phases g are summed at the end (butterfly over lanes ^16, ^32, fixed order).
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        f32x4 z[3][4];  // [op tile][tap 2 hf + (cc >> 1), ci tile cc & 1]
+        f32x4 z[2][4];  // [op tile][tap 2 hf + (cc >> 1), ci tile cc & 1]
+        f32x4 z4[4];    // ops 32..35 (4x4x1 blocks), per cc
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
+        for (int cc = 0; cc < 4; ++cc) {
+          z[0][cc] = z[1][cc] = z4[cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        V a2[2][3];  // [ring][op tile 0, 1; 2 = ops 32 + (lane & 3) for the 4x4x1 blocks]
+        auto a2load = [&](int ks, V* a) {
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) z[rt][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
-        V a2[2][3];
-#pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
-          a2[0][rt] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + kl);
+          for (int rt = 0; rt < 2; ++rt)
+            a[rt] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + ks * KS + kl);
+          a[2] = *reinterpret_cast<const V*>(d2s + (32 + (lane & 3)) * LDD + ks * KS + kl);
+        };
+        a2load(0, a2[0]);
 #pragma unroll
         for (int ks = 0; ks < NKO; ++ks) {
-          if (ks + 1 < NKO) {
+          if (ks + 1 < NKO) a2load(ks + 1, a2[(ks + 1) & 1]);
 #pragma unroll
-            for (int rt = 0; rt < 3; ++rt)
-              a2[(ks + 1) & 1][rt] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + (ks + 1) * KS + kl);
-          }
+          for (int e = 0; e < F::NE; ++e) {
 #pragma unroll
-          for (int e = 0; e < F::NE; ++e)
-#pragma unroll
-            for (int rt = 0; rt < 3; ++rt)
+            for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
               for (int cc = 0; cc < 4; ++cc)
                 z[rt][cc] = F::mma_e(e, wb[2 * hf + (cc >> 1)][ks][cc & 1], a2[ks & 1][rt], z[rt][cc]);
-        }
-#pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
-          const int op = 16 * rt + (lane & 15);
-          if (op < P2) {
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc)
-              *reinterpret_cast<f32x4*>(zw + op * LDZ + (2 * hf + (cc >> 1)) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
+              z4[cc] = __builtin_amdgcn_mfma_f32_4x4x1f32(wb[2 * hf + (cc >> 1)][ks][cc & 1][e],
+                                                         a2[ks & 1][2][e], z4[cc], 0, 0, 0);
           }
+        }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const int op = 16 * rt + (lane & 15);
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+            *reinterpret_cast<f32x4*>(zw + op * LDZ + (2 * hf + (cc >> 1)) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
+        }
+        // 4x4x1 blocks: lane 16 g + 4 og + j holds Z[ci 4 og + i (reg i)][op 32 + j] over the
+        // k-phase g; the g-sum ((g0 + g1) + (g2 + g3)) lands on every lane, lanes 0..15 store
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          f32x4 t;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t[q] = xor32_sum(xor16_sum(z4[cc][q]));
+          if (lane < 16)
+            *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ + (2 * hf + (cc >> 1)) * OC1 +
+                                      16 * (cc & 1) + 4 * (lane >> 2)) = t;
         }
       }
     }
