@@ -358,10 +358,13 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
     return ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
   };
   // conv2: 3 pixel tiles (3 accumulators), B fragments one k-step ahead
+  // fp32: pixel tile 2 holds only pixels 32..35; they run on 4x4x1 blocks (see the conv2 loop),
+  // whose B operand is pixel 32 + (lane & 3) at k-phase lane >> 4
   int c2row[3];
 #pragma unroll
   for (int pt = 0; pt < 3; ++pt) {
-    const int px = min(pt * 16 + (lane & 15), P2 - 1), oy = px / H2, ox = px - oy * H2;
+    const int px = (pt == 2 && !W2REG) ? 32 + (lane & 3) : min(pt * 16 + (lane & 15), P2 - 1);
+    const int oy = px / H2, ox = px - oy * H2;
     c2row[pt] = ((ST2 * oy) * A1P + ST2 * ox) * LDA1 + kl;
   }
   auto c2_off = [&](int ks) {
@@ -482,15 +485,43 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         else a = ar[ks % PD2];
         if constexpr (!W2REG) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int e = 0; e < F::NE; ++e)
+        for (int e = 0; e < F::NE; ++e) {
+          if constexpr (W2REG) {
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma_e(e, a, bq[ks & 1][pt], acc[pt]);
+            for (int pt = 0; pt < 3; ++pt) acc[pt] = F::mma_e(e, a, bq[ks & 1][pt], acc[pt]);
+          } else {
+            // pixels 0..31: two 16x16x4 tiles; 32..35: one v_mfma_f32_4x4x1_16b_f32 (block
+            // 4 g + og = oc rows 4 og .. 4 og + 3 of the same W2 element, k-phase g, pixel
+            // 32 + j) instead of a quarter-full third tile
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) acc[pt] = F::mma_e(e, a, bq[ks & 1][pt], acc[pt]);
+            acc[2] = __builtin_amdgcn_mfma_f32_4x4x1f32(a[e], bq[ks & 1][2][e], acc[2], 0, 0, 0);
+          }
+        }
         if constexpr (!W2REG) __builtin_amdgcn_sched_barrier(0);
       }
       if (f + G < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
       if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
+      if constexpr (!W2REG) {
+        // the 4x4x1 blocks: lane 16 g + 4 og + j holds act2[pixel 32 + j][oc 16 w + 4 og + reg]
+        // over k-phase g; ((g0 + g1) + (g2 + g3)) on every lane, lanes 0..15 store
+        const int pc = 32 + (lane & 3), oc0 = 16 * wave + 4 * ((lane >> 2) & 3);
+        f32x4 t;
 #pragma unroll
-      for (int pt = 0; pt < 3; ++pt) {
+        for (int q = 0; q < 4; ++q) t[q] = xor32_sum(xor16_sum(acc[2][q]));
+        if (lane < 16) {
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(t[q] + b2[oc0 + q], 0.f);
+          store4(act2 + ((size_t)f * P2 + pc) * OC2 + oc0, v);
+          if (tail) {
+            const int cy = pc / H2, cx = pc - cy * H2;
+            store4(a2s + ((f - f0) * A2F + cy * A2W + cx) * LDA2 + oc0, v);
+          }
+        }
+      }
+#pragma unroll
+      for (int pt = 0; pt < (W2REG ? 3 : 2); ++pt) {
         const int pc = pt * 16 + (lane & 15);
         if (pc < P2) {
           float v[4];

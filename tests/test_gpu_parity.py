@@ -327,7 +327,12 @@ def test_launch_modes_agree_fp32(env, monkeypatch):
     """The fp32 headline path (the reference's arithmetic): every fused / merged launch --
     the conv3 + LayerNorm tail of the forward, the fused per-frame backward, the merged FC and
     conv weight-gradient launches -- is bit-identical to the separate kernels it replaces, at
-    C2's frame run (B=64, T=20: 5 frames per workgroup, the fp32 tail's limit)."""
+    C2's frame run (B=64, T=20: 5 frames per workgroup, the fp32 tail's limit).
+    One exception: the fused forward computes conv2's last 4 output pixels on 4x4x1 MFMA blocks
+    whose four k-phases are summed at the end, the unfused gemm_tile conv2 in one k-ordered
+    chain, so IMPALA_FWD_FUSED=0 agrees to fp32 rounding: after two Adam steps every parameter
+    within one lr step (1e-4; Adam's normalised update turns rounding in a near-zero gradient
+    into an O(lr) move) and all but 0.1 % within 1e-7; metrics within 1e-5 relative."""
     dev = _dev()
     batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(64, 20, 15, seed=16)]
 
@@ -343,9 +348,17 @@ def test_launch_modes_agree_fp32(env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     alt = run()
+    assert np.isfinite(base[1]).all()
+    if env.get("IMPALA_FWD_FUSED") == "0":
+        d = np.abs(base[0] - alt[0])
+        print(f"fp32 fused vs unfused forward after 2 steps: max |dp| {d.max():.2e}, "
+              f"frac > 1e-7 {np.mean(d > 1e-7):.2e}")
+        assert d.max() <= 1e-4
+        assert np.mean(d > 1e-7) < 1e-3
+        np.testing.assert_allclose(base[1], alt[1], rtol=1e-5, atol=1e-7)
+        return
     np.testing.assert_array_equal(base[0], alt[0])
     np.testing.assert_array_equal(base[1], alt[1])
-    assert np.isfinite(base[1]).all()
 
 
 @pytest.mark.parametrize("B,T", [(24, 64), (160, 20)])

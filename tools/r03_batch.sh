@@ -1,3 +1,4 @@
 #!/bin/bash
 set -o pipefail
-bash tools/quick32.sh && bash tools/run_stamps.sh
+bash tools/quick32.sh
+grep -h "fused vs unfused" gpurun_out/quick32/tests.log || true
