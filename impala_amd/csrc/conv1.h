@@ -954,12 +954,13 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     };
     auto load_b = [&](int kk, uint32_t* raw) {
       const int g = lane >> 4, col = lane & 15;
+      int rr[4];
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int rr = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDIB + tapoff + col;
+      for (int jj = 0; jj < 4; ++jj) rr[jj] = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDIB + tapoff + col;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) raw[4 * j + jj] = img[rr + 16 * j];
-      }
+      for (int j = 0; j < 3; ++j)  // j-major: the next step's first-needed bytes are read first
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) raw[4 * j + jj] = img[rr[jj] + 16 * j];
     };
     constexpr int NKK = L::NROW / KS;
     V fa[2][2];
@@ -988,14 +989,17 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
         for (int e = 0; e < F::NE; ++e)
 #pragma unroll
           for (int i = 0; i < 2; ++i) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
+      // the next step's reads go out in the first sixteen gaps (dY1 fragments, then the bytes
+      // j-major) so the j = 0 bytes have most of a step to land before they are converted
       __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU: the j = 0 conversions
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU: j = 1, 2 conversions
       }
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
+      for (int g = 0; g < 8; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
       }
