@@ -703,19 +703,22 @@ constexpr int NCELL = QG * QG;
 
 // G 4-wave groups per workgroup take alternating frames of the run (G frames in flight per CU
 // on top of the one-frame register prefetch); their partials are summed in a fixed order.
-template <typename T> constexpr int c12_groups() { return sizeof(T) == 2 ? 2 : 1; }
+// (fp32: two 4-wave groups with different roles, see conv12_bwd_body_f32)
+template <typename T> constexpr int c12_groups() { return 2; }
 
-// fp32 body (conv12_bwd_body_f32) LDS, in 4-byte words: the frame's s2d image as BYTES (the
-// raw 0..255 values, converted when read; 48-byte rows), dY1 in pixel rows (240: the conv1
-// weight gradient's 15 k-steps of 16), dY2 as the scatter GEMM's A rows (48: 3 row tiles), one
-// Z tile per wave (its stride-parity class; row 36 stays zero: the gather's out-of-range taps
-// read it), then the mask words
+// fp32 body (conv12_bwd_body_f32) LDS, in 4-byte words, double-buffered per frame where the
+// two groups overlap: the frame's s2d image as BYTES (the raw 0..255 values, converted when
+// read) in [Y][channel][X] rows of XP bytes (4 consecutive X in one 32-bit word) x 2, dY1 in
+// pixel rows iy * 16 + ix (240: the conv1 weight gradient's 15 k-steps = the 15 pixel rows,
+// ix = 15 a zero pad) x 2, dY2 rows (36) x 2, one half-Z tile per stride-parity class (2 taps x 32 channels; row 36
+// stays zero: the gather's out-of-range taps read it), the mask words x 2
 struct C12B32 {
-  static constexpr int LDIB = c1::CH, LDX = c1::LB<float>::LDX;  // image row bytes, dY1 row
-  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = 48, LDZ = 4 * OC1 + 4, ZROWS = P2 + 1;
-  static constexpr int IMG = 0, DYT = IMG + c1::GRID * c1::GRID * LDIB / 4, D2S = DYT + NROW * LDX;
-  static constexpr int Z0 = D2S + DROWS * LDD, ZSZ = ZROWS * LDZ, MSK = Z0 + 4 * ZSZ;
-  static constexpr int BYTES = (MSK + c1::NPIX) * 4;
+  static constexpr int XP = 20, LDX = c1::LB<float>::LDX;  // image row bytes (X 0..16), dY1 row
+  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = P2, LDZ = 2 * OC1 + 4, ZROWS = P2 + 1;
+  static constexpr int IMGW = c1::GRID * c1::CH * XP / 4, DYW = NROW * LDX, D2W = DROWS * LDD;
+  static constexpr int IMG = 0, DYT = IMG + 2 * IMGW, D2S = DYT + 2 * DYW;
+  static constexpr int Z0 = D2S + 2 * D2W, ZSZ = ZROWS * LDZ, MSK = Z0 + 4 * ZSZ;
+  static constexpr int BYTES = (MSK + 2 * c1::NPIX) * 4;
 };
 
 // LDS of the body (bytes): per-group image / dY1 / dY2 tiles, the ReLU mask words, bias sums
@@ -734,17 +737,24 @@ template <typename T> struct C12BLds {
 //
 //   Z[op][t][ci] = sum_oc dY2[op][oc] W2[oc][t][ci]        (36 conv2 output pixels op)
 //   dY1[iy][ix][ci] = [act1 > 0] * sum_{t = (kh, kw): iy = 2 oy + kh, ix = 2 ox + kw} Z[op][t][ci]
+//   dW1'[oc][k'] += sum_p dY1[p][oc] * s2d[row(p, tap)][ch]     (1/255 at the end)
 //
 // The 16 taps fall into the four stride-parity classes (kh % 2, kw % 2) and a class's 4 taps
-// reach exactly the input pixels of that parity, so wave w owns class w: it computes Z for its
-// 4 taps (rows op: 3 tiles of 16, cols (tap, ci): 8 tiles, K = 64 oc; its W2 fragments in
-// registers, the dY2 rows as the A operand) into its own LDS tile, then gathers <= 4 Z terms
-// per (pixel, 4 channels) of its class in a fixed tap order, masks them and writes dY1 -- no
-// workgroup barrier between the GEMM and the gather.  384 MFMAs per wave per frame against the
-// gather form's 512 (whose K runs over zero-padded dY2 cells: 56 % useful); the conv1 weight
-// gradient then reduces over 240 pixel rows (225 real) instead of 256.  The image is kept as
-// bytes (12 KB instead of 53 KB of floats) and converted per fragment element, which is what
-// leaves room for the four Z tiles.  fp32 sums: oc in MFMA order, then taps in a fixed order.
+// reach exactly the input pixels of that parity.  512 threads in two 4-wave groups with
+// different roles, software-pipelined over the workgroup's frames (one barrier per step):
+//   group A (waves 0..3), frame i:   wave w owns class w: Z for its 4 taps in two halves of 2
+//       taps (rows op: 2 tiles of 16 + the last 4 on 4x4x1 blocks, cols (tap, ci), K = 64 oc;
+//       its W2 fragments in registers), each half gathered into dY1[i & 1] in a fixed tap
+//       order (the second half adds to the first half's partial sums, masks and keeps the
+//       conv1 bias partials); then it stages frame i + 1's dY2 / mask (and frame i + 2's loads);
+//   group B (waves 4..7), frame i - 1: the conv1 weight gradient, wave w owns tap w (48
+//       channels = 3 column tiles) for both 16-row oc tiles, over dY1[(i - 1) & 1] and the
+//       image bytes of frame i - 1.
+// With one wave of each group per SIMD, the gather / staging work of one group runs under the
+// other group's MFMAs (the one-group body ran every phase behind a workgroup barrier with one
+// wave per SIMD).  Every value is the same fp32 sum in the same order as that body: the tap
+// sums ((z0 + z1) + z2) + z3, oc in MFMA order, pixels in k-step order.  Each workgroup writes
+// one fp32 partial slab [32][192] (k' order) + bias sums, reduced by reduce_grads.
 // ---------------------------------------------------------------------------------------
 DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restrict__ w2t,
                              const float* __restrict__ dy2, const uint32_t* __restrict__ mask1,
@@ -753,117 +763,129 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   using F = Frag<float>;
   typedef F::vec V;
   using L = C12B32;
-  constexpr int KS = F::KSTEP, LDIB = L::LDIB, LDX = L::LDX, LDD = L::LDD, LDZ = L::LDZ;
+  constexpr int KS = F::KSTEP, XP = L::XP, LDX = L::LDX, LDD = L::LDD, LDZ = L::LDZ;
+  static_assert(L::NROW == H1 * 16 && H1 < 16 && c1::GRID == 16, "dY1 rows: 16 pixels per image row");
   constexpr int NKO = OC2 / KS;             // 4 k-steps over oc
   constexpr int D2V = P2 * OC2 / 4;         // float4 vectors of one dY2 frame (576)
   constexpr int ND2 = (D2V + 255) / 256;
   float* smem = reinterpret_cast<float*>(lds);
-  uint8_t* img = reinterpret_cast<uint8_t*>(smem + L::IMG);
-  float* dyt = smem + L::DYT;
-  float* d2s = smem + L::D2S;
-  uint32_t* msk = reinterpret_cast<uint32_t*>(smem + L::MSK);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
+  const int grp = (int)threadIdx.x >> 8, tid = (int)threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int f0 = wg * fpw, f1 = min(N, f0 + fpw), nF = max(f1 - f0, 0);
   const int kl = 4 * (lane >> 4);
-  const int py = wave >> 1, px = wave & 1;  // this wave's stride-parity class
+  auto img_buf = [&](int b) { return reinterpret_cast<uint8_t*>(smem + L::IMG + b * L::IMGW); };
+  auto dyt_buf = [&](int b) { return smem + L::DYT + b * L::DYW; };
+  auto d2s_buf = [&](int b) { return smem + L::D2S + b * L::D2W; };
+  auto msk_buf = [&](int b) { return reinterpret_cast<uint32_t*>(smem + L::MSK + b * c1::NPIX); };
+  // ---- group A state ----
+  const int py = wave >> 1, px = wave & 1;  // A: this wave's stride-parity class
   float* zw = smem + L::Z0 + wave * L::ZSZ;
-  f32x4 acc[2][3];
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};    // A: conv1 bias partials of this lane's 4 channels
+  V wb[4][NKO][2];                          // A: W2 fragments [tap j1*2+j2][k-step][ci tile]
+  // ---- group B state ----
+  f32x4 acc[2][3];                          // B: conv1 weight gradient, oc tile i x ch tile j
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // conv1 bias partials of this lane's 4 channels
-  uint4 nv[3];
-  f32x4 nd2[ND2];
-  uint32_t nmk = 0;
-  auto fetch = [&](int f) {
-    c1_load_frame<float>(x + (size_t)f * IMG, tid, nv);
-    const float* src = dy2 + (size_t)f * P2 * OC2;
+  // group A's staging, global loads then LDS stores (the latency runs under group B's MFMAs):
+  // frame fi's image bytes -> IMG[bi] as [Y][channel c = ci * 16 + bb * 4 + d][X] bytes (a
+  // 4 x 4 byte transpose of the 16 bytes a thread loads: 4 cells X x 4 columns d), frame fd's
+  // dY2 rows / mask words -> D2S[bd] / MSK[bd]
+  auto stage = [&](int fi, int bi, int fd, int bd) {
+    uint4 nv[3];
+    f32x4 nd2[ND2];
+    uint32_t nmk = 0;
+    if (fi >= 0) c1_load_frame<float>(x + (size_t)fi * IMG, tid, nv);
+    if (fd >= 0) {
+      const float* src = dy2 + (size_t)fd * P2 * OC2;
 #pragma unroll
-    for (int i = 0; i < ND2; ++i) {
-      const int e = tid + i * 256;
-      nd2[i] = e < D2V ? *reinterpret_cast<const f32x4*>(src + e * 4) : F::zero();
+      for (int i = 0; i < ND2; ++i) {
+        const int e = tid + i * 256;
+        nd2[i] = e < D2V ? *reinterpret_cast<const f32x4*>(src + e * 4) : F::zero();
+      }
+      if (tid < c1::NPIX) nmk = mask1[(size_t)fd * c1::NPIX + tid];
+      float* d2s = d2s_buf(bd);
+#pragma unroll
+      for (int i = 0; i < ND2; ++i) {
+        const int e = tid + i * 256;
+        if (e < D2V) *reinterpret_cast<f32x4*>(d2s + ((e * 4) / OC2) * LDD + (e * 4) % OC2) = nd2[i];
+      }
+      if (tid < c1::NPIX) msk_buf(bd)[tid] = nmk;
     }
-    if (tid < c1::NPIX) nmk = mask1[(size_t)f * c1::NPIX + tid];
-  };
-  if (f0 < f1) fetch(f0);  // the first frame is in flight during the prologue
-  // ---- W2 fragments, B[k = oc][n = ci] = W2[oc][kh][kw][ci] for the class's 4 taps: 16-byte
-  // loads from the transposed copy w2t[(kh*4+kw)*32 + ci][oc] (k = oc contiguous) ----
-  V wb[4][NKO][2];  // [tap j1*2+j2][k-step][ci tile]
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
-#pragma unroll
-    for (int ks = 0; ks < NKO; ++ks)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-        wb[t][ks][ct] = F::load(w2t + (size_t)((kh * KS2 + kw) * OC1 + 16 * ct + (lane & 15)) * OC2 + ks * KS + kl);
-  }
-  // zero the dY1 rows no pixel writes (225..239), the dY2 pad rows (36..47) and each Z tile's
-  // zero row once
-  if (lane < OC1) *reinterpret_cast<f32x4*>(zw + P2 * LDZ + 4 * lane) = F::zero();
-  for (int e = tid; e < (L::NROW - c1::NPIX) * LDX / 4; e += 256)
-    *reinterpret_cast<f32x4*>(dyt + c1::NPIX * LDX + 4 * e) = F::zero();
-  for (int e = tid; e < (L::DROWS - P2) * LDD / 4; e += 256)
-    *reinterpret_cast<f32x4*>(d2s + P2 * LDD + 4 * e) = F::zero();
-  const int tapoff = ((wave >> 1) * c1::GRID + (wave & 1)) * LDIB;  // conv1 wgrad: tap = wave
-  // gather items of this lane: channels 4 cg .. 4 cg + 3 of class cells (qy = i, qx = slot)
-  const int cg = lane & 7, slot = lane >> 3;
-  for (int f = f0; f < f1; ++f) {
-    __syncthreads();  // the previous frame's readers are done
-    // frame bytes -> s2d byte rows: the 4 bytes of a 32-bit word are d = 0..3 of one channel row
+    if (fi < 0) return;
+    uint8_t* img = img_buf(bi);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int vi = tid + i * 256, ci = vi >> 8, yy = (vi & 255) >> 2, xq = vi & 3;
-      const int Y = yy >> 2, b = yy & 3;
-      const uint32_t w[4] = {nv[i].x, nv[i].y, nv[i].z, nv[i].w};
+      const int Y = yy >> 2, bb = yy & 3;
+      const uint32_t w[4] = {nv[i].x, nv[i].y, nv[i].z, nv[i].w};  // word q: cell X = 4 xq + q
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<uint32_t*>(img + (Y * c1::GRID + 4 * xq + q) * LDIB + ci * 16 + b * 4) = w[q];
-    }
+      for (int d = 0; d < 4; ++d) {
+        uint32_t t = 0;
 #pragma unroll
-    for (int i = 0; i < ND2; ++i) {
-      const int e = tid + i * 256;
-      if (e < D2V) {
-        const int op = (e * 4) / OC2, oc = (e * 4) % OC2;
-        *reinterpret_cast<f32x4*>(d2s + op * LDD + oc) = nd2[i];
+        for (int q = 0; q < 4; ++q) t |= ((w[q] >> (8 * d)) & 255u) << (8 * q);
+        *reinterpret_cast<uint32_t*>(img + (Y * c1::CH + ci * 16 + bb * 4 + d) * XP + 4 * xq) = t;
       }
     }
-    if (tid < c1::NPIX) msk[tid] = nmk;
-    __syncthreads();
-    if (f + 1 < f1) fetch(f + 1);
-    // ---- conv2 dgrad of class `wave`: Z = dY2 rows x W2 (two halves of 2 taps) ----
-    {
-      // Z^T tiles: A = the W2 fragments (rows = ci), B = the dY2 rows (cols = op), so a lane
-      // holds four consecutive channels of one op and stores them as one 16-byte write (the
-      // products and their k order are those of Z = dY2 x W2).  The dY2 fragments are read one
-      // k-step ahead instead of all up front (register pressure: the W2 fragments must stay
-      // resident across the frame loop).
-      // ops 0..31 are two 16-wide MFMA tiles; the last 4 (32..35) would fill a third tile 25 %
-      // (64 of the 192 MFMAs per half).  They run on v_mfma_f32_4x4x1_16b_f32 instead: block b
-      // = 4 g + og (lane 16 g + 4 og + j) takes rows 4 og .. 4 og + 3 (ci) of the same W2
-      // fragment element e and k-phase g = lane >> 4, op 32 + j: one 4x4x1 per (k-step, e, ci
-      // tile) instead of four 16x16x4 (tools/probe/mfma4x4.hip: lane map and 9.2 cycles each).
-      // The four k-phases g are summed at the end (butterfly over lanes ^16, ^32, fixed order).
+  };
+  if (grp == 0 && nF > 0) {
+    // W2 fragments, B[k = oc][n = ci] = W2[oc][kh][kw][ci] for the class's 4 taps: 16-byte loads
+    // from the transposed copy w2t[(kh*4+kw)*32 + ci][oc] (k = oc contiguous)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
+#pragma unroll
+      for (int ks = 0; ks < NKO; ++ks)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+          wb[t][ks][ct] = F::load(w2t + (size_t)((kh * KS2 + kw) * OC1 + 16 * ct + (lane & 15)) * OC2 + ks * KS + kl);
+    }
+  }
+  // zero once: each half-Z tile's row 36, and the dY1 pad rows (ix = 15) of both buffers
+  if (grp == 0 && lane < OC1 / 2) *reinterpret_cast<f32x4*>(zw + P2 * LDZ + 4 * lane) = F::zero();
+  for (int e = (int)threadIdx.x; e < 2 * H1 * (LDX / 4); e += 512) {
+    const int b = e / (H1 * (LDX / 4)), r = e % (H1 * (LDX / 4));
+    *reinterpret_cast<f32x4*>(dyt_buf(b) + ((r / (LDX / 4)) * 16 + 15) * LDX + 4 * (r % (LDX / 4))) = F::zero();
+  }
+  if (grp == 0 && nF > 0) stage(-1, 0, f0, 0);
+  __syncthreads();
+  // A: gather items of this lane: channels 4 cg .. 4 cg + 3 of class cells (qy, qx = slot)
+  const int cg = lane & 7, slot = lane >> 3;
+  // B: this wave's tap (ty, tx) of the conv1 weight gradient
+  const int ty = wave >> 1, tx = wave & 1;
+  // the groups run separate loops with the same barrier count (nF + 1), so that the compiler
+  // keeps each group's loop-carried registers (A: the W2 fragments; B: the accumulators) apart
+  if (grp == 0) {
+    for (int it = 0; it < nF; ++it) {
+      const int f = f0 + it, b = it & 1;
+      // the gather's lane offsets recomputed per frame (not hoisted out of the loop as ~50 live
+      // VGPRs)
+      int sl = slot;
+      asm volatile("" : "+v"(sl));
+      const float* d2s = d2s_buf(b);
+      const uint32_t* msk = msk_buf(b);
+      float* dyt = dyt_buf(b);
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
+        __builtin_amdgcn_sched_barrier(0);  // one half's registers live at a time
+        // ---- Z of taps 2 hf, 2 hf + 1 (Z^T tiles: A = the W2 fragments, rows = ci; B = the
+        // dY2 rows, cols = op, read one k-step ahead), ops 32..35 on 4x4x1 blocks: block b =
+        // 4 g + og (lane 16 g + 4 og + j) takes rows 4 og .. + 3 of W2 element e at k-phase
+        // g = lane >> 4, op 32 + j; the k-phases summed by a fixed butterfly at the end ----
         f32x4 z[2][4];  // [op tile][tap 2 hf + (cc >> 1), ci tile cc & 1]
-        f32x4 z4[4];    // ops 32..35 (4x4x1 blocks), per cc
+        f32x4 z4[4];    // ops 32..35, per cc
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          z[0][cc] = z[1][cc] = z4[cc] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        V a2[2][3];  // [ring][op tile 0, 1; 2 = ops 32 + (lane & 3) for the 4x4x1 blocks]
+        for (int cc = 0; cc < 4; ++cc) z[0][cc] = z[1][cc] = z4[cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+        V a2[2][3];
         auto a2load = [&](int ks, V* a) {
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt)
             a[rt] = *reinterpret_cast<const V*>(d2s + (16 * rt + (lane & 15)) * LDD + ks * KS + kl);
           a[2] = *reinterpret_cast<const V*>(d2s + (32 + (lane & 3)) * LDD + ks * KS + kl);
         };
-        a2load(0, a2[0]);
 #pragma unroll
         for (int ks = 0; ks < NKO; ++ks) {
-          if (ks + 1 < NKO) a2load(ks + 1, a2[(ks + 1) & 1]);
+          a2load(ks, a2[ks & 1]);
 #pragma unroll
           for (int e = 0; e < F::NE; ++e) {
 #pragma unroll
@@ -877,156 +899,170 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
                                                          a2[ks & 1][2][e], z4[cc], 0, 0, 0);
           }
         }
+        // the previous half's gather reads of the Z tile are done before it is overwritten
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
           const int op = 16 * rt + (lane & 15);
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc)
-            *reinterpret_cast<f32x4*>(zw + op * LDZ + (2 * hf + (cc >> 1)) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
+            *reinterpret_cast<f32x4*>(zw + op * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
         }
-        // 4x4x1 blocks: lane 16 g + 4 og + j holds Z[ci 4 og + i (reg i)][op 32 + j] over the
-        // k-phase g; the g-sum ((g0 + g1) + (g2 + g3)) lands on every lane, lanes 0..15 store
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
           f32x4 t;
 #pragma unroll
           for (int q = 0; q < 4; ++q) t[q] = xor32_sum(xor16_sum(z4[cc][q]));
           if (lane < 16)
-            *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ + (2 * hf + (cc >> 1)) * OC1 +
-                                      16 * (cc & 1) + 4 * (lane >> 2)) = t;
+            *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) +
+                                      4 * (lane >> 2)) = t;
         }
+        // the wave's own Z stores are done before its gather reads them (LDS is in order per
+        // wave; the wait + clobber keeps the compiler from moving the reads up)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // ---- col2im of class (py, px), taps (j1 = hf, j2): input pixel (2 qy + py, 2 qx + px)
+        // adds tap (py + 2 hf, px + 2 j2) at dY2 cell (qy - hf, qx - j2), order j2.  Half 0
+        // stores the partial sum, half 1 adds to it, masks, keeps the bias partials.  Branch-
+        // free (an out-of-range tap reads the zero row), row qy + 1's reads in flight while row
+        // qy is summed (two-stage pipeline pinned by scheduling barriers) ----
+        f32x4 zt[2][3];
+        uint32_t mk[2];
+        auto gload = [&](int qy, f32x4* zz, uint32_t& m) {
+          const int qx = sl, iy = 2 * qy + py, ix = 2 * qx + px;
+          const bool pv = iy < H1 && ix < H1;
+#pragma unroll
+          for (int j2 = 0; j2 < 2; ++j2) {
+            const int oy = qy - hf, ox = qx - j2;
+            const bool ok = pv && oy >= 0 && oy < H2 && ox >= 0 && ox < H2;
+            zz[j2] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + j2 * OC1 + 4 * cg);
+          }
+          if (hf == 1) {
+            zz[2] = *reinterpret_cast<const f32x4*>(dyt + (pv ? iy * 16 + ix : 0) * LDX + 4 * cg);
+            m = msk[pv ? iy * H1 + ix : 0];
+          }
+        };
+        gload(0, zt[0], mk[0]);
+#pragma unroll
+        for (int qy = 0; qy < 8; ++qy) {
+          if (qy + 1 < 8) gload(qy + 1, zt[(qy + 1) & 1], mk[(qy + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          const int qx = sl, iy = 2 * qy + py, ix = 2 * qx + px;
+          const bool pv = iy < H1 && ix < H1;
+          f32x4 v;
+          if (hf == 0) {
+            f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+            sum += zt[qy & 1][0];
+            sum += zt[qy & 1][1];
+            v = sum;
+          } else {
+            f32x4 sum = zt[qy & 1][2];
+            sum += zt[qy & 1][0];
+            sum += zt[qy & 1][1];
+            const uint32_t m = pv ? mk[qy & 1] : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[q] = (m >> (4 * cg + q)) & 1u ? sum[q] : 0.f;
+              bsum[q] += v[q];
+            }
+          }
+          if (pv) *reinterpret_cast<f32x4*>(dyt + (iy * 16 + ix) * LDX + 4 * cg) = v;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // half 1 reads back the partial sums this wave stored (LDS order per wave)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
+      // ---- stage frame f's image for group B and frame f + 1's dY2 / mask for the next step
+      stage(f, b, it + 1 < nF ? f + 1 : -1, b ^ 1);
+      __syncthreads();
     }
-    // the wave's own Z stores are done before its gather reads them (LDS is in order per wave;
-    // the wait + clobber keeps the compiler from moving the reads up)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // ---- col2im of class (py, px): input pixel (2 qy + py, 2 qx + px) sums taps
-    // (kh, kw) = (py + 2 j1, px + 2 j2) at dY2 cell (qy - j1, qx - j2), order j1, j2 ----
-    // Branch-free: every term is loaded (an out-of-range tap reads the zero row; + 0 leaves the
-    // sum of the in-range terms unchanged), so all of a lane's reads can be in flight at once.
-    // Two-stage pipeline pinned by scheduling barriers: row qy + 1's five reads are in flight
-    // while row qy is summed, masked and stored (left alone, every row waited for its own reads
-    // behind an lgkmcnt(0)).
-    f32x4 zt[2][4];
-    uint32_t mk[2];
-    auto gload = [&](int qy, f32x4* z, uint32_t& m) {
-      const int qx = slot, iy = 2 * qy + py, ix = 2 * qx + px;
-      const bool pv = iy < H1 && ix < H1;
+    __syncthreads();
+  } else {
+    __syncthreads();
+    for (int it = 1; it <= nF; ++it) {
+      // ---- conv1 weight gradient of frame it - 1 over its 15 x 16 pixel rows: A = dY1 (k =
+      // pixel), B = the image bytes of cell (iy + ty, ix + tx), channel n, converted to fp32:
+      // k-step iy, lane group g holds ix = 4 g .. 4 g + 3 = one 32-bit word (two aligned words
+      // funnel-shifted by tx bytes) ----
+      const int b = (it - 1) & 1;
+      const float* dyt = dyt_buf(b);
+      const uint8_t* img = img_buf(b);
+      auto load_a = [&](int kk, V* a) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int oy = qy - (t >> 1), ox = qx - (t & 1);
-        const bool ok = pv && oy >= 0 && oy < H2 && ox >= 0 && ox < H2;
-        z[t] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + t * OC1 + 4 * cg);
+        for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
+      };
+      const uint8_t* ib = img + (ty * c1::CH + (lane & 15)) * XP + 4 * (lane >> 4);
+      auto load_b = [&](int kk, uint32_t* raw) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(ib + ((kk / KS) * c1::CH + 16 * j) * XP);
+          raw[2 * j] = wp[0];
+          raw[2 * j + 1] = wp[1];
+        }
+      };
+      constexpr int NKK = L::NROW / KS;
+      V fa[2][2];
+      uint32_t raw[2][6];
+      load_a(0, fa[0]);
+      load_b(0, raw[0]);
+#pragma unroll
+      for (int s2 = 0; s2 < NKK; ++s2) {
+        // one scheduling region per k-step: the next step's reads ahead of this step's MFMAs,
+        // the bytes converted at the top of the step that uses them; MFMA order (j, e, i)
+        V fb[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const uint32_t w = __builtin_amdgcn_alignbyte(raw[s2 & 1][2 * j + 1], raw[s2 & 1][2 * j], tx);
+          fb[j] = V{(float)(w & 255u), (float)((w >> 8) & 255u), (float)((w >> 16) & 255u), (float)(w >> 24)};
+        }
+        if (s2 + 1 < NKK) {
+          load_a((s2 + 1) * KS, fa[(s2 + 1) & 1]);
+          load_b((s2 + 1) * KS, raw[(s2 + 1) & 1]);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU: the j = 0 word + conversions
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU: j = 1, 2, addresses
+        }
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      m = msk[pv ? iy * H1 + ix : 0];
-    };
-    gload(0, zt[0], mk[0]);
-#pragma unroll
-    for (int qy = 0; qy < 8; ++qy) {
-      if (qy + 1 < 8) gload(qy + 1, zt[(qy + 1) & 1], mk[(qy + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      const int qx = slot, iy = 2 * qy + py, ix = 2 * qx + px;
-      const bool pv = iy < H1 && ix < H1;
-      f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) sum += zt[qy & 1][t];
-      const uint32_t m = pv ? mk[qy & 1] : 0u;
-      f32x4 v;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[q] = (m >> (4 * cg + q)) & 1u ? sum[q] : 0.f;
-        bsum[q] += v[q];
-      }
-      if (pv) *reinterpret_cast<f32x4*>(dyt + (iy * H1 + ix) * LDX + 4 * cg) = v;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();  // dY1 complete
-    // ---- conv1 weight gradient over the 240 pixel rows: A = dY1 (k = pixel), B = the s2d
-    // image bytes at row(pixel, tap = wave), converted to fp32 ----
-    // The software pipeline is pinned with scheduling barriers: the LDS reads of k-step s + 1
-    // are issued ahead of the MFMAs of step s, and the bytes are converted at the top of the
-    // step that uses them.  Left alone, the scheduler (at this kernel's register pressure) sinks
-    // every read down to its use behind an lgkmcnt(0): 6 MFMAs per LDS round trip, the loop at
-    // 75 % of the MFMA issue rate (r03 stamps).
-    auto load_a = [&](int kk, V* a) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
-    };
-    auto load_b = [&](int kk, uint32_t* raw) {
-      const int g = lane >> 4, col = lane & 15;
-      int rr[4];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) rr[jj] = c1_row(min(kk + 4 * g + jj, c1::NPIX - 1), 0) * LDIB + tapoff + col;
-#pragma unroll
-      for (int j = 0; j < 3; ++j)  // j-major: the next step's first-needed bytes are read first
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) raw[4 * j + jj] = img[rr[jj] + 16 * j];
-    };
-    constexpr int NKK = L::NROW / KS;
-    V fa[2][2];
-    uint32_t raw[2][12];
-    load_a(0, fa[0]);
-    load_b(0, raw[0]);
-#pragma unroll
-    for (int s2 = 0; s2 < NKK; ++s2) {
-      // One scheduling region per k-step, its order pinned with group barriers: the j = 0
-      // bytes converted first, the j = 1, 2 conversions in the gaps of the first eight MFMAs
-      // (j = 0), step s + 1's sixteen LDS reads in the gaps of the next sixteen (j = 1, 2), so
-      // the MFMA pipe never drains between k-steps (32-cycle issue: room for one other
-      // instruction per gap).  MFMA order (j, e, i): acc[i][j] still sees e = 0..3 in turn.
-      V fb[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        fb[j] = V{(float)raw[s2 & 1][4 * j], (float)raw[s2 & 1][4 * j + 1],
-                  (float)raw[s2 & 1][4 * j + 2], (float)raw[s2 & 1][4 * j + 3]};
-      if (s2 + 1 < NKK) {
-        load_a((s2 + 1) * KS, fa[(s2 + 1) & 1]);
-        load_b((s2 + 1) * KS, raw[(s2 + 1) & 1]);
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int e = 0; e < F::NE; ++e)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
-      // the next step's reads go out in the first sixteen gaps (dY1 fragments, then the bytes
-      // j-major) so the j = 0 bytes have most of a step to land before they are converted
-      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU: the j = 0 conversions
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU: j = 1, 2 conversions
-      }
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
     }
   }
-  // conv1 bias: the 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order
-  __syncthreads();  // every frame's readers are done: the Z area holds the bias partials
+  // conv1 bias: group A's 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order
   float* bred = smem + L::Z0;
-  *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
+  if (grp == 0) *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
   __syncthreads();
-  if (tid < OC1) {
+  if (grp == 0 && tid < OC1) {
     float bs = 0.f;
 #pragma unroll 8
     for (int s = 0; s < 32; ++s) bs += bred[4 * (s * 8 + (tid >> 2)) + (tid & 3)];
     slab_bias[(size_t)wg * OC1 + tid] = bs;
   }
-  const size_t so = (size_t)wg * OC1 * K1;
+  if (grp == 1) {
+    const size_t so = (size_t)wg * OC1 * K1;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int col = wave * c1::CH + 16 * j + (lane & 15);
+      for (int j = 0; j < 3; ++j) {
+        const int col = wave * c1::CH + 16 * j + (lane & 15);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);
-    }
+        for (int q = 0; q < 4; ++q)
+          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);
+      }
+  }
 }
 
 template <typename T>

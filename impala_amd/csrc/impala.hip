@@ -447,7 +447,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
 stage_b:
   if (lc12) {
     if (int r = klaunch(h, K_LNC12_BWD, "ln_conv3_conv2_dgrad_conv1_wgrad", lnc3_conv12_bwd<T>,
-                        dim3(h->n_ln_wg), dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy,
+                        dim3(h->n_ln_wg), dim3(lnc3_threads<T>()), st, (const float*)h->dy,
                         (const T*)h->act3, (const float*)h->lnstat,
                         (const float*)(h->vecs + Vecs::lng), sw + sh.w3, sw + sh.w3t,
                         (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, b->obs,
@@ -456,7 +456,7 @@ stage_b:
       return r;
   } else if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
     if (int r = klaunch(h, K_LNC3_BWD, "ln_bwd_conv3_dgrad", lnc3_bwd<T>, dim3(h->n_ln_wg),
-                        dim3(256 * lnc3_groups<T>()), st, (const float*)h->dy, (const T*)h->act3,
+                        dim3(lnc3_threads<T>()), st, (const float*)h->dy, (const T*)h->act3,
                         (const float*)h->lnstat, (const float*)(h->vecs + Vecs::lng), sw + sh.w3,
                         sw + sh.w3t, (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, N,
                         h->ln_fpw))

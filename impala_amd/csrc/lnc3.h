@@ -28,6 +28,15 @@ constexpr int ZR = 9 * OC2 + 4;  // Z row (fp32): [tap][ci] of one output pixel,
 }
 
 template <typename T> constexpr int lnc3_groups() { return sizeof(T) == 2 ? 2 : 1; }
+// threads of a launch: bf16 2 groups of 4 waves on alternating frames; fp32 8 waves on one
+// frame (lnc3_body_f32)
+template <typename T> constexpr int lnc3_threads() { return sizeof(T) == 2 ? 256 * lnc3_groups<T>() : 512; }
+
+// fp32 LDS (bytes): Z (fp32 [16 + 1][ZR], row 16 zero), the dact3 tile [16][LD3], the LN sums
+struct Lnc3F32 {
+  static constexpr int LD3 = OC3 + 8;
+  static constexpr int D3 = (P3 + 1) * lc3::ZR * 4, RED = D3 + P3 * LD3 * 4, BYTES = RED + 4 * 2 * 4;
+};
 
 // LDS of the body (bytes): the W3 staging / per-group Z + dact3 tiles, then red and comb
 template <typename T> struct Lnc3Lds {
@@ -38,13 +47,14 @@ template <typename T> struct Lnc3Lds {
   // W3 staging (bf16; fp32 loads its fragments from the transposed copy)
   static constexpr int STG = REG ? OC3 * LW * (int)sizeof(T) : 0;
   static constexpr int SMEM = STG > G * GB ? STG : G * GB;
-  static constexpr int RED = SMEM, COMB = RED + G * 4 * 2 * 4, BYTES = COMB + 2 * FLAT * 4;
+  static constexpr int RED = SMEM, COMB = RED + G * 4 * 2 * 4;
+  static constexpr int BYTES = sizeof(T) == 4 ? Lnc3F32::BYTES : COMB + 2 * FLAT * 4;
 };
 
 // The kernel body, on workgroup `wg` (frames wg*fpw ..) with the LDS passed in
 // (Lnc3Lds<T>::BYTES), so a launch can run it ahead of another per-frame body.
 template <typename T>
-DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
+DEV void lnc3_body_g(const float* __restrict__ dy, const T* __restrict__ act3,
                    const float* __restrict__ stats, const float* __restrict__ gam,
                    const T* __restrict__ w3, const T* __restrict__ w3t,
                    const T* __restrict__ act2, T* __restrict__ dact3,
@@ -250,8 +260,179 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
         *reinterpret_cast<const f32x4*>(comb + 4 * e);
 }
 
+// fp32: one frame at a time on 8 waves (512 threads: the shape of the two-group conv12 body it
+// is fused with, whose launch bounds leave 256 VGPRs per lane -- the one-group form held all
+// nine taps' W3 fragments, 144 VGPRs, per wave).  The LayerNorm part runs on waves 0..3 as
+// in the one-group form (lane: 4 consecutive features); the scatter GEMM splits the taps:
+// wave w owns ci tile w & 3 of taps 0..4 (w < 4) or 5..8 (w >= 4); the gather runs on all
+// 512 threads.  Same sums in the same order as the one-group form.
+DEV void lnc3_body_f32(const float* __restrict__ dy, const float* __restrict__ act3,
+                       const float* __restrict__ stats, const float* __restrict__ gam,
+                       const float* __restrict__ w3t, const float* __restrict__ act2,
+                       float* __restrict__ dact3, float* __restrict__ dact2, float* __restrict__ slab,
+                       int N, int fpw, int wg, char* __restrict__ lds) {
+  using F = Frag<float>;
+  typedef F::vec V;
+  constexpr int KS = F::KSTEP, NKO = OC3 / KS, LD3 = Lnc3F32::LD3;
+  constexpr int NGI = (P2 * 16 + 511) / 512;  // gather items per thread
+  constexpr int NT0 = 5;                      // taps of the first half
+  float* zs = reinterpret_cast<float*>(lds);
+  float* d3s = reinterpret_cast<float*>(lds + Lnc3F32::D3);
+  float (*red)[2] = reinterpret_cast<float (*)[2]>(lds + Lnc3F32::RED);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool ln = wave < 4;  // waves 0..3: the LayerNorm features
+  const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
+  const int kl = 4 * (lane >> 4);
+  const int j0 = 256 * (wave & 3) + 4 * lane, p0 = j0 >> 6, c0 = j0 & 63;
+  const int ct = wave & 3, th = wave >> 2;  // Z: ci tile, tap half
+  f32x4 ndy = f32x4{0.f, 0.f, 0.f, 0.f};
+  float nx[4] = {0.f, 0.f, 0.f, 0.f}, nm = 0.f, nr = 0.f, na[NGI][4];
+  auto fetch = [&](int f) {
+    if (ln) {
+      ndy = *reinterpret_cast<const f32x4*>(dy + (size_t)f * FLAT + j0);
+      load4(act3 + (size_t)f * FLAT + j0, nx);
+      nm = stats[2 * f];
+      nr = stats[2 * f + 1];
+    }
+#pragma unroll
+    for (int r = 0; r < NGI; ++r) {  // gather items e = t + 512 r: pixel e / 16, channels 4 (e % 16)
+      const int e = min(t + 512 * r, P2 * 16 - 1);
+      load4(act2 + ((size_t)f * P2 + (e >> 4)) * OC2 + 4 * (e & 15), na[r]);
+    }
+  };
+  if (f0 < f1) fetch(f0);
+  float gm[4], dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gm[q] = gam[j0 + q];
+  // W3 fragments of this wave's taps, from the transposed copy w3t[tap*64 + ci][oc]
+  V wa[NT0][NKO];
+#pragma unroll
+  for (int tt = 0; tt < NT0; ++tt) {
+    const int tap = min(NT0 * th + tt, 8);
+#pragma unroll
+    for (int ko = 0; ko < NKO; ++ko)
+      wa[tt][ko] = F::load(w3t + (size_t)(tap * OC2 + 16 * ct + (lane & 15)) * OC3 + ko * KS + kl);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(gm[q]));
+  for (int e = t; e < lc3::ZR / 4; e += 512)  // the Z tile's zero row
+    *reinterpret_cast<f32x4*>(zs + P3 * lc3::ZR + 4 * e) = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Z^T for NT taps of this wave: the taps' accumulators side by side (MFMA e of every tap
+  // before e + 1); a lane stores four consecutive channels of one pixel per tap
+  auto zgemm = [&](auto ntc) {
+    constexpr int NT = decltype(ntc)::value;
+    V a[NKO];
+#pragma unroll
+    for (int ko = 0; ko < NKO; ++ko)
+      a[ko] = *reinterpret_cast<const V*>(d3s + (lane & 15) * LD3 + ko * KS + kl);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ko = 0; ko < NKO; ++ko)
+#pragma unroll
+      for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) acc[tt] = F::mma_e(e, wa[tt][ko], a[ko], acc[tt]);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+      *reinterpret_cast<f32x4*>(zs + (lane & 15) * lc3::ZR + (NT0 * th + tt) * OC2 + 16 * ct + kl) = acc[tt];
+  };
+  for (int f = f0; f < f1; ++f) {
+    __syncthreads();  // the previous frame's readers of Z / dact3 / red are done
+    float d[4], x[4], xh[4], am[NGI][4];
+    const float mean = nm, rstd = nr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { d[q] = ndy[q]; x[q] = nx[q]; }
+#pragma unroll
+    for (int r = 0; r < NGI; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) am[r][q] = na[r][q];
+    // ---- LayerNorm backward: the two per-frame sums ----
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xh[q] = (x[q] - mean) * rstd;
+      const float gd = d[q] * gm[q];
+      s1 += gd;
+      s2 += gd * xh[q];
+    }
+    if (ln) {
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      if (lane == 0) { red[wave][0] = s1; red[wave][1] = s2; }
+    }
+    __syncthreads();
+    if (f + 1 < f1) fetch(f + 1);
+    if (ln) {
+      const float S1 = (red[0][0] + red[1][0] + red[2][0] + red[3][0]) * (1.f / FLAT);
+      const float S2 = (red[0][1] + red[1][1] + red[2][1] + red[3][1]) * (1.f / FLAT);
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dg[q] += d[q] * xh[q];
+        db[q] += d[q];
+        const float gx = rstd * (d[q] * gm[q] - S1 - xh[q] * S2);
+        o[q] = x[q] > 0.f ? gx : 0.f;
+      }
+      store4(dact3 + (size_t)f * FLAT + j0, o);
+      store4(d3s + p0 * LD3 + c0, o);
+    }
+    __syncthreads();
+    // ---- Z[p][tap][ci] = sum_oc dact3[p][oc] W3[oc][tap][ci] ----
+    if (th == 0)
+      zgemm(std::integral_constant<int, NT0>{});
+    else
+      zgemm(std::integral_constant<int, 9 - NT0>{});
+    __syncthreads();
+    // ---- col2im gather in a fixed (kh, kw) order + conv2's ReLU mask -> dact2 ----
+#pragma unroll
+    for (int r = 0; r < NGI; ++r) {
+      const int e = t + 512 * r;
+      if (e < P2 * 16) {
+        const int px = e >> 4, ci = 4 * (e & 15), iy = px / H2, ix = px - iy * H2;
+        f32x4 zt[9];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int oy = iy - kh, ox = ix - kw;
+            const bool ok = oy >= 0 && oy < H3 && ox >= 0 && ox < H3;
+            zt[kh * 3 + kw] = *reinterpret_cast<const f32x4*>(
+                zs + (ok ? oy * H3 + ox : P3) * lc3::ZR + (kh * 3 + kw) * OC2 + ci);
+          }
+        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 9; ++k) sum += zt[k];
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = am[r][q] > 0.f ? sum[q] : 0.f;
+        store4(dact2 + ((size_t)f * P2 + px) * OC2 + ci, o);
+      }
+    }
+  }
+  // ---- gamma / beta partials -> slab [2][1024] ----
+  if (ln) {
+    *reinterpret_cast<f32x4*>(slab + (size_t)wg * 2 * FLAT + j0) = f32x4{dg[0], dg[1], dg[2], dg[3]};
+    *reinterpret_cast<f32x4*>(slab + (size_t)wg * 2 * FLAT + FLAT + j0) = f32x4{db[0], db[1], db[2], db[3]};
+  }
+}
+
 template <typename T>
-__global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
+DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
+                   const float* __restrict__ stats, const float* __restrict__ gam,
+                   const T* __restrict__ w3, const T* __restrict__ w3t,
+                   const T* __restrict__ act2, T* __restrict__ dact3,
+                   T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw, int wg,
+                   char* __restrict__ lds) {
+  if constexpr (sizeof(T) == 4)
+    lnc3_body_f32(dy, act3, stats, gam, w3t, act2, dact3, dact2, slab, N, fpw, wg, lds);
+  else
+    lnc3_body_g<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, slab, N, fpw, wg, lds);
+}
+
+template <typename T>
+__global__ __launch_bounds__(lnc3_threads<T>()) void lnc3_bwd(
     const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
     const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ w3t,
     const T* __restrict__ act2, T* __restrict__ dact3, T* __restrict__ dact2,
@@ -267,14 +448,14 @@ __global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_bwd(
 // The two bodies share the LDS (its size is the larger of theirs).  The conv3 / conv2 weight
 // gradients, which need dact3 / dact2 of all frames, run after it.
 template <typename T>
-__global__ __launch_bounds__(256 * lnc3_groups<T>()) void lnc3_conv12_bwd(
+__global__ __launch_bounds__(lnc3_threads<T>()) void lnc3_conv12_bwd(
     const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
     const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ w3t,
     const T* __restrict__ act2, T* __restrict__ dact3, T* __restrict__ dact2,
     float* __restrict__ ln_slab, const uint8_t* __restrict__ x, const T* __restrict__ w2,
     const T* __restrict__ w2t, const uint32_t* __restrict__ mask1,
     float* __restrict__ c1_slab, float* __restrict__ c1_slab_bias, int N, int fpw) {
-  static_assert(lnc3_groups<T>() == c12_groups<T>(), "one block shape for both bodies");
+  static_assert(lnc3_threads<T>() == 256 * c12_groups<T>(), "one block shape for both bodies");
   constexpr int B1 = Lnc3Lds<T>::BYTES, B2 = C12BLds<T>::BYTES;
   __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
   lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
