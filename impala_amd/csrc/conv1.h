@@ -787,7 +787,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // group A's staging, global loads then LDS stores (the latency runs under group B's MFMAs):
+  // group B's staging, global loads then LDS stores (the latency runs under group A's work):
   // frame fi's image bytes -> IMG[bi] as [Y][channel c = ci * 16 + bb * 4 + d][X] bytes (a
   // 4 x 4 byte transpose of the 16 bytes a thread loads: 4 cells X x 4 columns d), frame fd's
   // dY2 rows / mask words -> D2S[bd] / MSK[bd]
@@ -847,7 +847,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     const int b = e / (H1 * (LDX / 4)), r = e % (H1 * (LDX / 4));
     *reinterpret_cast<f32x4*>(dyt_buf(b) + ((r / (LDX / 4)) * 16 + 15) * LDX + 4 * (r % (LDX / 4))) = F::zero();
   }
-  if (grp == 0 && nF > 0) stage(-1, 0, f0, 0);
+  if (grp == 1 && nF > 0) stage(-1, 0, f0, 0);
   __syncthreads();
   // A: gather items of this lane: channels 4 cg .. 4 cg + 3 of class cells (qy, qx = slot)
   const int cg = lane & 7, slot = lane >> 3;
@@ -971,12 +971,13 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
         // half 1 reads back the partial sums this wave stored (LDS order per wave)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      // ---- stage frame f's image for group B and frame f + 1's dY2 / mask for the next step
-      stage(f, b, it + 1 < nF ? f + 1 : -1, b ^ 1);
       __syncthreads();
     }
     __syncthreads();
   } else {
+    // group B stages every frame: in step k (after its weight gradient of frame k - 1), frame
+    // k's image (read by B in step k + 1) and frame k + 1's dY2 / mask (read by A in step k + 1)
+    stage(nF > 0 ? f0 : -1, 0, nF > 1 ? f0 + 1 : -1, 1);
     __syncthreads();
     for (int it = 1; it <= nF; ++it) {
       // ---- conv1 weight gradient of frame it - 1 over its 15 x 16 pixel rows: A = dY1 (k =
@@ -1038,6 +1039,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      stage(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1);
       __syncthreads();
     }
   }

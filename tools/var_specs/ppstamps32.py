@@ -2,27 +2,28 @@
 # group A wave 0 (thread 0) per frame: top / Z half 0 / gather half 0 / Z half 1 / gather half 1
 # / staged; group B wave 4 (thread 256) per step: top / wgrad done.  "PP" lines.
 C = "conv1.h"
+LN = "lnc3.h"
 def S(i, t=0):
     return (f"__builtin_amdgcn_sched_barrier(0); if (blockIdx.x == 0 && threadIdx.x == {t}) g_pp[{i}] = "
             "__builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); ")
 VARIANTS = {
     "ppst": [
+        (LN, "  const bool ln = wave < 4;  // waves 0..3: the LayerNorm features\n", "  const bool ln = wave < 4;  // waves 0..3: the LayerNorm features\n  " + S(61) + "\n"),
+        (LN, "  // ---- gamma / beta partials -> slab [2][1024] ----\n", "  " + S(62) + "\n  // ---- gamma / beta partials -> slab [2][1024] ----\n"),
         (C, "namespace c1 {\nconstexpr int GRID", "__device__ long long g_pp[64];\nnamespace c1 {\nconstexpr int GRID"),
         (C, "  if (grp == 0 && nF > 0) {\n    // W2", "  " + S(0) + "\n  if (grp == 0 && nF > 0) {\n    // W2"),
-        (C, "  if (grp == 0 && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();",
-            "  if (grp == 0 && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();\n  " + S(1)),
+        (C, "  if (grp == 1 && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();",
+            "  if (grp == 1 && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();\n  " + S(1)),
         (C, '      asm volatile("" : "+v"(sl));', '      asm volatile("" : "+v"(sl));\n      ' + S("2 + 6 * it")),
         (C, "        // the previous half's gather reads of the Z tile are done before it is overwritten",
             "        " + S("3 + 6 * it + 2 * hf") + "\n        // the previous half's gather reads of the Z tile are done before it is overwritten"),
         (C, "        // half 1 reads back the partial sums this wave stored",
             "        " + S("4 + 6 * it + 2 * hf") + "\n        // half 1 reads back the partial sums this wave stored"),
-        (C, "      stage(f, b, it + 1 < nF ? f + 1 : -1, b ^ 1);\n      __syncthreads();",
-            "      stage(f, b, it + 1 < nF ? f + 1 : -1, b ^ 1);\n      " + S("7 + 6 * it") + "\n      __syncthreads();"),
+        (C, "      stage(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1);\n",
+            "      " + S("41 + 2 * (it - 1)", 256) + "\n      stage(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1);\n      " + S("52 + (it - 1)", 256) + "\n"),
         (C, '      const int b = (it - 1) & 1;\n      const float* dyt = dyt_buf(b);', '      ' + S("40 + 2 * (it - 1)", 256) + '\n      const int b = (it - 1) & 1;\n      const float* dyt = dyt_buf(b);'),
-        (C, "        __builtin_amdgcn_sched_barrier(0);\n      }\n      __syncthreads();\n    }\n  }",
-            "        __builtin_amdgcn_sched_barrier(0);\n      }\n      " + S("41 + 2 * (it - 1)", 256) + "\n      __syncthreads();\n    }\n  }"),
         (C, "          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n      }\n  }\n}",
             "          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n      }\n  }\n  __syncthreads();\n  " + S(60)
-            + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("PP"); for (int q = 1; q < 61; ++q) if (q < 32 || (q >= 40 && q < 52) || q == 60) printf(" %lld", g_pp[q] ? g_pp[q] - g_pp[0] : -1); printf("\\n"); }\n}'),
+            + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("PP"); for (int q = 1; q < 63; ++q) if (q < 32 || (q >= 40 && q < 58) || q >= 60) printf(" %lld", g_pp[q] ? g_pp[q] - g_pp[0] : -1); printf("\\n"); }\n}'),
     ],
 }
