@@ -146,6 +146,30 @@ DEV float xor32_sum(float v) {
   swap32(a, b);
   return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);
 }
+// Four values reduced over the four rows at once (3 swaps, 3 adds, instead of 4 x 2 of each):
+// row r of the result holds ((x[row 0] + x[row 1]) + (x[row 2] + x[row 3])) of x = a, b, c, d for
+// r = 0, 1, 2, 3 -- the value and the order of xor32_sum(xor16_sum(x)).
+DEV float rows_sum4(float a, float b, float c, float d) {
+  // one asm block: its inputs come straight from MFMAs, whose results a following VALU /
+  // permlane may only read after the XDL write latency (the leading 20 wait states; the
+  // compiler does not insert them for inline asm), and the adds -> permlane32 read hazard
+  // (s_nop 1).  Rows after the swaps: a = [a0 b0 a2 b2], b = [a1 b1 a3 b3]; after the adds and
+  // the xor-32 swap, a = [a01 b01 c01 d01], c = [a23 b23 c23 d23].
+  asm volatile(
+      "s_nop 7\n\ts_nop 7\n\ts_nop 3\n\t"
+      "v_permlane16_swap_b32 %0, %1\n\t"
+      "v_permlane16_swap_b32 %2, %3\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32 %0, %0, %1\n\t"
+      "v_add_f32 %2, %2, %3\n\t"
+      "s_nop 1\n\t"
+      "v_permlane32_swap_b32 %0, %2\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32 %0, %0, %2\n\t"
+      "s_nop 1"
+      : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+  return a;
+}
 DEV uint32_t xor16_or(uint32_t v) {
   uint32_t a = v, b = v;
   swap16(a, b);

@@ -504,20 +504,14 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
       if constexpr (!W2REG) {
         // the 4x4x1 blocks: lane 16 g + 4 og + j holds act2[pixel 32 + j][oc 16 w + 4 og + reg]
-        // over k-phase g; ((g0 + g1) + (g2 + g3)) on every lane, lanes 0..15 store
-        const int pc = 32 + (lane & 3), oc0 = 16 * wave + 4 * ((lane >> 2) & 3);
-        f32x4 t;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = xor32_sum(xor16_sum(acc[2][q]));
-        if (lane < 16) {
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(t[q] + b2[oc0 + q], 0.f);
-          store4(act2 + ((size_t)f * P2 + pc) * OC2 + oc0, v);
-          if (tail) {
-            const int cy = pc / H2, cx = pc - cy * H2;
-            store4(a2s + ((f - f0) * A2F + cy * A2W + cx) * LDA2 + oc0, v);
-          }
+        // over k-phase g; ((g0 + g1) + (g2 + g3)) of reg q lands on row q (rows_sum4), so lane
+        // 16 q + 4 og + j stores one value
+        const int pc = 32 + (lane & 3), oc = 16 * wave + 4 * ((lane >> 2) & 3) + (lane >> 4);
+        const float v = fmaxf(rows_sum4(acc[2][0], acc[2][1], acc[2][2], acc[2][3]) + b2[oc], 0.f);
+        act2[((size_t)f * P2 + pc) * OC2 + oc] = (T)v;
+        if (tail) {
+          const int cy = pc / H2, cx = pc - cy * H2;
+          a2s[((f - f0) * A2F + cy * A2W + cx) * LDA2 + oc] = (T)v;
         }
       }
 #pragma unroll
@@ -908,14 +902,15 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
           for (int cc = 0; cc < 4; ++cc)
             *reinterpret_cast<f32x4*>(zw + op * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
         }
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
+        {
+          // the k-phase sums of the four cc at once: row cc of t holds cc's (rows_sum4), lane
+          // 16 cc + 4 og + j stores ci 16 (cc & 1) + 4 og .. + 3 of op 32 + j
           f32x4 t;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) t[q] = xor32_sum(xor16_sum(z4[cc][q]));
-          if (lane < 16)
-            *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) +
-                                      4 * (lane >> 2)) = t;
+          for (int q = 0; q < 4; ++q) t[q] = rows_sum4(z4[0][q], z4[1][q], z4[2][q], z4[3][q]);
+          const int cc = lane >> 4;
+          *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) +
+                                    4 * ((lane >> 2) & 3)) = t;
         }
         // the wave's own Z stores are done before its gather reads them (LDS is in order per
         // wave; the wait + clobber keeps the compiler from moving the reads up)
@@ -950,14 +945,13 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
           const bool pv = iy < H1 && ix < H1;
           f32x4 v;
           if (hf == 0) {
-            f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-            sum += zt[qy & 1][0];
-            sum += zt[qy & 1][1];
-            v = sum;
+            v = zt[qy & 1][0] + zt[qy & 1][1];
           } else {
             f32x4 sum = zt[qy & 1][2];
             sum += zt[qy & 1][0];
             sum += zt[qy & 1][1];
+            // the ReLU mask as a bit mask: a sign-extended 1-bit field is 0 or ~0, so the AND
+            // keeps the sum or makes +0 (a select, in two instructions instead of three)
             const uint32_t m = pv ? mk[qy & 1] : 0u;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
