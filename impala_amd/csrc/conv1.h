@@ -726,6 +726,31 @@ template <typename T> struct C12BLds {
   static constexpr int BYTES = sizeof(T) == 4 ? C12B32::BYTES : BRED + 4 * G * OC1 * 4;
 };
 
+// The W2 fragments of stride-parity class `cls` (conv12_bwd_body_f32's group A wave):
+// B[k = oc][n = ci] = W2[oc][kh][kw][ci] for the class's 4 taps, 16-byte loads from the
+// transposed copy w2t[(kh*4+kw)*32 + ci][oc] (k = oc contiguous)
+DEV void c12_load_w2(const float* __restrict__ w2t, Frag<float>::vec (&wb)[4][OC2 / Frag<float>::KSTEP][2],
+                     int cls, int lane, int t0 = 0, int t1 = 4) {  // taps [t0, t1)
+  using F = Frag<float>;
+  constexpr int KS = F::KSTEP, NKO = OC2 / KS;
+  // 32-bit element offsets from the (uniform) base, from a lane value the compiler cannot hoist:
+  // a caller inside a frame loop would otherwise keep 32 64-bit addresses live across it
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  const int py = cls >> 1, px = cls & 1;
+  const uint32_t o0 = (uint32_t)((ln & 15) * OC2 + 4 * (ln >> 4));
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t < t0 || t >= t1) continue;
+    const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
+#pragma unroll
+    for (int ks = 0; ks < NKO; ++ks)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+        wb[t][ks][ct] = F::load(w2t + (o0 + (uint32_t)(((kh * KS2 + kw) * OC1 + 16 * ct) * OC2 + ks * KS)));
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // fp32 conv2 input gradient + ReLU mask + conv1 weight gradient, per frame, in SCATTER form:
 //
@@ -750,10 +775,12 @@ template <typename T> struct C12BLds {
 // sums ((z0 + z1) + z2) + z3, oc in MFMA order, pixels in k-step order.  Each workgroup writes
 // one fp32 partial slab [32][192] (k' order) + bias sums, reduced by reduce_grads.
 // ---------------------------------------------------------------------------------------
+template <int ROLE>
 DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restrict__ w2t,
                              const float* __restrict__ dy2, const uint32_t* __restrict__ mask1,
                              float* __restrict__ slab, float* __restrict__ slab_bias, int N,
-                             int fpw, int wg, char* __restrict__ lds) {
+                             int fpw, int wg, char* __restrict__ lds,
+                             Frag<float>::vec (&wb)[4][OC2 / Frag<float>::KSTEP][2], bool load_w2) {
   using F = Frag<float>;
   typedef F::vec V;
   using L = C12B32;
@@ -763,7 +790,10 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   constexpr int D2V = P2 * OC2 / 4;         // float4 vectors of one dY2 frame (576)
   constexpr int ND2 = (D2V + 255) / 256;
   float* smem = reinterpret_cast<float*>(lds);
-  const int grp = (int)threadIdx.x >> 8, tid = (int)threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  // ROLE 0 / 1: this wave's group is known at compile time (the fused kernel runs each group as
+  // its own code path); -1: decided per wave here
+  const bool is_a = ROLE == 0 ? true : ROLE == 1 ? false : ((int)threadIdx.x >> 8) == 0;
+  const int tid = (int)threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   const int f0 = wg * fpw, f1 = min(N, f0 + fpw), nF = max(f1 - f0, 0);
   const int kl = 4 * (lane >> 4);
   auto img_buf = [&](int b) { return reinterpret_cast<uint8_t*>(smem + L::IMG + b * L::IMGW); };
@@ -774,7 +804,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   const int py = wave >> 1, px = wave & 1;  // A: this wave's stride-parity class
   float* zw = smem + L::Z0 + wave * L::ZSZ;
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};    // A: conv1 bias partials of this lane's 4 channels
-  V wb[4][NKO][2];                          // A: W2 fragments [tap j1*2+j2][k-step][ci tile]
+  // A: W2 fragments wb[tap j1*2+j2][k-step][ci tile] (c12_load_w2; loaded here if load_w2)
   // ---- group B state ----
   f32x4 acc[2][3];                          // B: conv1 weight gradient, oc tile i x ch tile j
 #pragma unroll
@@ -822,26 +852,14 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
       }
     }
   };
-  if (grp == 0 && nF > 0) {
-    // W2 fragments, B[k = oc][n = ci] = W2[oc][kh][kw][ci] for the class's 4 taps: 16-byte loads
-    // from the transposed copy w2t[(kh*4+kw)*32 + ci][oc] (k = oc contiguous)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int kh = py + 2 * (t >> 1), kw = px + 2 * (t & 1);
-#pragma unroll
-      for (int ks = 0; ks < NKO; ++ks)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-          wb[t][ks][ct] = F::load(w2t + (size_t)((kh * KS2 + kw) * OC1 + 16 * ct + (lane & 15)) * OC2 + ks * KS + kl);
-    }
-  }
+  if (is_a && nF > 0 && load_w2) c12_load_w2(w2t, wb, wave, lane);
   // zero once: each half-Z tile's row 36, and the dY1 pad rows (ix = 15) of both buffers
-  if (grp == 0 && lane < OC1 / 2) *reinterpret_cast<f32x4*>(zw + P2 * LDZ + 4 * lane) = F::zero();
+  if (is_a && lane < OC1 / 2) *reinterpret_cast<f32x4*>(zw + P2 * LDZ + 4 * lane) = F::zero();
   for (int e = (int)threadIdx.x; e < 2 * H1 * (LDX / 4); e += 512) {
     const int b = e / (H1 * (LDX / 4)), r = e % (H1 * (LDX / 4));
     *reinterpret_cast<f32x4*>(dyt_buf(b) + ((r / (LDX / 4)) * 16 + 15) * LDX + 4 * (r % (LDX / 4))) = F::zero();
   }
-  if (grp == 1 && nF > 0) stage(-1, 0, f0, 0);
+  if (!is_a && nF > 0) stage(-1, 0, f0, 0);
   __syncthreads();
   // A: gather items of this lane: channels 4 cg .. 4 cg + 3 of class cells (qy, qx = slot)
   const int cg = lane & 7, slot = lane >> 3;
@@ -849,7 +867,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   const int ty = wave >> 1, tx = wave & 1;
   // the groups run separate loops with the same barrier count (nF + 1), so that the compiler
   // keeps each group's loop-carried registers (A: the W2 fragments; B: the accumulators) apart
-  if (grp == 0) {
+  if (is_a) {
     for (int it = 0; it < nF; ++it) {
       const int f = f0 + it, b = it & 1;
       // the gather's lane offsets recomputed per frame (not hoisted out of the loop as ~50 live
@@ -1039,15 +1057,15 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   }
   // conv1 bias: group A's 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order
   float* bred = smem + L::Z0;
-  if (grp == 0) *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
+  if (is_a) *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
   __syncthreads();
-  if (grp == 0 && tid < OC1) {
+  if (is_a && tid < OC1) {
     float bs = 0.f;
 #pragma unroll 8
     for (int s = 0; s < 32; ++s) bs += bred[4 * (s * 8 + (tid >> 2)) + (tid & 3)];
     slab_bias[(size_t)wg * OC1 + tid] = bs;
   }
-  if (grp == 1) {
+  if (!is_a) {
     const size_t so = (size_t)wg * OC1 * K1;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1067,8 +1085,9 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
                          float* __restrict__ slab, float* __restrict__ slab_bias, int N, int fpw,
                          int wg, char* __restrict__ lds) {
   if constexpr (sizeof(T) == 4) {  // fp32: the scatter-form body above
-    conv12_bwd_body_f32(x, reinterpret_cast<const float*>(w2t), reinterpret_cast<const float*>(dy2),
-                        mask1, slab, slab_bias, N, fpw, wg, lds);
+    Frag<float>::vec wb[4][OC2 / Frag<float>::KSTEP][2];
+    conv12_bwd_body_f32<-1>(x, reinterpret_cast<const float*>(w2t), reinterpret_cast<const float*>(dy2),
+                            mask1, slab, slab_bias, N, fpw, wg, lds, wb, true);
     return;
   }
   using F = Frag<T>;

@@ -262,33 +262,41 @@ DEV void lnc3_body_g(const float* __restrict__ dy, const T* __restrict__ act3,
 
 // fp32: one frame at a time on 8 waves (512 threads: the shape of the two-group conv12 body it
 // is fused with, whose launch bounds leave 256 VGPRs per lane -- the one-group form held all
-// nine taps' W3 fragments, 144 VGPRs, per wave).  The LayerNorm part runs on waves 0..3 as
-// in the one-group form (lane: 4 consecutive features); the scatter GEMM splits the taps:
-// wave w owns ci tile w & 3 of taps 0..4 (w < 4) or 5..8 (w >= 4); the gather runs on all
-// 512 threads.  Same sums in the same order as the one-group form.
-DEV void lnc3_body_f32(const float* __restrict__ dy, const float* __restrict__ act3,
-                       const float* __restrict__ stats, const float* __restrict__ gam,
-                       const float* __restrict__ w3t, const float* __restrict__ act2,
-                       float* __restrict__ dact3, float* __restrict__ dact2, float* __restrict__ slab,
-                       int N, int fpw, int wg, char* __restrict__ lds) {
+// nine taps' W3 fragments, 144 VGPRs, on every wave).  Two roles, each a separate code path
+// (ROLE is a template parameter; a workgroup runs role 0 on waves 0..3 and role 1 on waves
+// 4..7, with the same barriers):
+//   role 0: the LayerNorm backward (lane: 4 consecutive features, as in the one-group form) and
+//           half of the gather; its registers stay free for the conv12 body's W2 fragments,
+//           which `pre(k)` loads during the frames, one tap (32 KB per workgroup) in frame
+//           1 + k after that frame's prefetch, so the W3 burst is not delayed and no frame's
+//           loads queue behind all 128 KB (one 128 KB burst in frame 1 made the LayerNorm part
+//           8.4k clocks longer: the CU's load path, not the latency, bounds it);
+//   role 1: the W3 fragments of all nine taps (ci tile = wave & 3), the scatter GEMM, the other
+//           half of the gather.
+// Same sums in the same order as the one-group form.
+template <int ROLE, class Pre>
+DEV void lnc3_body_f32r(const float* __restrict__ dy, const float* __restrict__ act3,
+                        const float* __restrict__ stats, const float* __restrict__ gam,
+                        const float* __restrict__ w3t, const float* __restrict__ act2,
+                        float* __restrict__ dact3, float* __restrict__ dact2, float* __restrict__ slab,
+                        int N, int fpw, int wg, char* __restrict__ lds, Pre&& pre) {
   using F = Frag<float>;
   typedef F::vec V;
   constexpr int KS = F::KSTEP, NKO = OC3 / KS, LD3 = Lnc3F32::LD3;
   constexpr int NGI = (P2 * 16 + 511) / 512;  // gather items per thread
-  constexpr int NT0 = 5;                      // taps of the first half
+  constexpr bool LN = ROLE == 0;
   float* zs = reinterpret_cast<float*>(lds);
   float* d3s = reinterpret_cast<float*>(lds + Lnc3F32::D3);
   float (*red)[2] = reinterpret_cast<float (*)[2]>(lds + Lnc3F32::RED);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const bool ln = wave < 4;  // waves 0..3: the LayerNorm features
   const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = 4 * (lane >> 4);
   const int j0 = 256 * (wave & 3) + 4 * lane, p0 = j0 >> 6, c0 = j0 & 63;
-  const int ct = wave & 3, th = wave >> 2;  // Z: ci tile, tap half
+  const int ct = wave & 3;  // Z: ci tile
   f32x4 ndy = f32x4{0.f, 0.f, 0.f, 0.f};
   float nx[4] = {0.f, 0.f, 0.f, 0.f}, nm = 0.f, nr = 0.f, na[NGI][4];
   auto fetch = [&](int f) {
-    if (ln) {
+    if constexpr (LN) {
       ndy = *reinterpret_cast<const f32x4*>(dy + (size_t)f * FLAT + j0);
       load4(act3 + (size_t)f * FLAT + j0, nx);
       nm = stats[2 * f];
@@ -302,69 +310,53 @@ DEV void lnc3_body_f32(const float* __restrict__ dy, const float* __restrict__ a
   };
   if (f0 < f1) fetch(f0);
   float gm[4], dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
+  // W3 fragments of the nine taps (role 1), from the transposed copy w3t[tap*64 + ci][oc]
+  V wa[LN ? 1 : 9][NKO];
+  if constexpr (LN) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) gm[q] = gam[j0 + q];
-  // W3 fragments of this wave's taps, from the transposed copy w3t[tap*64 + ci][oc]
-  V wa[NT0][NKO];
+    for (int q = 0; q < 4; ++q) gm[q] = gam[j0 + q];
 #pragma unroll
-  for (int tt = 0; tt < NT0; ++tt) {
-    const int tap = min(NT0 * th + tt, 8);
+    for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(gm[q]));
+  } else {
 #pragma unroll
-    for (int ko = 0; ko < NKO; ++ko)
-      wa[tt][ko] = F::load(w3t + (size_t)(tap * OC2 + 16 * ct + (lane & 15)) * OC3 + ko * KS + kl);
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int ko = 0; ko < NKO; ++ko)
+        wa[tap][ko] = F::load(w3t + (size_t)(tap * OC2 + 16 * ct + (lane & 15)) * OC3 + ko * KS + kl);
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(gm[q]));
   for (int e = t; e < lc3::ZR / 4; e += 512)  // the Z tile's zero row
     *reinterpret_cast<f32x4*>(zs + P3 * lc3::ZR + 4 * e) = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Z^T for NT taps of this wave: the taps' accumulators side by side (MFMA e of every tap
-  // before e + 1); a lane stores four consecutive channels of one pixel per tap
-  auto zgemm = [&](auto ntc) {
-    constexpr int NT = decltype(ntc)::value;
-    V a[NKO];
-#pragma unroll
-    for (int ko = 0; ko < NKO; ++ko)
-      a[ko] = *reinterpret_cast<const V*>(d3s + (lane & 15) * LD3 + ko * KS + kl);
-    f32x4 acc[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ko = 0; ko < NKO; ++ko)
-#pragma unroll
-      for (int e = 0; e < F::NE; ++e)
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) acc[tt] = F::mma_e(e, wa[tt][ko], a[ko], acc[tt]);
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt)
-      *reinterpret_cast<f32x4*>(zs + (lane & 15) * lc3::ZR + (NT0 * th + tt) * OC2 + 16 * ct + kl) = acc[tt];
-  };
   for (int f = f0; f < f1; ++f) {
     __syncthreads();  // the previous frame's readers of Z / dact3 / red are done
-    float d[4], x[4], xh[4], am[NGI][4];
-    const float mean = nm, rstd = nr;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { d[q] = ndy[q]; x[q] = nx[q]; }
+    float am[NGI][4];
 #pragma unroll
     for (int r = 0; r < NGI; ++r)
 #pragma unroll
       for (int q = 0; q < 4; ++q) am[r][q] = na[r][q];
-    // ---- LayerNorm backward: the two per-frame sums ----
-    float s1 = 0.f, s2 = 0.f;
+    // ---- LayerNorm backward (role 0): the two per-frame sums, then dact3 ----
+    float d[4], x[4], xh[4];
+    const float mean = nm, rstd = nr;
+    if constexpr (LN) {
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      xh[q] = (x[q] - mean) * rstd;
-      const float gd = d[q] * gm[q];
-      s1 += gd;
-      s2 += gd * xh[q];
-    }
-    if (ln) {
+      for (int q = 0; q < 4; ++q) {
+        d[q] = ndy[q];
+        x[q] = nx[q];
+        xh[q] = (x[q] - mean) * rstd;
+        const float gd = d[q] * gm[q];
+        s1 += gd;
+        s2 += gd * xh[q];
+      }
       s1 = wave_sum(s1);
       s2 = wave_sum(s2);
       if (lane == 0) { red[wave][0] = s1; red[wave][1] = s2; }
     }
     __syncthreads();
     if (f + 1 < f1) fetch(f + 1);
-    if (ln) {
+    if constexpr (LN) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (f == f0 + 1 + k) pre(k);
       const float S1 = (red[0][0] + red[1][0] + red[2][0] + red[3][0]) * (1.f / FLAT);
       const float S2 = (red[0][1] + red[1][1] + red[2][1] + red[3][1]) * (1.f / FLAT);
       float o[4];
@@ -379,11 +371,27 @@ DEV void lnc3_body_f32(const float* __restrict__ dy, const float* __restrict__ a
       store4(d3s + p0 * LD3 + c0, o);
     }
     __syncthreads();
-    // ---- Z[p][tap][ci] = sum_oc dact3[p][oc] W3[oc][tap][ci] ----
-    if (th == 0)
-      zgemm(std::integral_constant<int, NT0>{});
-    else
-      zgemm(std::integral_constant<int, 9 - NT0>{});
+    // ---- Z[p][tap][ci] = sum_oc dact3[p][oc] W3[oc][tap][ci] (role 1): Z^T tiles, the nine
+    // taps' accumulators side by side (MFMA e of every tap before e + 1); a lane stores four
+    // consecutive channels of one pixel per tap ----
+    if constexpr (!LN) {
+      V a[NKO];
+#pragma unroll
+      for (int ko = 0; ko < NKO; ++ko)
+        a[ko] = *reinterpret_cast<const V*>(d3s + (lane & 15) * LD3 + ko * KS + kl);
+      f32x4 acc[9];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) acc[tap] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ko = 0; ko < NKO; ++ko)
+#pragma unroll
+        for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) acc[tap] = F::mma_e(e, wa[tap][ko], a[ko], acc[tap]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+        *reinterpret_cast<f32x4*>(zs + (lane & 15) * lc3::ZR + tap * OC2 + 16 * ct + kl) = acc[tap];
+    }
     __syncthreads();
     // ---- col2im gather in a fixed (kh, kw) order + conv2's ReLU mask -> dact2 ----
 #pragma unroll
@@ -411,8 +419,11 @@ DEV void lnc3_body_f32(const float* __restrict__ dy, const float* __restrict__ a
       }
     }
   }
-  // ---- gamma / beta partials -> slab [2][1024] ----
-  if (ln) {
+  if constexpr (LN) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (f1 - f0 < k + 2) pre(k);
+    // ---- gamma / beta partials -> slab [2][1024] ----
     *reinterpret_cast<f32x4*>(slab + (size_t)wg * 2 * FLAT + j0) = f32x4{dg[0], dg[1], dg[2], dg[3]};
     *reinterpret_cast<f32x4*>(slab + (size_t)wg * 2 * FLAT + FLAT + j0) = f32x4{db[0], db[1], db[2], db[3]};
   }
@@ -425,9 +436,12 @@ DEV void lnc3_body(const float* __restrict__ dy, const T* __restrict__ act3,
                    const T* __restrict__ act2, T* __restrict__ dact3,
                    T* __restrict__ dact2, float* __restrict__ slab, int N, int fpw, int wg,
                    char* __restrict__ lds) {
-  if constexpr (sizeof(T) == 4)
-    lnc3_body_f32(dy, act3, stats, gam, w3t, act2, dact3, dact2, slab, N, fpw, wg, lds);
-  else
+  if constexpr (sizeof(T) == 4) {
+    if (threadIdx.x < 256)
+      lnc3_body_f32r<0>(dy, act3, stats, gam, w3t, act2, dact3, dact2, slab, N, fpw, wg, lds, [](int) {});
+    else
+      lnc3_body_f32r<1>(dy, act3, stats, gam, w3t, act2, dact3, dact2, slab, N, fpw, wg, lds, [](int) {});
+  } else
     lnc3_body_g<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, slab, N, fpw, wg, lds);
 }
 
@@ -458,7 +472,32 @@ __global__ __launch_bounds__(lnc3_threads<T>()) void lnc3_conv12_bwd(
   static_assert(lnc3_threads<T>() == 256 * c12_groups<T>(), "one block shape for both bodies");
   constexpr int B1 = Lnc3Lds<T>::BYTES, B2 = C12BLds<T>::BYTES;
   __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
-  lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
-  __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
-  conv12_bwd_body<T>(x, w2, w2t, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds);
+  if constexpr (sizeof(T) == 4) {
+    // fp32: each 4-wave group runs its role of both bodies as one code path, so group A's W2
+    // fragments (loaded during the LayerNorm frames) and group B's W3 fragments / weight-gradient
+    // accumulators never share the register budget
+    const float* w3f = reinterpret_cast<const float*>(w3t);
+    const float* w2f = reinterpret_cast<const float*>(w2t);
+    const float* a3 = reinterpret_cast<const float*>(act3);
+    const float* a2 = reinterpret_cast<const float*>(act2);
+    float* d3 = reinterpret_cast<float*>(dact3);
+    float* d2 = reinterpret_cast<float*>(dact2);
+    Frag<float>::vec wb[4][OC2 / Frag<float>::KSTEP][2];
+    const int wg = (int)blockIdx.x;
+    if (threadIdx.x < 256) {
+      const int cls = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+      lnc3_body_f32r<0>(dy, a3, stats, gam, w3f, a2, d3, d2, ln_slab, N, fpw, wg, lds,
+                        [&](int k) { c12_load_w2(w2f, wb, cls, lane, k, k + 1); });
+      __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
+      conv12_bwd_body_f32<0>(x, w2f, d2, mask1, c1_slab, c1_slab_bias, N, fpw, wg, lds, wb, false);
+    } else {
+      lnc3_body_f32r<1>(dy, a3, stats, gam, w3f, a2, d3, d2, ln_slab, N, fpw, wg, lds, [](int) {});
+      __syncthreads();
+      conv12_bwd_body_f32<1>(x, w2f, d2, mask1, c1_slab, c1_slab_bias, N, fpw, wg, lds, wb, false);
+    }
+  } else {
+    lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
+    __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
+    conv12_bwd_body<T>(x, w2, w2t, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds);
+  }
 }

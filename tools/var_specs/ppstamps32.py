@@ -8,12 +8,12 @@ def S(i, t=0):
             "__builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); ")
 VARIANTS = {
     "ppst": [
-        (LN, "  const bool ln = wave < 4;  // waves 0..3: the LayerNorm features\n", "  const bool ln = wave < 4;  // waves 0..3: the LayerNorm features\n  " + S(61) + "\n"),
-        (LN, "  // ---- gamma / beta partials -> slab [2][1024] ----\n", "  " + S(62) + "\n  // ---- gamma / beta partials -> slab [2][1024] ----\n"),
-        (C, "namespace c1 {\nconstexpr int GRID", "__device__ long long g_pp[64];\nnamespace c1 {\nconstexpr int GRID"),
-        (C, "  if (grp == 0 && nF > 0) {\n    // W2", "  " + S(0) + "\n  if (grp == 0 && nF > 0) {\n    // W2"),
-        (C, "  if (grp == 1 && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();",
-            "  if (grp == 1 && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();\n  " + S(1)),
+        (LN, "  const int ct = wave & 3;  // Z: ci tile\n", "  const int ct = wave & 3;  // Z: ci tile\n  " + S(61) + S(63, 256) + "\n"),
+        (LN, "    for (int k = 0; k < 4; ++k)\n      if (f1 - f0 < k + 2) pre(k);\n", "    for (int k = 0; k < 4; ++k)\n      if (f1 - f0 < k + 2) pre(k);\n    " + S(62) + "\n"),
+        (C, "namespace c1 {\nconstexpr int GRID", "__device__ long long g_pp[80];\nnamespace c1 {\nconstexpr int GRID"),
+        (C, "  if (is_a && nF > 0 && load_w2) c12_load_w2(w2t, wb, wave, lane);", "  " + S(0) + "\n  if (is_a && nF > 0 && load_w2) c12_load_w2(w2t, wb, wave, lane);"),
+        (C, "  if (!is_a && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();",
+            "  if (!is_a && nF > 0) stage(-1, 0, f0, 0);\n  __syncthreads();\n  " + S(1)),
         (C, '      asm volatile("" : "+v"(sl));', '      asm volatile("" : "+v"(sl));\n      ' + S("2 + 6 * it")),
         (C, "        // the previous half's gather reads of the Z tile are done before it is overwritten",
             "        " + S("3 + 6 * it + 2 * hf") + "\n        // the previous half's gather reads of the Z tile are done before it is overwritten"),
@@ -24,6 +24,6 @@ VARIANTS = {
         (C, '      const int b = (it - 1) & 1;\n      const float* dyt = dyt_buf(b);', '      ' + S("40 + 2 * (it - 1)", 256) + '\n      const int b = (it - 1) & 1;\n      const float* dyt = dyt_buf(b);'),
         (C, "          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n      }\n  }\n}",
             "          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);\n      }\n  }\n  __syncthreads();\n  " + S(60)
-            + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("PP"); for (int q = 1; q < 63; ++q) if (q < 32 || (q >= 40 && q < 58) || q >= 60) printf(" %lld", g_pp[q] ? g_pp[q] - g_pp[0] : -1); printf("\\n"); }\n}'),
+            + '\n  if (blockIdx.x == 0 && threadIdx.x == 0) { printf("PP"); for (int q = 1; q < 64; ++q) if (q < 32 || (q >= 40 && q < 58) || q >= 60) printf(" %lld", g_pp[q] ? g_pp[q] - g_pp[0] : -1); printf("\\n"); }\n}'),
     ],
 }
