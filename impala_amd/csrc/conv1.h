@@ -638,8 +638,15 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       for (int fr = 0; fr < FMAX; ++fr)
         if (fr < nF) *reinterpret_cast<f32x4*>(ets + (fr * P3 + p) * LDE + 16 * wave + 4 * (lane >> 4)) = acc3[fr];
       __syncthreads();
-      for (int fr = wave; fr < nF; fr += 4)
-        ln_frame_epilogue<T>(ets + fr * P3 * LDE, LDE, f0 + fr, lane, lk, c3.act3, c3.y, c3.stats);
+      // frames wave and wave + 4 (FMAX <= 8) in one interleaved pass
+      static_assert(FMAX <= 8, "two frames per wave");
+      if (wave + 4 < nF) {
+        const int fr2[2] = {f0 + wave, f0 + wave + 4};
+        ln_frames_epilogue<T, 2>(ets + wave * P3 * LDE, 4 * P3 * LDE, LDE, fr2, lane, lk, c3.act3, c3.y, c3.stats);
+      } else if (wave < nF) {
+        const int fr1[1] = {f0 + wave};
+        ln_frames_epilogue<T, 1>(ets + wave * P3 * LDE, 0, LDE, fr1, lane, lk, c3.act3, c3.y, c3.stats);
+      }
     }
   }
 }

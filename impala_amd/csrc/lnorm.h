@@ -65,3 +65,55 @@ DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const 
     stats[2 * frame + 1] = rstd;
   }
 }
+
+// M frames of one wavefront at once (the fp32 forward tail: 5 frames on 4 waves), each with
+// exactly the arithmetic of ln_frame_epilogue; the M independent reduction chains interleave.
+template <typename T, int M>
+DEV void ln_frames_epilogue(const float* et, int fstride, int ldt, const int (&frame)[M], int lane,
+                            const LnLane& k, T* act3, T* y, float* stats) {
+  using namespace net;
+  const int p = lane >> 2, c0 = (lane & 3) * 16;
+  float v[M][16], mean[M], rstd[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float* src = et + m * fstride + p * ldt + c0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[m][i] = fmaxf(src[i] + k.b[i], 0.f);
+  }
+  float sum[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    sum[m] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sum[m] += v[m][i];
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) mean[m] = wave_sum(sum[m]) * (1.f / FLAT);
+  float q[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    q[m] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) q[m] += (v[m][i] - mean[m]) * (v[m][i] - mean[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) rstd[m] = 1.f / sqrtf(wave_sum(q[m]) * (1.f / FLAT) + LN_EPS);
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const size_t o = (size_t)frame[m] * FLAT + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      float yy[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        yy[c] = (v[m][i + c] - mean[m]) * rstd[m] * k.g[i + c] + k.e[i + c];
+      store4(act3 + o + i, v[m] + i);
+      store4(y + o + i, yy);
+    }
+    if (lane == 0) {
+      stats[2 * frame[m]] = mean[m];
+      stats[2 * frame[m] + 1] = rstd[m];
+    }
+  }
+}
+
