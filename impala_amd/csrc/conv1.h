@@ -876,7 +876,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   // keeps each group's loop-carried registers (A: the W2 fragments; B: the accumulators) apart
   if (is_a) {
     for (int it = 0; it < nF; ++it) {
-      const int f = f0 + it, b = it & 1;
+      const int b = it & 1;
       // the gather's lane offsets recomputed per frame (not hoisted out of the loop as ~50 live
       // VGPRs)
       int sl = slot;
