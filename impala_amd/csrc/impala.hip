@@ -740,9 +740,10 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->n_red_wg = 11 + (OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT + HID * FLAT +
                       HID + HEADS * HID + HEADS) / 4 / 16;
   h->sph.S = h->n_loss_wg;  // heads weight-gradient partials: one slab per head workgroup
-  // FC weight-gradient splits: 96 workgroups for bf16; fp32 256 (fc_bwd 23.4 -> 21.0 us, the
-  // reduction +0.5 us; 384: 23.3 us, tools/var_specs/fc32b.py)
-  h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), h->bf16 ? 96 : 256);
+  // FC weight-gradient splits: 96 workgroups for bf16; fp32 128 (8 splits: fc_bwd 20.3 us and
+  // the reduction 7.55 against 20.7 / 7.75 for 256 workgroups, 27.8 us for 64;
+  // tools/var_specs/{fc32b,spfc32}.py)
+  h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), h->bf16 ? 96 : 128);
   // one-split FC weight gradient written straight into the canonical gradient (opt-in,
   // IMPALA_FC_DIRECT=1, up to 8192 frames): it drops the 6.3 MB FC slab and 256 reduction
   // workgroups, but the one-split GEMM is latency-bound on its per-CU load concurrency and the
