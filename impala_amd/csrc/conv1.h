@@ -129,25 +129,57 @@ DEV void c1_stash_frame_rot(T* img, int tid, const uint4 v[3]) {
 // forward: act1[n][p][oc] = relu(sum W'[oc][k'] s2d * 1/255 + b1), weights in registers;
 // optionally the ReLU bit mask mask[n][p] (bit oc = act1 > 0) for the fused backward.
 // ---------------------------------------------------------------------------------------
+// W1 as bf16 conv1 A fragments (bf16 fragment layout: 8 consecutive k per lane), rows
+// oc = 16 i + (lane & 15): bf16 W1 as is; fp32 W1 split exactly into three bf16 terms
+// x = hi + mid + lo (round-to-nearest 8-bit pieces of a 24-bit significand: every product with
+// an image byte, exact in bf16, is exact in the fp32 accumulator, so the three MFMA passes
+// compute the fp32 products).  Shared by both conv1 forward kernels (bitwise-equal act1).
+template <typename T>
+DEV void c1_load_w1(const T* __restrict__ w1, int lane,
+                    Frag<__bf16>::vec (&wa)[2][K1 / Frag<__bf16>::KSTEP][sizeof(T) == 4 ? 3 : 1]) {
+  using FB = Frag<__bf16>;
+  constexpr int NKB = K1 / FB::KSTEP;
+  const int klb = FB::KPL * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      const T* src = w1 + (16 * i + (lane & 15)) * K1 + kb * FB::KSTEP + klb;
+      if constexpr (sizeof(T) == 2) {
+        wa[i][kb][0] = FB::load(src);
+      } else {
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(src), u1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float xv = c < 4 ? u0[c] : u1[c - 4];
+          const __bf16 h = (__bf16)xv;
+          const float r1 = xv - (float)h;
+          const __bf16 m = (__bf16)r1;
+          wa[i][kb][0][c] = h;
+          wa[i][kb][1][c] = m;
+          wa[i][kb][2][c] = (__bf16)(r1 - (float)m);
+        }
+      }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__ x,
                                                      const T* __restrict__ w,  // [32][192] k'
                                                      const float* __restrict__ bias,
                                                      T* __restrict__ out,
                                                      uint32_t* __restrict__ mask, int N) {
-  using F = Frag<T>;
-  typedef typename F::vec V;
-  constexpr int LDI = c1::L<T>::LDI;
-  constexpr int NKS = K1 / F::KSTEP;  // 6 (bf16) / 12 (f32)
-  __shared__ __attribute__((aligned(16))) T img[c1::GRID * c1::GRID * LDI];
+  // the image in LDS as bf16 (exact bytes) in both modes; conv1 on bf16 MFMAs (fp32: three
+  // exact passes, c1_load_w1)
+  using FB = Frag<__bf16>;
+  typedef FB::vec VB;
+  constexpr int LDI = c1::L<__bf16>::LDI;
+  constexpr int NKB = K1 / FB::KSTEP, NT = sizeof(T) == 4 ? 3 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 img[c1::GRID * c1::GRID * LDI];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kl = F::KPL * (lane >> 4);
-  V wa[2][NKS];  // A fragments: rows oc = 16*i + (lane & 15), all of K
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-      wa[i][ks] = F::load(w + (16 * i + (lane & 15)) * K1 + ks * F::KSTEP + kl);
+  const int kl = FB::KPL * (lane >> 4);
+  VB wa[2][NKB][NT];  // A fragments: rows oc = 16*i + (lane & 15), all of K
+  c1_load_w1<T>(w, lane, wa);
   float bb[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -159,7 +191,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
   c1_load_frame<T>(x + (size_t)f * IMG, tid, nv);
   for (; f < N; f += gridDim.x) {
     __syncthreads();  // previous frame's readers are done
-    c1_stash_frame<T>(img, tid, nv);
+    c1_stash_frame<__bf16>(img, tid, nv);
     __syncthreads();
     if (f + (int)gridDim.x < N) c1_load_frame<T>(x + (size_t)(f + gridDim.x) * IMG, tid, nv);
     for (int tile = wave; tile < 15; tile += 4) {  // 15 x 16 pixel tiles cover the 225 pixels
@@ -167,14 +199,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
       const int base = c1_row(p, 0) * LDI;
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int k = ks * F::KSTEP + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
+      for (int kb = 0; kb < NKB; ++kb) {
+        const int k = kb * FB::KSTEP + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
         const int off = ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
-        const V b = *reinterpret_cast<const V*>(img + base + off);
+        const VB b = *reinterpret_cast<const VB*>(img + base + off);
 #pragma unroll
-        for (int e = 0; e < F::NE; ++e) {
-          acc[0] = F::mma_e(e, wa[0][ks], b, acc[0]);
-          acc[1] = F::mma_e(e, wa[1][ks], b, acc[1]);
+        for (int tm = 0; tm < NT; ++tm) {
+          acc[0] = FB::mma(wa[0][kb][tm], b, acc[0]);
+          acc[1] = FB::mma(wa[1][kb][tm], b, acc[1]);
         }
       }
       const int pc = tile * 16 + (lane & 15);
@@ -268,8 +300,15 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   T* a2s = smem + G * GSZ;
   const bool tail = c3.act3 != nullptr;
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-  T* img = smem + grp * GSZ;
-  T* a1s = img + IMGSZ;
+  // the image is bf16 in both modes: the bytes 0..255 are exact in bf16.  fp32 runs conv1 as
+  // three exact bf16 MFMA passes (W1 split hi + mid + lo, below) over it.
+  using FB = Frag<__bf16>;
+  typedef FB::vec VB;
+  constexpr int ILDI = c1::LF<__bf16>::LDI, NKB1 = K1 / FB::KSTEP;
+  static_assert(sizeof(T) == 4 || ILDI == LDI, "bf16 image layout");
+  __bf16* img = reinterpret_cast<__bf16*>(smem + grp * GSZ);
+  T* a1s = smem + grp * GSZ + IMGSZ;
+  const int klb = FB::KPL * (lane >> 4);
   const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = KPL * (lane >> 4);
   uint4 nv[3];
@@ -291,7 +330,11 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // Weights: every wave needs all of W1 and its 16 rows of W2 as MFMA fragments.  For bf16
   // both are staged once per workgroup through LDS with coalesced 16-byte loads (76 KB per
   // workgroup instead of 8 waves x 28 KB of fragment loads through the CU's L2 port).
-  V wa1[2][NKS1];  // conv1: rows oc = 16 i + (lane & 15), all of K
+  // conv1 A fragments, rows oc = 16 i + (lane & 15), all of K: bf16 W1 (bf16 mode) or fp32 W1
+  // split exactly into three bf16 terms x = hi + mid + lo (fp32 mode: round-to-nearest 8-bit
+  // pieces of a 24-bit significand; each product with an image byte is exact in the fp32
+  // accumulator, so the three passes give the fp32 products)
+  VB wa1[2][NKB1][sizeof(T) == 4 ? 3 : 1];
   const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
   // bf16: this wave's W2 rows in registers for the whole frame run (64 VGPRs).  fp32 reads its
   // fragments from L2 per k-step: holding all 128 VGPRs of them made the kernel 3.5 us slower
@@ -327,17 +370,14 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int ks = 0; ks < NKS1; ++ks)
-        wa1[i][ks] = *reinterpret_cast<const V*>(w1s + (16 * i + (lane & 15)) * LW1 + ks * KS + kl);
+        wa1[i][ks][0] = *reinterpret_cast<const V*>(w1s + (16 * i + (lane & 15)) * LW1 + ks * KS + kl);
 #pragma unroll
     for (int ks = 0; ks < NKS2; ++ks)
       wa2[ks] = *reinterpret_cast<const V*>(w2s + (16 * wave + (lane & 15)) * LW2 + ks * KS + kl);
     __syncthreads();  // the staging area becomes the frame tiles
   } else {
-    // fp32: 16-byte fragment loads straight from L2, issued once for the frame run
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int ks = 0; ks < NKS1; ++ks) wa1[i][ks] = F::load(w1 + (16 * i + (lane & 15)) * K1 + ks * KS + kl);
+    // fp32: W1 straight from L2, split into its three bf16 terms (c1_load_w1)
+    c1_load_w1<T>(w1, lane, wa1);
   }
   // consume the bias loads here: waits for them placed inside the loop would (merged over the
   // back-edge) also stall every iteration on its in-flight frame prefetch
@@ -352,10 +392,10 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // (scale, bias, ReLU, bf16 pack, mask bits, stores) runs on the VALU.
   int c1base[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) c1base[t] = (min(wave + 4 * t, 14) * c1::GRID + (lane & 15)) * LDI;
-  auto c1_off = [&](int ks) {
-    const int k = ks * KS + kl, tap = k / c1::CH, ch = k - tap * c1::CH;
-    return ((tap >> 1) * c1::GRID + (tap & 1)) * LDI + ch;
+  for (int t = 0; t < 4; ++t) c1base[t] = (min(wave + 4 * t, 14) * c1::GRID + (lane & 15)) * ILDI;
+  auto c1_off = [&](int kb) {  // bf16 fragment k-block kb: this lane's 8 k = 8 channels of one tap
+    const int k = kb * FB::KSTEP + klb, tap = k / c1::CH, ch = k - tap * c1::CH;
+    return ((tap >> 1) * c1::GRID + (tap & 1)) * ILDI + ch;
   };
   // conv2: 3 pixel tiles (3 accumulators), B fragments one k-step ahead
   // fp32: pixel tile 2 holds only pixels 32..35; they run on 4x4x1 blocks (see the conv2 loop),
@@ -382,22 +422,23 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   auto c1_mma = [&](f32x4 (&acc)[2][2], int t0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    V bq[2][2];
+    constexpr int NT = sizeof(T) == 4 ? 3 : 1;  // W1 terms
+    VB bq[2][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) bq[0][u] = *reinterpret_cast<const V*>(img + c1base[t0 + u] + c1_off(0));
+    for (int u = 0; u < 2; ++u) bq[0][u] = *reinterpret_cast<const VB*>(img + c1base[t0 + u] + c1_off(0));
 #pragma unroll
-    for (int ks = 0; ks < NKS1; ++ks) {
-      if (ks + 1 < NKS1) {
-        const int off = c1_off(ks + 1);
+    for (int kb = 0; kb < NKB1; ++kb) {
+      if (kb + 1 < NKB1) {
+        const int off = c1_off(kb + 1);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) bq[(ks + 1) & 1][u] = *reinterpret_cast<const V*>(img + c1base[t0 + u] + off);
+        for (int u = 0; u < 2; ++u) bq[(kb + 1) & 1][u] = *reinterpret_cast<const VB*>(img + c1base[t0 + u] + off);
       }
 #pragma unroll
-      for (int e = 0; e < F::NE; ++e)
+      for (int tm = 0; tm < NT; ++tm)
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          acc[u][0] = F::mma_e(e, wa1[0][ks], bq[ks & 1][u], acc[u][0]);
-          acc[u][1] = F::mma_e(e, wa1[1][ks], bq[ks & 1][u], acc[u][1]);
+          acc[u][0] = FB::mma(wa1[0][kb][tm], bq[kb & 1][u], acc[u][0]);
+          acc[u][1] = FB::mma(wa1[1][kb][tm], bq[kb & 1][u], acc[u][1]);
         }
     }
   };
@@ -440,7 +481,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   };
   // the group's first frame goes into the image now (the weight staging area is free), and the
   // second is fetched; every later frame is staged during the previous frame's conv2
-  if (f0 + grp < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
+  if (f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, tid, nv);
   if (f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, tid, nv);
   __syncthreads();
   for (int it = 0; it < n_it; ++it) {
@@ -500,7 +541,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         }
         if constexpr (!W2REG) __builtin_amdgcn_sched_barrier(0);
       }
-      if (f + G < f1) c1_stash_frame_rot<T, LDI>(img, tid, nv);
+      if (f + G < f1) c1_stash_frame_rot<__bf16, ILDI>(img, tid, nv);
       if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
       if constexpr (!W2REG) {
         // the 4x4x1 blocks: lane 16 g + 4 og + j holds act2[pixel 32 + j][oc 16 w + 4 og + reg]

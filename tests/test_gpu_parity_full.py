@@ -205,8 +205,17 @@ def test_step_gradients_and_params_match_oracle(B):
     for name in ("fp64", "native"):
         d = np.abs(hip["p"][0] - ys[name]["p"][0])
         assert d.max() <= 1e-6, (name, d.max())
+    # after 3 steps against the native oracle (another fp32 rounding path): Adam turns a
+    # rounding-level difference in a near-zero gradient element into an O(lr) move, so the
+    # bound is the launch-mode test's (tests/test_gpu_parity.py, IMPALA_FWD_FUSED=0): every
+    # parameter within two lr steps, all but 0.1 % within 1e-6.  (conv1 runs as three exact
+    # bf16 MFMA passes since round 3: its gradient is as close to float64 as before -- rel-L2
+    # 1.05e-6 at C2 -- but 29 of the 344,496 parameters land 1e-6..2.1e-5 from this oracle)
     d3 = np.abs(hip["p"][1] - ys["native"]["p"][1])
-    assert d3.max() <= 1e-6, d3.max()
+    print(f"B={B} params step 3 vs native: max {d3.max():.2e}, frac > 1e-6 {np.mean(d3 > 1e-6):.2e}, "
+          f"n > 1e-6 {int(np.sum(d3 > 1e-6))}")
+    assert d3.max() <= 2e-4, d3.max()
+    assert np.mean(d3 > 1e-6) <= 1e-3, np.mean(d3 > 1e-6)
     # against torch's default fp32 (its conv gradients off by ~1e-3 at C2): Adam's first
     # steps move a parameter by ~lr * sign(m), so a gradient element near 0 can flip: one lr
     # step everywhere; away from 1e-6 no more often than fp32 itself is away from float64
