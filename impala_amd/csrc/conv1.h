@@ -1040,64 +1040,98 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     stage(nF > 0 ? f0 : -1, 0, nF > 1 ? f0 + 1 : -1, 1);
     __syncthreads();
     for (int it = 1; it <= nF; ++it) {
-      // ---- conv1 weight gradient of frame it - 1 over its 15 x 16 pixel rows: A = dY1 (k =
-      // pixel), B = the image bytes of cell (iy + ty, ix + tx), channel n, converted to fp32:
-      // k-step iy, lane group g holds ix = 4 g .. 4 g + 3 = one 32-bit word (two aligned words
-      // funnel-shifted by tx bytes) ----
+      // ---- conv1 weight gradient of frame it - 1, as three exact bf16 MFMA passes: A = dY1
+      // (rows oc, k = pixel) split exactly into hi + mid + lo bf16 terms (truncation: the top 8
+      // significand bits of x, then of the remainder, then the <= 8 bits left -- each term's fp32
+      // bits are its bf16 in the high half), B = the image bytes of cell (iy + ty, ix + tx),
+      // channel n (exact in bf16).  Every product is the fp32 product; 16x16x32 bf16 MFMAs take
+      // half the cycles of 16x16x4 f32 for 8x the K.  k-block kb = pixel rows 32 kb .. 32 kb + 31
+      // (image rows 2 kb, 2 kb + 1); lane group g holds pixels 8 g .. 8 g + 7 of it: dY1 rows
+      // (clamped to the 240 that exist) and 8 consecutive image bytes (funnel-shifted by tx).
+      // The 16 pixels of image row 15 (kb = 7, g >= 2) are padding: their B operand is zero. ----
       const int b = (it - 1) & 1;
       const float* dyt = dyt_buf(b);
       const uint8_t* img = img_buf(b);
-      auto load_a = [&](int kk, V* a) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = lds_frag_k(dyt + kk * LDX + 16 * i, LDX, lane);
+      using FB = Frag<__bf16>;
+      typedef FB::vec VB;
+      constexpr int NKB = 8;
+      const int g = lane >> 4, col = lane & 15;
+      struct Raw {
+        float a[2][8];     // dY1 of oc 16 i + col, pixels 8 g .. 8 g + 7
+        uint32_t w[3][3];  // image dwords at X = 8 (g & 1) + {0, 4, 8}, channel tile j
       };
-      const uint8_t* ib = img + (ty * c1::CH + (lane & 15)) * XP + 4 * (lane >> 4);
-      auto load_b = [&](int kk, uint32_t* raw) {
+      auto load = [&](int kb, Raw& r) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int pr = min(32 * kb + 8 * g + c, L::NROW - 1);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) r.a[i][c] = dyt[pr * LDX + 16 * i + col];
+        }
+        const int Y = min(2 * kb + (g >> 1) + ty, c1::GRID - 1);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const uint32_t* wp = reinterpret_cast<const uint32_t*>(ib + ((kk / KS) * c1::CH + 16 * j) * XP);
-          raw[2 * j] = wp[0];
-          raw[2 * j + 1] = wp[1];
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + (Y * c1::CH + 16 * j + col) * XP + 8 * (g & 1));
+#pragma unroll
+          for (int q = 0; q < 3; ++q) r.w[j][q] = wp[q];
         }
       };
-      constexpr int NKK = L::NROW / KS;
-      V fa[2][2];
-      uint32_t raw[2][6];
-      load_a(0, fa[0]);
-      load_b(0, raw[0]);
+      // the high halves of two fp32 words as a bf16 pair (x0 low, x1 high)
+      auto hi2 = [](uint32_t x0, uint32_t x1) { return __builtin_amdgcn_perm(x1, x0, 0x07060302u); };
+      Raw rr[2];
+      load(0, rr[0]);
 #pragma unroll
-      for (int s2 = 0; s2 < NKK; ++s2) {
-        // one scheduling region per k-step: the next step's reads ahead of this step's MFMAs,
-        // the bytes converted at the top of the step that uses them; MFMA order (j, e, i)
-        V fb[3];
+      for (int kb = 0; kb < NKB; ++kb) {
+        const Raw& r = rr[kb & 1];
+        // A: the three terms of the 16 dY1 values
+        VB fa[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          uint32_t th[4], tm[4], tl[4];
+#pragma unroll
+          for (int c = 0; c < 8; c += 2) {
+            uint32_t x[2], r1[2], r2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              x[u] = __builtin_bit_cast(uint32_t, r.a[i][c + u]);
+              const float f1 = r.a[i][c + u] - __builtin_bit_cast(float, x[u] & 0xffff0000u);
+              r1[u] = __builtin_bit_cast(uint32_t, f1);
+              r2[u] = __builtin_bit_cast(uint32_t, f1 - __builtin_bit_cast(float, r1[u] & 0xffff0000u));
+            }
+            th[c / 2] = hi2(x[0], x[1]);
+            tm[c / 2] = hi2(r1[0], r1[1]);
+            tl[c / 2] = hi2(r2[0], r2[1]);
+          }
+          fa[i][0] = __builtin_bit_cast(VB, th);
+          fa[i][1] = __builtin_bit_cast(VB, tm);
+          fa[i][2] = __builtin_bit_cast(VB, tl);
+        }
+        // B: 8 image bytes per channel tile -> bf16 (exact), zero on the padding row
+        const bool pad = kb == NKB - 1 && g >= 2;
+        VB fb[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const uint32_t w = __builtin_amdgcn_alignbyte(raw[s2 & 1][2 * j + 1], raw[s2 & 1][2 * j], tx);
-          fb[j] = V{(float)(w & 255u), (float)((w >> 8) & 255u), (float)((w >> 16) & 255u), (float)(w >> 24)};
+          const uint32_t w0 = __builtin_amdgcn_alignbyte(r.w[j][1], r.w[j][0], tx);
+          const uint32_t w1 = __builtin_amdgcn_alignbyte(r.w[j][2], r.w[j][1], tx);
+          uint32_t t[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t w = h ? w1 : w0;
+            const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)(w & 255u));
+            const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> 8) & 255u));
+            const uint32_t f2 = __builtin_bit_cast(uint32_t, (float)((w >> 16) & 255u));
+            const uint32_t f3 = __builtin_bit_cast(uint32_t, (float)(w >> 24));
+            t[2 * h] = pad ? 0u : hi2(f0, f1);
+            t[2 * h + 1] = pad ? 0u : hi2(f2, f3);
+          }
+          fb[j] = __builtin_bit_cast(VB, t);
         }
-        if (s2 + 1 < NKK) {
-          load_a((s2 + 1) * KS, fa[(s2 + 1) & 1]);
-          load_b((s2 + 1) * KS, raw[(s2 + 1) & 1]);
-        }
+        if (kb + 1 < NKB) load(kb + 1, rr[(kb + 1) & 1]);
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int tm = 0; tm < 3; ++tm)
 #pragma unroll
-          for (int e = 0; e < F::NE; ++e)
+          for (int j = 0; j < 3; ++j)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) acc[i][j] = F::mma_e(e, fa[s2 & 1][i], fb[j], acc[i][j]);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU: the j = 0 word + conversions
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU: j = 1, 2, addresses
-        }
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        }
-        __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < 2; ++i) acc[i][j] = FB::mma(fa[i][tm], fb[j], acc[i][j]);
       }
       stage(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1);
       __syncthreads();
