@@ -134,6 +134,36 @@ DEV void c1_stash_frame_rot(T* img, int tid, const uint4 v[3]) {
 // x = hi + mid + lo (round-to-nearest 8-bit pieces of a 24-bit significand: every product with
 // an image byte, exact in bf16, is exact in the fp32 accumulator, so the three MFMA passes
 // compute the fp32 products).  Shared by both conv1 forward kernels (bitwise-equal act1).
+DEV void c1_split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+// fp32 W1 staged once per workgroup as its three bf16 planes (plane p: [32][C1W_LD] bf16, rows
+// padded by 16: conflict-free 16-byte fragment reads), instead of every wave loading all of W1
+// (4 x 24.6 KB through the CU's load path) and splitting it
+constexpr int C1W_LD = K1 + 16;
+DEV void c1_stage_w1_f32(const float* __restrict__ w1, __bf16* __restrict__ planes, int tid) {
+  constexpr int NV = OC1 * K1 / 4;  // float4s
+#pragma unroll
+  for (int i = 0; i < NV / 256; ++i) {
+    const int e = tid + 256 * i, r = e / (K1 / 4), c = (e % (K1 / 4)) * 4;
+    const f32x4 u = *reinterpret_cast<const f32x4*>(w1 + (size_t)e * 4);
+    bf16x4 o[3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __bf16 h, m, l;
+      c1_split3(u[q], h, m, l);
+      o[0][q] = h;
+      o[1][q] = m;
+      o[2][q] = l;
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x4*>(planes + (p * OC1 + r) * C1W_LD + c) = o[p];
+  }
+}
+
 template <typename T>
 DEV void c1_load_w1(const T* __restrict__ w1, int lane,
                     Frag<__bf16>::vec (&wa)[2][K1 / Frag<__bf16>::KSTEP][sizeof(T) == 4 ? 3 : 1]) {
@@ -151,13 +181,11 @@ DEV void c1_load_w1(const T* __restrict__ w1, int lane,
         const f32x4 u0 = *reinterpret_cast<const f32x4*>(src), u1 = *reinterpret_cast<const f32x4*>(src + 4);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const float xv = c < 4 ? u0[c] : u1[c - 4];
-          const __bf16 h = (__bf16)xv;
-          const float r1 = xv - (float)h;
-          const __bf16 m = (__bf16)r1;
+          __bf16 h, m, l;
+          c1_split3(c < 4 ? u0[c] : u1[c - 4], h, m, l);
           wa[i][kb][0][c] = h;
           wa[i][kb][1][c] = m;
-          wa[i][kb][2][c] = (__bf16)(r1 - (float)m);
+          wa[i][kb][2][c] = l;
         }
       }
     }
@@ -376,8 +404,21 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       wa2[ks] = *reinterpret_cast<const V*>(w2s + (16 * wave + (lane & 15)) * LW2 + ks * KS + kl);
     __syncthreads();  // the staging area becomes the frame tiles
   } else {
-    // fp32: W1 straight from L2, split into its three bf16 terms (c1_load_w1)
-    c1_load_w1<T>(w1, lane, wa1);
+    // fp32: W1 staged once as its three bf16 planes (c1_stage_w1_f32, the split of c1_load_w1),
+    // the fragments read from LDS
+    static_assert(3 * OC1 * C1W_LD * 2 <= (int)sizeof(T) * G * GSZ, "W1 plane staging");
+    __bf16* w1p = reinterpret_cast<__bf16*>(smem);
+    c1_stage_w1_f32(reinterpret_cast<const float*>(w1), w1p, (int)threadIdx.x);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kb = 0; kb < NKB1; ++kb)
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm)
+          wa1[i][kb][tm] = *reinterpret_cast<const VB*>(w1p + (tm * OC1 + 16 * i + (lane & 15)) * C1W_LD +
+                                                        kb * FB::KSTEP + klb);
+    __syncthreads();  // the staging area becomes the frame tiles
   }
   // consume the bias loads here: waits for them placed inside the loop would (merged over the
   // back-edge) also stall every iteration on its in-flight frame prefetch
