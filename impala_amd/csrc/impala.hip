@@ -140,6 +140,11 @@ struct impala_learner {
   // tiles only start on CUs the conv workgroups free, all at the end (step 0.1202 vs 0.1180 ms)
   bool fwd_chain = false;
   unsigned* chain_flags = nullptr;  // [N] one word per conv workgroup
+  int fc_splitk = 0;                // fp32 FC forward: 1 = K split over workgroups (in-launch
+                                    // combine), 2 = K split over the waves of a workgroup
+  int fcsk_pub = 1;                 // its publish form (ops.h fc_fwd_splitk_f32)
+  float* fcsk_slab = nullptr;       // [tiles][4 splits][64 x 80] fp32 partials
+  unsigned* fcsk_cnt = nullptr;     // [tiles] ticket counters (grow by 4 per launch)
   unsigned chain_epoch = 0;
   Split sp1, sp2, sp3, spfc, sph;
   int n_ln_wg = 0, ln_fpw = 2, n_loss_wg = 0, S_seg = 32, n_red_wg = 0, n_adam_wg = 256;
@@ -308,7 +313,23 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
                         dim3(persist_grid(h, cdiv((long)n * P3, 64))), dim3(256), st, op, 1))
       return r;
   }
-  {
+  if (sizeof(T) == 4 && h->fc_splitk == 2) {
+    FcFwd<float> op{n, (const float*)(sw + sh.wfc), vv + Vecs::bfc, (const float*)h->y, h->zg,
+                    (float*)h->h};
+    const int grid = (HID / fcwk::ROWS) * cdiv(n, fcwk::COLS);
+    if (int r = klaunch(h, K_FC_FWD, "fc_fwd_wsplit", fc_fwd_wsplit_f32, dim3(grid), dim3(256), st, op))
+      return r;
+  } else if (sizeof(T) == 4 && h->fc_splitk == 1) {
+    // fp32: 64 x 80 tiles, K split 4 ways, combined by each tile's last split (ops.h)
+    FcFwd<float> op{n, (const float*)(sw + sh.wfc), vv + Vecs::bfc, (const float*)h->y, h->zg,
+                    (float*)h->h};
+    const int grid = (HID / fcsk::ROWS) * cdiv(n, fcsk::COLS) * fcsk::NS;
+    auto kern = h->fcsk_pub == 0 ? fc_fwd_splitk_f32<0>
+                : h->fcsk_pub == 2 ? fc_fwd_splitk_f32<2> : fc_fwd_splitk_f32<1>;
+    if (int r = klaunch(h, K_FC_FWD, "fc_fwd_splitk", kern, dim3(grid), dim3(256), st, op,
+                        h->fcsk_slab, h->fcsk_cnt))
+      return r;
+  } else {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->zg, (T*)h->h};
     // 32 x 32 tiles: 320 workgroups (5.9 vs 6.7 us for 64 x 32, tools/var_specs/fcfwd.py)
     if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 32, 32, BK(256), 2, 2, FcFwd<T>>,
@@ -801,6 +822,10 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t o_gran = take((size_t)h->n_red_wg * 8);  // fused update granules (upper bound)
   const size_t o_fsync = take(16);                       // epoch counter, fault word
   const size_t o_chain = take((size_t)N * 4);            // forward-chain producer flags
+  if (const char* e = std::getenv("IMPALA_FC_SPLITK")) h->fc_splitk = es == 4 ? std::atoi(e) : 0;
+  const size_t fcsk_tiles = h->fc_splitk == 1 ? (size_t)(HID / fcsk::ROWS) * cdiv(N, fcsk::COLS) : 0;
+  const size_t o_fcsk = take(fcsk_tiles * fcsk::NS * fcsk::PART * 4);  // opt-in split-K partials
+  const size_t o_fcskc = take(fcsk_tiles * 4);
   h->ws_bytes = off;
   hipError_t e = hipMalloc(&h->ws, off);
   if (e != hipSuccess) {
@@ -833,6 +858,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->fsync.epoch_ctr = (unsigned*)(w + o_fsync);
   h->fsync.fault = (unsigned*)(w + o_fsync + 4);
   h->chain_flags = (unsigned*)(w + o_chain);
+  h->fcsk_slab = (float*)(w + o_fcsk);
+  h->fcsk_cnt = (unsigned*)(w + o_fcskc);
+  if (const char* e = std::getenv("IMPALA_FCSK_PUB")) h->fcsk_pub = std::atoi(e);
   if (const char* rm = std::getenv("IMPALA_RED_MODE")) h->red_mode = std::atoi(rm);
   if (const char* ff = std::getenv("IMPALA_FWD_FUSED")) h->fwd_fused = ff[0] != '0';
   if (const char* e = std::getenv("IMPALA_FC_MERGED")) h->fc_merged = e[0] != '0';

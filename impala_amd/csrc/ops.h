@@ -100,6 +100,207 @@ template <typename T> struct FcFwd {
   }
 };
 
+// fp32 FC forward as a split-K GEMM with its combine in the same launch.  The 32 x 32 tile
+// kernel (320 workgroups, whole K each) streams 256 KB per workgroup for 1 M MACs and leaves
+// 64 CUs with a second tile; here a workgroup owns a 64 (hidden) x 80 (frame) tile over one
+// quarter of K: 144 KB streamed for 1.3 M MACs, and 256 workgroups at B*T = 1280 (one per CU).
+// Wave w holds rows 16w..16w+15 of the tile as 16 float4 A fragments in registers; the tile's
+// 80 frames x 256 k of y sit in LDS.  Each workgroup stores its fp32 partial (20 KB, in the
+// accumulator layout) and takes a ticket on its tile's counter; the one that draws the 4th
+// ticket sums the four partials in split order ((p0 + p1) + p2) + p3 -- whichever arrives
+// last, so the result is deterministic -- and runs FcFwd's bias + GELU epilogue.  Hand-off:
+// cdna_hip_programming.md's split-K recipe (plain slab stores, agent release before the
+// ticket, agent acquire in the reducer).  The counters only ever grow by 4 per tile per launch
+// (zeroed once at create), so no reset is needed.  The 4 splits and the 4 row tiles of a
+// column tile run on one XCD when the tile count allows (speed only, not correctness).
+namespace fcsk {
+constexpr int ROWS = 64, COLS = 80, NS = 4, KS = FLAT / NS, LDB = KS + 4, PART = ROWS * COLS;
+constexpr int NCF = COLS / 16, NKB = KS / 16;
+}  // namespace fcsk
+// PUB (publish form): 1 = write-through (sc1) slab stores and sc1 slab loads, no fences
+// (the default); 0 = plain stores, agent release before the ticket, agent acquire in the
+// reducer; 2 = measurement knock-out (partials stored, no combine: wrong results).
+DEV void st_sc1(float* p, f32x4 v) {
+  const unsigned long long lo = __builtin_bit_cast(unsigned long long, float2{v[0], v[1]});
+  const unsigned long long hi = __builtin_bit_cast(unsigned long long, float2{v[2], v[3]});
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p) + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV f32x4 ld_sc1(const float* p) {
+  auto* q = reinterpret_cast<unsigned long long*>(const_cast<float*>(p));
+  const float2 lo = __builtin_bit_cast(float2, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const float2 hi = __builtin_bit_cast(float2, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+template <int PUB>
+__global__ __launch_bounds__(256) void fc_fwd_splitk_f32(const FcFwd<float> op, float* __restrict__ slab,
+                                                         unsigned* __restrict__ cnt) {
+  using namespace fcsk;
+  __shared__ __attribute__((aligned(16))) float sb[COLS * LDB + 4];
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x, n_tiles = nb / NS;
+  int tile, s;
+  if (n_tiles % 8 == 0) {
+    const int x = b % 8, l = b / 8;
+    tile = x * (n_tiles / 8) + l / NS;
+    s = l % NS;
+  } else {
+    tile = b / NS;
+    s = b % NS;
+  }
+  constexpr int NRT = HID / ROWS;
+  const int r0 = (tile % NRT) * ROWS, c0 = (tile / NRT) * COLS, k0 = s * KS;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // A fragments: row r0 + 16w + (lane & 15), k = k0 + 16 kb + 4 (lane >> 4) + e
+  f32x4 a[NKB];
+  const float* ap = op.w + (size_t)(r0 + wave * 16 + (lane & 15)) * FLAT + k0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) a[kb] = *reinterpret_cast<const f32x4*>(ap + kb * 16);
+  // y tile -> LDS: column (frame) rows of 256 k, padded by 4 floats (conflict-free b128 reads)
+#pragma unroll
+  for (int i = 0; i < COLS / 4; ++i) {
+    const int col = i * 4 + wave, k = lane * 4;
+    const int c = min(c0 + col, op.C - 1);  // frames past C: any valid row, results dropped
+    *reinterpret_cast<f32x4*>(sb + col * LDB + k) =
+        *reinterpret_cast<const f32x4*>(op.y + (size_t)c * FLAT + k0 + k);
+  }
+  __syncthreads();
+  f32x4 acc[NCF];
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf) acc[cf] = Frag<float>::zero();
+  const float* bp = sb + (lane & 15) * LDB + 4 * (lane >> 4);
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    f32x4 bv[NCF];
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf) bv[cf] = *reinterpret_cast<const f32x4*>(bp + cf * 16 * LDB + kb * 16);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int cf = 0; cf < NCF; ++cf) acc[cf] = Frag<float>::mma_e(e, a[kb], bv[cf], acc[cf]);
+  }
+  // publish this split's partial, take a ticket
+  float* tp = slab + (size_t)tile * NS * PART;
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf) {
+    float* dst = tp + (size_t)s * PART + ((wave * NCF + cf) * 64 + lane) * 4;
+    if constexpr (PUB == 1) st_sc1(dst, acc[cf]);
+    else *reinterpret_cast<f32x4*>(dst) = acc[cf];
+  }
+  if constexpr (PUB == 2) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* last = reinterpret_cast<int*>(sb + COLS * LDB);
+  if (tid == 0) {
+    if constexpr (PUB == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned old = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int is_last = (old % NS) == NS - 1;
+    if (PUB == 0 && is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *last = is_last;
+  }
+  __syncthreads();
+  if (!*last) return;
+  const int o = r0 + wave * 16 + 4 * (lane >> 4);
+  const auto ep = op.epi(o, 0);
+  // every partial load of the tile in flight at once (the own split's too: same bits as acc)
+  f32x4 p[NCF][NS];
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const float* src = tp + (size_t)q * PART + ((wave * NCF + cf) * 64 + lane) * 4;
+      p[cf][q] = PUB == 1 ? ld_sc1(src) : *reinterpret_cast<const f32x4*>(src);
+    }
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf) {
+    f32x4 v = p[cf][0] + p[cf][1];
+#pragma unroll
+    for (int q = 2; q < NS; ++q) v += p[cf][q];
+    const int c = c0 + cf * 16 + (lane & 15);
+    if (c < op.C) {
+      float vv[4] = {v[0], v[1], v[2], v[3]};
+      op.store(o, c, vv, ep);
+    }
+  }
+}
+
+// fp32 FC forward, K split over the 4 waves of a workgroup instead of over workgroups: a
+// workgroup owns 16 hidden x 80 frames over all of K (256 workgroups at B*T = 1280, one per
+// CU, 384 KB streamed each against 2 x 256 KB on the CUs that get two 32 x 32 tiles), wave w
+// takes k in [256 w, 256 w + 256) with its B fragments straight from global (no operand is
+// shared between the waves), and the four 16 x 80 partials meet in LDS, summed in wave order
+// ((w0 + w1) + w2) + w3 before FcFwd's bias + GELU epilogue.
+namespace fcwk {
+constexpr int ROWS = 16, COLS = 80, KW = FLAT / 4, NCF = COLS / 16, NKB = KW / 16, CH = 4;
+}  // namespace fcwk
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_fwd_wsplit_f32(
+    const FcFwd<float> op) {
+  using namespace fcwk;
+  __shared__ __attribute__((aligned(16))) float red[4 * NCF * 64 * 4];
+  constexpr int NRT = HID / ROWS;
+  const int t = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+  const int r0 = (t % NRT) * ROWS, c0 = (t / NRT) * COLS;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6, k0 = wave * KW;
+  f32x4 a[NKB];
+  const float* ap = op.w + (size_t)(r0 + (lane & 15)) * FLAT + k0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) a[kb] = *reinterpret_cast<const f32x4*>(ap + kb * 16);
+  const float* bp[NCF];
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf)
+    bp[cf] = op.y + (size_t)min(c0 + cf * 16 + (lane & 15), op.C - 1) * FLAT + k0 + 4 * (lane >> 4);
+  f32x4 acc[NCF];
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf) acc[cf] = Frag<float>::zero();
+  // B in chunks of CH k-steps, double-buffered: chunk c + 1 in flight under chunk c's MFMAs
+  f32x4 bq[2][CH][NCF];
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf) bq[0][j][cf] = *reinterpret_cast<const f32x4*>(bp[cf] + j * 16);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int ch = 0; ch < NKB / CH; ++ch) {
+    if (ch + 1 < NKB / CH) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+#pragma unroll
+        for (int cf = 0; cf < NCF; ++cf)
+          bq[(ch + 1) & 1][j][cf] = *reinterpret_cast<const f32x4*>(bp[cf] + ((ch + 1) * CH + j) * 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the next chunk's loads ahead of these MFMAs
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int cf = 0; cf < NCF; ++cf)
+          acc[cf] = Frag<float>::mma_e(e, a[ch * CH + j], bq[ch & 1][j][cf], acc[cf]);
+  }
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf)
+    *reinterpret_cast<f32x4*>(red + ((wave * NCF + cf) * 64 + lane) * 4) = acc[cf];
+  __syncthreads();
+  for (int i = tid; i < NCF * 64; i += 256) {
+    const int cf = i >> 6, ln = i & 63;
+    const float* q = red + (cf * 64 + ln) * 4;
+    constexpr int WS = NCF * 64 * 4;  // one wave's partial
+    f32x4 v = *reinterpret_cast<const f32x4*>(q) + *reinterpret_cast<const f32x4*>(q + WS);
+    v += *reinterpret_cast<const f32x4*>(q + 2 * WS);
+    v += *reinterpret_cast<const f32x4*>(q + 3 * WS);
+    const int o = r0 + 4 * (ln >> 4), c = c0 + cf * 16 + (ln & 15);
+    if (c < op.C) {
+      float vv[4] = {v[0], v[1], v[2], v[3]};
+      op.store(o, c, vv, op.epi(o, c));
+    }
+  }
+}
+
 // actor ‖ critic heads fused into one 16-row GEMM (models/models.py:69-70, 76).
 template <typename T> struct HeadsFwd {
   static constexpr bool A_KMAJOR = false;
