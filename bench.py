@@ -103,6 +103,40 @@ def kernel_work(es):
 
 
 STEP_FLOPS_PER_FRAME = 17_743_872  # fwd 6,836,224 + bwd 10,907,648 (no conv1 dgrad)
+
+# The MFMA instruction mix the fp32 step executes.  conv1's image operand is
+# bytes (exact in bf16) and its other operand (W1 in the forward, dY1 in the weight gradient) is
+# split exactly into three bf16 terms, so conv1 runs as three v_mfma_f32_16x16x32_bf16 passes
+# (conv1.h c1_load_w1, conv12_bwd_body_f32 group B); everything else runs on
+# v_mfma_f32_16x16x4_f32.  Per kernel: {mfma type: (FLOPs executed per frame)} -- conv1's
+# algorithmic FLOPs x 3 at the bf16 rate.  bf16 mode: every contraction on bf16 MFMA, once.
+CONV1_FLOPS = 2 * 225 * 32 * 192  # per frame, forward or weight gradient
+CONV1_PASSES_FP32 = 3
+
+
+def kernel_mix(k, work, dtype):
+    """-> {"fp32": FLOPs/frame on f32 MFMA, "bf16": FLOPs/frame on bf16 MFMA} for kernel k."""
+    f = work[k][0]
+    if dtype == "bf16":
+        return {"fp32": 0, "bf16": f}
+    c1 = CONV1_FLOPS if k in ("conv1_fwd", "conv1_fwd_conv2_fwd", "conv1_conv2_conv3_fwd",
+                              "conv123_fwd_fc_fwd", "conv2_dgrad_conv1_wgrad",
+                              "ln_conv3_conv2_dgrad_conv1_wgrad") else 0
+    return {"fp32": f - c1, "bf16": CONV1_PASSES_FP32 * c1}
+
+
+def mix_floor_s(mix, frames):
+    """Time the executed instruction mix takes at the dense peaks of its MFMA types."""
+    return frames * (mix["fp32"] / (PEAK_TFLOPS["fp32"] * 1e12) +
+                     mix["bf16"] / (PEAK_TFLOPS["bf16"] * 1e12))
+
+
+def step_mix(dtype):
+    """The whole step's executed mix per frame: conv1 forward + conv1 weight gradient."""
+    if dtype == "bf16":
+        return {"fp32": 0, "bf16": STEP_FLOPS_PER_FRAME}
+    return {"fp32": STEP_FLOPS_PER_FRAME - 2 * CONV1_FLOPS,
+            "bf16": CONV1_PASSES_FP32 * 2 * CONV1_FLOPS}
 # PPO: same trunk, one loss head per transition (the heads' work is ~0.1 % of the total)
 STEP_FLOPS_PER_FRAME_PPO = STEP_FLOPS_PER_FRAME
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md
@@ -584,6 +618,8 @@ def main():
     ap.add_argument("--no-alt-line", "--no-fp32-line", dest="no_alt_line", action="store_true",
                     help="skip the other-precision sub-record (bf16_mode / fp32_parity_mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dp-variants", action="store_true",
+                    help="N > 1: skip timing / cross-checking every all-reduce arrangement")
     ap.add_argument("--no-host-staged", action="store_true",
                     help="skip the PCIe-inclusive pass (host batches through impala_stage)")
     ap.add_argument("--algo", default="impala", choices=["impala", "ppo", "sac"],
@@ -637,8 +673,9 @@ def main():
         dist.broadcast(model.flat, 0)
         model.params_changed()
 
-    # data parallel: the library's own RCCL communicator (impala_dp_train_step) unless
-    # IMPALA_DP_NATIVE=0 selects the torch.distributed all-reduce
+    # data parallel: the learner's default (torch.distributed all-reduce) unless
+    # IMPALA_DP_NATIVE=1 selects the library's own RCCL communicator (impala_dp_train_step);
+    # every variant is timed and cross-checked in dp_variants below
     native_dp = dist is not None and native_dp_enabled()
     dp_buckets = native_dp_buckets() if native_dp else None
 
@@ -702,6 +739,10 @@ def main():
         alt = "fp32" if args.dtype == "bf16" else "bf16"
         out["fp32_parity_mode" if alt == "fp32" else "bf16_mode"] = alt_line(
             alt, args, B, T, A, dev, dist, world, make_step, ppo)
+    if native_dp:
+        out["config"]["rccl_nranks"] = eng.dp_nranks
+    if dist is not None and not args.no_dp_variants:
+        out["dp_variants"] = dp_variants(args, B, T, A, dev, dist, world, batch)
     if not args.no_host_staged:
         out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -718,6 +759,85 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+DP_VARIANTS = (("c10d_1bucket", False, 1), ("native_1bucket", True, 1),
+               ("native_2bucket", True, 2))
+
+
+def params_fingerprint(flat):
+    """An exact fingerprint of a float32 buffer: its bit patterns summed with position
+    weights in int64 (equal buffers give equal fingerprints; -0.0 and 0.0 differ)."""
+    bits = flat.contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+    return int((bits * w).sum().item())
+
+
+def replicas_bitwise_equal(flat, dist):
+    """True when every rank holds the same parameters (its fingerprint's max == min over
+    ranks)."""
+    fp = params_fingerprint(flat)
+    t = torch.tensor([fp, -fp], dtype=torch.int64, device=flat.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(int(t[0].item()) == -int(t[1].item()))
+
+
+def dp_variant_record(name, elapsed, steps, frames_per_step, world, nranks=None,
+                      replicas_equal=None, equal_to_default=None):
+    """One dp_variants entry (shape checked by tests/test_bench_launch.py)."""
+    rec = {"ms_per_step": round(elapsed * 1e3 / steps, 4),
+           "value": round(world * frames_per_step * steps / elapsed, 1),
+           "replicas_bitwise_equal": replicas_equal}
+    if nranks is not None:
+        rec["rccl_nranks"] = nranks
+    if equal_to_default is not None:
+        rec["bitwise_equal_to_c10d_1bucket"] = equal_to_default
+    return rec
+
+
+def dp_variants(args, B, T, A, dev, dist, world, batch):
+    """Multi-GPU only: every all-reduce arrangement of the data-parallel step, each from the
+    same seed-0 weights on the same per-rank batch for warmup + steps steps: the timed steps'
+    ms / value (max over ranks), the RCCL communicator's rank count (ncclCommCount) for the
+    native ones, whether the replicas ended bit-identical (fingerprint max == min over ranks)
+    and whether each native arrangement ended bit-identical to the c10d default."""
+    from impala_amd.distributed import compute_grads_allreduced
+    from impala_amd.engine import Engine
+    from impala_amd.model import AtariPPOModel
+    out, finals = {}, {}
+    for name, native, buckets in DP_VARIANTS:
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=args.dtype, seed=0)
+        e = Engine(m, batch_size=B, rollout_length=T, world_size=world, algo=args.algo)
+        m._train_engine = e
+        dist.broadcast(m.flat, 0)
+        m.params_changed()
+        if native:
+            e.dp_init()
+
+        def step(e=e, m=m, native=native, buckets=buckets):
+            if native:
+                e.dp_train_step(*batch, buckets=buckets)
+            else:
+                compute_grads_allreduced(e, batch, m.flat_grad, buckets=buckets)
+                e.apply_update()
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        elapsed, _ = timed_steps(e, step, [], args, dist, dev)
+        torch.cuda.synchronize()
+        finals[name] = m.flat.clone()
+        same = None
+        if name != DP_VARIANTS[0][0]:
+            same = torch.tensor([int(torch.equal(m.flat, finals[DP_VARIANTS[0][0]]))],
+                                dtype=torch.int64, device=dev)
+            dist.all_reduce(same, op=dist.ReduceOp.MIN)
+            same = bool(same.item())
+        out[name] = dp_variant_record(name, elapsed, args.steps, B * T, world,
+                                      e.dp_nranks if native else None,
+                                      replicas_bitwise_equal(m.flat, dist), same)
+        e.close()
+    return out
 
 
 def select_kernels(eng, step, work, args):
@@ -779,8 +899,16 @@ def kernel_roofline(k, timing, work, frames, dtype, algo):
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
     traffic, tsrc = profiled_traffic(k, dtype, algo=algo)
+    mix = kernel_mix(k, work, dtype)
+    floor = mix_floor_s(mix, frames)
     return {"bound": bound, "kernel": k, "achieved": round(achieved, 2), "peak": peak,
-            "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
+            "unit": unit, "frac": round(achieved / peak, 4),
+            # against the instruction mix the kernel executes (kernel_mix): the time its MFMAs
+            # take at the dense peak of their own type / the measured duration
+            "frac_mix": round(floor / t_s, 4),
+            "mix": {"fp32_mfma_flops": mix["fp32"] * frames, "bf16_mfma_flops": mix["bf16"] * frames,
+                    "floor_us": round(floor * 1e6, 2)},
+            "traffic": traffic,
             "traffic_source": (f"profiles/{tsrc}/summary.json (rocprofv3 PMC FETCH_SIZE*2+"
                                "WRITE_SIZE, bytes per launch)") if tsrc else None,
             "algorithmic": {"flops": flops, "bytes": nbytes},
@@ -793,9 +921,14 @@ def step_roofline(frames_per_s_per_gpu, flops_per_frame, dtype):
     """the whole step against the dense MFMA peak (frames/s x algorithmic
     FLOPs per frame, per GPU)."""
     ach = frames_per_s_per_gpu * flops_per_frame / 1e12
+    mix = step_mix(dtype)
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype],
             "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dtype], 4),
-            "flops_per_frame": flops_per_frame}
+            "flops_per_frame": flops_per_frame,
+            # the executed mix's floor per frame x frames/s (= floor / measured step time)
+            "frac_mix": round(mix_floor_s(mix, 1) * frames_per_s_per_gpu, 4),
+            "mix_per_frame": {"fp32_mfma_flops": mix["fp32"], "bf16_mfma_flops": mix["bf16"],
+                              "floor_us_per_frame": round(mix_floor_s(mix, 1) * 1e6, 6)}}
 
 
 def alt_line(dtype, args, B, T, A, dev, dist, world, make_step, ppo):

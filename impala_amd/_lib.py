@@ -18,7 +18,27 @@ IMPALA_DTYPE_BF16 = 1
 IMPALA_ALGO_IMPALA = 0
 IMPALA_ALGO_PPO = 1
 DP_ID_BYTES = 128  # IMPALA_DP_ID_BYTES (ncclUniqueId)
-ABI_VERSION = 2
+# V-trace gradient semantics (IMPALA_VTRACE_SG_*, include/impala_hip.h):
+# what the backward treats as constant.  "sg_advantage" (the default, SURVEY §8(c)'s
+# restatement): targets and pg advantages; "sg_targets": rlax's stop_target_gradients=True
+# with the advantage learning.py:155 multiplies in left live; "sg_none":
+# stop_target_gradients=False.
+VTRACE_GRAD_MODES = {"sg_advantage": 0, "sg_targets": 1, "sg_none": 2}
+DEFAULT_VTRACE_GRAD_MODE = "sg_advantage"
+
+
+def vtrace_grad_mode(mode) -> int:
+    """A mode name (VTRACE_GRAD_MODES) or its int -> the IMPALA_VTRACE_SG_* value."""
+    if mode is None:
+        mode = DEFAULT_VTRACE_GRAD_MODE
+    if isinstance(mode, str):
+        if mode not in VTRACE_GRAD_MODES:
+            raise ValueError(f"vtrace grad mode {mode!r}: one of {sorted(VTRACE_GRAD_MODES)}")
+        return VTRACE_GRAD_MODES[mode]
+    if int(mode) not in VTRACE_GRAD_MODES.values():
+        raise ValueError(f"vtrace grad mode {mode!r}: one of {sorted(VTRACE_GRAD_MODES.values())}")
+    return int(mode)
+ABI_VERSION = 3
 NUM_METRICS = 9  # slots 0-6 METRIC_NAMES, 7 step, 8 PPO train/target
 METRIC_NAMES = ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl",
                 "train/ratio", "train/grad_norm")
@@ -39,6 +59,7 @@ EXPORTS = (
     "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
     "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
     "impala_timer_read_kernel", "impala_dp_unique_id", "impala_dp_init", "impala_dp_train_step",
+    "impala_dp_nranks",
 )
 # every symbol declared in include/sac_hip.h
 SAC_EXPORTS = (
@@ -64,6 +85,7 @@ class ImpalaConfig(C.Structure):
         ("entropy_coeff", C.c_float), ("vtrace_lambda", C.c_float),
         ("clip_rho_threshold", C.c_float), ("clip_pg_rho_threshold", C.c_float),
         ("world_size", C.c_int), ("algo", C.c_int), ("ppo_clip", C.c_float),
+        ("vtrace_grad_mode", C.c_int),
     ]
 
 
@@ -133,11 +155,12 @@ def _declare(lib):
     lib.impala_dp_unique_id.argtypes = [_P]
     lib.impala_dp_init.argtypes = [_P, _P, C.c_int, C.c_int]
     lib.impala_dp_train_step.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int, _P]
+    lib.impala_dp_nranks.argtypes = [_P, C.POINTER(C.c_int)]
     lib.impala_vtrace.argtypes = [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_float, C.c_float,
                                   C.c_float, _P, _P, _P, _P]
     lib.impala_loss_head.argtypes = [_P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
-                                     C.c_float, C.c_float, C.c_float, C.c_float, _P, _P, _P,
-                                     _P, _P, _P, _P, _P]
+                                     C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, _P, _P,
+                                     _P, _P, _P, _P, _P, _P]
     lib.impala_gather_rows.argtypes = [C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_size_t),
                                        C.c_int, _P, C.c_int, _P]
     lib.impala_stage_init.argtypes = [_P, C.c_int]
@@ -190,6 +213,9 @@ def lib():
                     "(run `python -m impala_amd.build`); there is no CPU fallback")
             handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
             _declare(handle)
+            if handle.impala_abi_version() != ABI_VERSION:
+                raise RuntimeError(f"{LIB_PATH}: ABI version {handle.impala_abi_version()}, "
+                                   f"expected {ABI_VERSION} (rebuild: python -m impala_amd.build)")
             _lib = handle
         return _lib
 

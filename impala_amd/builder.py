@@ -126,7 +126,8 @@ class ImpalaBuilder(Builder):
                              learning_starts=self.cfg.agent.learning_starts,
                              rollout_length=self.cfg.agent.rollout_length,
                              dtype=self._learner_cfg("dtype", None), process_group=pg,
-                             world_size=ws, **kw)
+                             world_size=ws,
+                             vtrace_grad_mode=self._learner_cfg("vtrace_grad_mode", None), **kw)
 
     def make_network(self, env_spec=None):  # builder.py:51-59
         obs_shape, n_act = (3, 64, 64), 15

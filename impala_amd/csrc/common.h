@@ -15,6 +15,14 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 #define WAVE 64
+// IMPALA_AB=1 (python -m impala_amd.build --ab) also compiles the measured-slower alternative
+// kernels kept for A/B runs (fc_fwd_splitk_f32 / fc_fwd_wsplit_f32, fwd_chain_kernel,
+// reduce_adam_kernel, wgrad23r_kernel); the product library is built without them, and asking
+// a non-A/B library for one (IMPALA_FC_SPLITK, IMPALA_FWD_CHAIN, IMPALA_FUSED_UPDATE,
+// IMPALA_EARLY_RED) fails impala_create with IMPALA_E_UNSUPPORTED.
+#ifndef IMPALA_AB
+#define IMPALA_AB 0
+#endif
 #define DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------------------------------
@@ -84,6 +92,51 @@ template <> struct Frag<__bf16> {
   }
 };
 
+// ---------------------------------------------------------------------------------------
+// fp32 contractions as exact bf16 MFMA passes.  An fp32 value splits exactly into three bf16
+// terms x = hi + mid + lo (round-to-nearest 8-bit pieces of its 24-bit significand: the
+// residual after hi has <= 16 significant bits, after mid <= 8).  The nine products of two
+// such splits are each exact in fp32 (8 x 8 bits), so nine v_mfma_f32_16x16x32_bf16 (16 cycles
+// per 32 k) compute the fp32 products of a 32-deep k-step -- only the grouping of the fp32
+// additions differs from a v_mfma_f32_16x16x4_f32 chain -- at 9 x 16 = 144 cycles against the
+// 8 x 32 = 256 of the fp32 MFMAs: 1.78x the fp32 MFMA rate, the same arithmetic class as
+// conv1's three passes (one of whose operands is exact in bf16 already).
+// ---------------------------------------------------------------------------------------
+struct X3 {
+  Frag<__bf16>::vec h, m, l;
+};
+DEV void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+DEV X3 split3_8(const float (&x)[8]) {
+  X3 s;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    __bf16 h, m, l;
+    split3(x[c], h, m, l);
+    s.h[c] = h;
+    s.m[c] = m;
+    s.l[c] = l;
+  }
+  return s;
+}
+// the nine exact partial products into one fp32 accumulator, smallest terms first
+DEV f32x4 mma_x3(const X3& a, const X3& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+  return c;
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.  Remap a linear
 // dispatch id so that consecutive work items (which share an operand: the row tiles of one
 // column tile, the column tiles of one split) run on the same XCD and share its L2.
@@ -129,7 +182,7 @@ template <int CTRL> DEV uint32_t dppu(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
 }
 enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROW_MIRROR = 0x140,
-             DPP_ROW_HALF_MIRROR = 0x141, DPP_WAVE_SHL1 = 0x130 };
+             DPP_ROW_HALF_MIRROR = 0x141, DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138 };
 // x[lane ^ 16] (resp. ^ 32) exchanges across rows with v_permlane16/32_swap_b32.  Inline asm
 // with two read-write operands keeps the two copies in distinct registers: the builtin lets the
 // compiler tie both operands to one register, which swaps a register with itself.  The s_nop
@@ -210,6 +263,8 @@ DEV float wave_max(float v) {
 }
 // lane i reads lane i + 1 (lane 63 reads 0): __shfl_down(v, 1) without the LDS crossbar
 DEV float shift_down1(float v) { return dppf<DPP_WAVE_SHL1>(v); }
+// lane i reads lane i - 1 (lane 0 reads 0): __shfl_up(v, 1)
+DEV float shift_up1(float v) { return dppf<DPP_WAVE_SHR1>(v); }
 
 // exact (erf) GELU, models/models.py:68 nn.GELU() default approximate='none'
 DEV float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752440f)); }

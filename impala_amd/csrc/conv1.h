@@ -134,12 +134,7 @@ DEV void c1_stash_frame_rot(T* img, int tid, const uint4 v[3]) {
 // x = hi + mid + lo (round-to-nearest 8-bit pieces of a 24-bit significand: every product with
 // an image byte, exact in bf16, is exact in the fp32 accumulator, so the three MFMA passes
 // compute the fp32 products).  Shared by both conv1 forward kernels (bitwise-equal act1).
-DEV void c1_split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-  h = (__bf16)x;
-  const float r1 = x - (float)h;
-  m = (__bf16)r1;
-  l = (__bf16)(r1 - (float)m);
-}
+DEV void c1_split3(float x, __bf16& h, __bf16& m, __bf16& l) { split3(x, h, m, l); }
 // fp32 W1 staged once per workgroup as its three bf16 planes (plane p: [32][C1W_LD] bf16, rows
 // padded by 16: conflict-free 16-byte fragment reads), instead of every wave loading all of W1
 // (4 x 24.6 KB through the CU's load path) and splitting it

@@ -5,8 +5,9 @@
 //   phase 1  stage h[F][256] of the group's F frames in LDS; heads = Wh . h + bh (MFMA)
 //   phase 2a all 4 waves, one 16-lane row per frame, one lane per action: log-softmax of the
 //            policy and behaviour logits, entropy, KL, log pi(a), rho (row reductions by DPP)
-//   phase 2b wave 0: one lane per (trajectory, t); V-trace as a wavefront shuffle scan
-//            (seg_rev_scan) -> d loss / d value and the per-frame policy-gradient coefficient
+//   phase 2b wave 0: one lane per (trajectory, t); V-trace in the reference's sequential order
+//            (kernels.h vtrace_lane) -> d loss / d value and the per-frame policy-gradient
+//            coefficient d loss / d log pi(a) under the gradient mode (vtrace_grad_lane)
 //   phase 2c all 4 waves, frame x action lanes again: d loss / d logits -> dH[F][32] in LDS
 //   phase 3  dz[f][j] = gelu'(z[f][j]) * sum_o' dH[f][o'] Wh[o'][j]        (MFMA, K = 32;
 //            gelu'(z) comes precomputed from the FC forward epilogue)
@@ -36,6 +37,7 @@ struct HeadArgs {
   // batch
   const int64_t* act; const float* rew; const float* disc; const float* mu;
   int B, T, A, S, TPW;  // TPW = trajectories per workgroup = 64 / S
+  int vt_mode;          // VT_SG_* (kernels.h): what the V-trace gradient treats as constant
   float lam, crho, cpg, ent_coef;
   float clip_lo, clip_hi;  // PPO: ratio clamp bounds (1 -+ clip_coeff)
   // outputs
@@ -217,16 +219,13 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         for (int k = 0; k < 6; ++k) pp[k] = q[k];
       }
     } else {
+      const int tv = valid ? t : 64;  // lanes of missing trajectories are dead in the scans
       const float v_n = shift_down1(v);
-      const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
-      const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
-      const float e = seg_rev_scan(aa, td, t, L, S);
-      const float tgt = e + v;
-      const float err = tgt - v;
-      const float tgt_n = shift_down1(tgt);
-      const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
-      const float qq = r + g * boot;
-      const float adv = fminf(a.cpg, rho) * (qq - v);
+      const VtLane o = vtrace_lane(v, v_n, v_n, r, g, rho, tv, L, a.lam, a.crho, a.cpg);
+      const float err = o.err, qq = o.q, adv = o.adv;
+      const float c_pg = 1.f / (float)(a.B * L);
+      const VtGrad gr = vtrace_grad_lane(o, a.vt_mode, v, v_n, r, g, rho, logpa, tv, L, a.lam,
+                                         a.crho, a.cpg, c_pg);
       if (a.vt_dbg && lead && valid) {
         const size_t BL = (size_t)a.B * L, o = (size_t)(traj0 + tl) * L + t;
         if (inL) {
@@ -238,9 +237,8 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         a.vt_dbg[3 * BL + (size_t)a.B * T_ + f0 + fl] = v;
       }
       if (valid) {
-        const float c_pg = 1.f / (float)(a.B * L);
-        fsc[4][f] = inL ? -c_pg * adv : 0.f;
-        dHs[f * LDD + VCOL] = (T)(inL ? -2.f * c_pg * err : 0.f);
+        fsc[4][f] = gr.dlogpa;
+        dHs[f * LDD + VCOL] = (T)gr.dv;
       }
       float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
       s0 = wave_sum(s0); s1 = wave_sum(s1);

@@ -274,6 +274,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     // training forward (no heads launch after it): the FC forward joins the launch, each FC
     // tile waiting on flags of the conv workgroups that produce its frames (not under graph
     // capture: the epoch argument changes every launch)
+#if IMPALA_AB
     if (sizeof(T) == 2 && conv3_done && !with_heads && h->fwd_chain && !h->use_graph) {
       if (++h->chain_epoch == 0) h->chain_epoch = 1;
       c3.y_sc1 = 1;
@@ -289,6 +290,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
       }
       return 0;
     }
+#endif
     if (int r = klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>,
                         dim3(cdiv(n, fpw)), dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1,
                         vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
@@ -313,6 +315,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
                         dim3(persist_grid(h, cdiv((long)n * P3, 64))), dim3(256), st, op, 1))
       return r;
   }
+#if IMPALA_AB
   if (sizeof(T) == 4 && h->fc_splitk == 2) {
     FcFwd<float> op{n, (const float*)(sw + sh.wfc), vv + Vecs::bfc, (const float*)h->y, h->zg,
                     (float*)h->h};
@@ -329,7 +332,9 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     if (int r = klaunch(h, K_FC_FWD, "fc_fwd_splitk", kern, dim3(grid), dim3(256), st, op,
                         h->fcsk_slab, h->fcsk_cnt))
       return r;
-  } else {
+  } else
+#endif
+  {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->zg, (T*)h->h};
     // 32 x 32 tiles: 320 workgroups (5.9 vs 6.7 us for 64 x 32, tools/var_specs/fcfwd.py)
     if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 32, 32, BK(256), 2, 2, FcFwd<T>>,
@@ -405,6 +410,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     ha.B = B; ha.T = Tl; ha.A = h->A; ha.S = h->S_seg; ha.TPW = 64 / h->S_seg;
     ha.lam = h->cfg.vtrace_lambda; ha.crho = h->cfg.clip_rho_threshold;
     ha.cpg = h->cfg.clip_pg_rho_threshold; ha.ent_coef = h->cfg.entropy_coeff;
+    ha.vt_mode = h->cfg.vtrace_grad_mode;
     ha.dz = h->dz; ha.partials = h->loss_part; ha.slab_h = h->s_h; ha.slab_bh = h->s_bh;
     ha.heads_out = h->heads;
     ha.vt_dbg = h->cfg.algo == IMPALA_ALGO_PPO ? nullptr : h->vt_dbg;
@@ -501,6 +507,7 @@ stage_b:
         return r;
     }
     const int g3x = K3 / 64, g3z = h->sp3.S, g2x = K2 / 128, g2z = h->sp2.S;
+#if IMPALA_AB
     if (early) {
       // conv1 + b1 and LayerNorm (+ FC and heads unless part 2 reduced them) units ride along
       const int* ws = h->red.wg_start;
@@ -511,7 +518,9 @@ stage_b:
                           o3, h->s_w3, h->s_b3, h->sp3.mps, g3x, g3z, o2, h->s_w2, h->s_b2,
                           h->sp2.mps, g2x, g2z, h->red, u0, n0, u1, n1))
         return r;
-    } else if (int r = klaunch(h, K_WGRAD23, "conv3_wgrad_conv2_wgrad", wgrad23_kernel<T, WG4>,
+    } else
+#endif
+    if (int r = klaunch(h, K_WGRAD23, "conv3_wgrad_conv2_wgrad", wgrad23_kernel<T, WG4>,
                                dim3(g3x * g3z + g2x * g2z), dim3(256 * WG4), st, o3, h->s_w3,
                                h->s_b3, h->sp3.mps, g3x, g3z, o2, h->s_w2, h->s_b2, h->sp2.mps,
                                g2x, g2z)) {
@@ -621,6 +630,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
                  dim3(256), st, aa);
 }
 
+#if IMPALA_AB
 // slab reduction + clip + Adam in one launch (world_size 1; backward run with part 5)
 template <typename T>
 int launch_reduce_adam(impala_learner* h, hipStream_t st) {
@@ -637,6 +647,7 @@ int launch_reduce_adam(impala_learner* h, hipStream_t st) {
                  dim3(cdiv(h->n_red_wg, FU_MAX_UNITS)),
                  dim3(256), st, h->red, aa, h->fsync);
 }
+#endif  // IMPALA_AB
 
 template <typename T>
 int launch_pack(impala_learner* h, hipStream_t st) {
@@ -706,6 +717,7 @@ int impala_config_default(impala_config* c) {
   c->world_size = 1;
   c->algo = IMPALA_ALGO_IMPALA;
   c->ppo_clip = 0.1f;
+  c->vtrace_grad_mode = IMPALA_VTRACE_SG_ADVANTAGE;
   return 0;
 }
 
@@ -726,9 +738,21 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
     return fail(IMPALA_E_INVALID, "ppo_clip must be in [0, 1)");
   if (cfg->num_actions < 1 || cfg->num_actions > MAX_A)
     return fail(IMPALA_E_UNSUPPORTED, "num_actions must be in [1, 15]");
+  if (cfg->vtrace_grad_mode < IMPALA_VTRACE_SG_ADVANTAGE || cfg->vtrace_grad_mode > IMPALA_VTRACE_SG_NONE)
+    return fail(IMPALA_E_INVALID, "unknown vtrace_grad_mode");
   if (cfg->dtype != IMPALA_DTYPE_F32 && cfg->dtype != IMPALA_DTYPE_BF16)
     return fail(IMPALA_E_INVALID, "unknown dtype");
   if (cfg->world_size < 1) return fail(IMPALA_E_INVALID, "world_size must be >= 1");
+#if !IMPALA_AB
+  // the measured-slower alternatives are compiled into A/B builds only (common.h IMPALA_AB)
+  for (const char* v : {"IMPALA_FC_SPLITK", "IMPALA_FWD_CHAIN", "IMPALA_FUSED_UPDATE",
+                        "IMPALA_EARLY_RED"}) {
+    const char* e = std::getenv(v);
+    if (e && e[0] && e[0] != '0')
+      return fail(IMPALA_E_UNSUPPORTED, std::string(v) + " selects an A/B variant this library "
+                                        "was built without (python -m impala_amd.build --ab)");
+  }
+#endif
   CK(hipSetDevice(device));
   impala_learner* h = new (std::nothrow) impala_learner();
   if (!h) return fail(IMPALA_E_INVALID, "out of host memory");
@@ -968,6 +992,7 @@ struct RcclApi {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommCount) comm_count = nullptr;
   std::string err;
 };
 const RcclApi& rccl() {
@@ -986,7 +1011,9 @@ const RcclApi& rccl() {
     a.all_reduce = (decltype(a.all_reduce))dlsym(lib, "ncclAllReduce");
     a.comm_destroy = (decltype(a.comm_destroy))dlsym(lib, "ncclCommDestroy");
     a.error_string = (decltype(a.error_string))dlsym(lib, "ncclGetErrorString");
-    if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy || !a.error_string)
+    a.comm_count = (decltype(a.comm_count))dlsym(lib, "ncclCommCount");
+    if (!a.get_unique_id || !a.comm_init_rank || !a.all_reduce || !a.comm_destroy ||
+        !a.error_string || !a.comm_count)
       a.err = "librccl lacks an expected entry point";
     return a;
   }();
@@ -1227,16 +1254,43 @@ int impala_dp_init(impala_learner* h, const void* unique_id, int nranks, int ran
     h->dp_comm = nullptr;
     return rccl_fail("ncclCommInitRank", r);
   }
-  CK(hipStreamCreateWithFlags(&h->dp_stream, hipStreamNonBlocking));
-  for (auto& e : h->dp_ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  h->dp_nranks = nranks;
+  // the rest cannot leave a half-initialised handle: any failure releases the communicator
+  // (impala_dp_train_step then reports that impala_dp_init has not run)
+  hipError_t e = hipStreamCreateWithFlags(&h->dp_stream, hipStreamNonBlocking);
+  for (auto& ev : h->dp_ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    dp_release(h);
+    return fail((int)e, std::string("impala_dp_init: ") + hipGetErrorString(e));
+  }
+  int count = 0;
+  if (ncclResult_t r = api.comm_count(h->dp_comm, &count)) {
+    dp_release(h);
+    return rccl_fail("ncclCommCount", r);
+  }
+  if (count != nranks) {
+    dp_release(h);
+    return fail(IMPALA_E_RCCL, "ncclCommCount disagrees with nranks");
+  }
+  h->dp_nranks = count;
   h->dp_rank = rank;
+  return 0;
+}
+
+int impala_dp_nranks(const impala_learner* h, int* nranks) {
+  if (!h || !nranks) return fail(IMPALA_E_INVALID, "null argument");
+  *nranks = 0;
+  if (!h->dp_comm) return 0;
+  const RcclApi& api = rccl();
+  if (!api.err.empty()) return fail(IMPALA_E_RCCL, api.err);
+  if (ncclResult_t r = api.comm_count(h->dp_comm, nranks)) return rccl_fail("ncclCommCount", r);
   return 0;
 }
 
 int impala_dp_train_step(impala_learner* h, const impala_batch* b, int buckets, void* stream) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
-  if (!h->dp_comm) return fail(IMPALA_E_STATE, "impala_dp_init has not run on this handle");
+  if (!h->dp_comm || !h->dp_stream || !h->dp_ev[2])
+    return fail(IMPALA_E_STATE, "impala_dp_init has not run on this handle");
   if (buckets != 1 && buckets != 2) return fail(IMPALA_E_INVALID, "buckets must be 1 or 2");
   if (int r = check_bound(h)) return r;
   if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
@@ -1285,10 +1339,12 @@ int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
   if (int r = check_batch(b, h->cfg.algo == IMPALA_ALGO_PPO)) return r;
   CK(hipSetDevice(h->device));
   return run_graphed(h, G_STEP, b, (hipStream_t)stream, [&](hipStream_t s) {
+#if IMPALA_AB
     if (h->fused_update) {
       if (int r = enqueue_grads(h, b, s, 5)) return r;
       return h->bf16 ? launch_reduce_adam<__bf16>(h, s) : launch_reduce_adam<float>(h, s);
     }
+#endif
     if (int r = enqueue_grads(h, b, s)) return r;
     return enqueue_update(h, s);
   });
@@ -1545,10 +1601,12 @@ int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const 
 int impala_loss_head(const float* logits, const float* values, const int64_t* actions,
                      const float* rewards, const float* discounts, const float* behaviour_logits,
                      int B, int T, int A, float entropy_coeff, float lambda_, float clip_rho,
-                     float clip_pg_rho, float* dlogits, float* dvalues, float* metrics6,
-                     float* adv, float* err, float* q, float* rho, void* stream) {
+                     float clip_pg_rho, int vtrace_grad_mode, float* dlogits, float* dvalues,
+                     float* metrics6, float* adv, float* err, float* q, float* rho, void* stream) {
   if (B < 1 || T < 2 || T > 64 || A < 1 || A > net::MAX_A)
     return fail(IMPALA_E_INVALID, "need B >= 1, 2 <= T <= 64, 1 <= A <= 15");
+  if (vtrace_grad_mode < IMPALA_VTRACE_SG_ADVANTAGE || vtrace_grad_mode > IMPALA_VTRACE_SG_NONE)
+    return fail(IMPALA_E_INVALID, "unknown vtrace_grad_mode");
   if (!logits || !values || !actions || !rewards || !discounts || !behaviour_logits || !dlogits ||
       !dvalues || !metrics6)
     return fail(IMPALA_E_INVALID, "null pointer");
@@ -1561,7 +1619,7 @@ int impala_loss_head(const float* logits, const float* values, const int64_t* ac
   LossArgs la{};
   la.logits = logits; la.lg_ld = A; la.values = values; la.v_ld = 1;
   la.act = actions; la.rew = rewards; la.disc = discounts; la.mu = behaviour_logits;
-  la.B = B; la.T = T; la.A = A; la.S = S;
+  la.B = B; la.T = T; la.A = A; la.S = S; la.vt_mode = vtrace_grad_mode;
   la.lam = lambda_; la.crho = clip_rho; la.cpg = clip_pg_rho; la.ent_coef = entropy_coeff;
   la.partials = part;
   la.dbg_adv = dbg ? adv : nullptr; la.dbg_err = dbg ? err : nullptr; la.dbg_q = dbg ? q : nullptr;

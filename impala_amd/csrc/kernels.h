@@ -9,26 +9,119 @@
 using namespace net;
 
 // =========================================================================================
-// V-trace as a segmented reverse linear-recurrence scan across the lanes of a wavefront.
-// Lane t of a segment holds (a_t, b_t) with e_t = b_t + a_t * e_{t+1}, e_L = 0.  Hillis-Steele
-// over __shfl_down: after the step with offset d every lane holds the composition of the maps
-// t .. t+2d-1, so log2(S) shuffle rounds give e_t on every lane (S = segment size <= 64).
-// (rlax/rlego vtrace_td_error_and_advantage; agents/impala/learning.py:15-26,150-153.)
+// V-trace (rlax/rlego vtrace_td_error_and_advantage as called through
+// agents/impala/learning.py:15-26,150-153), one lane per (trajectory, t) of a wavefront segment
+// of S lanes, L = T - 1 live lanes.
+//
+// Forward order.  Every operation rounds once, in the order of the fp32 restatement
+// (oracle/vtrace.py: td = rho' * ((r + g v_t) - v_tm1); acc = td + (g c) * acc; target = acc +
+// v_tm1; ...): floating-point contraction is off in these functions, so on identical inputs the
+// outputs are bit-identical to the sequential fp32 loop.  The reverse recurrence
+// e_t = b_t + a_t e_{t+1} runs as L sweeps over the segment, each lane recomputing its e from
+// its neighbour's value of the previous sweep (DPP wave shift): after sweep k the lanes
+// t >= L - k hold their final value, computed from the final e_{t+1} -- the sequential loop's
+// own operations, so its own rounding (a log-depth composition of the affine maps would sum in
+// tree order instead).  L <= 63 sweeps of 3 VALU operations.
+//
 // Return order (pg_advantage, td_error, q_estimate): taken from the reference's unpacking
 // `adv, err, _ =` (learning.py:150); rlax's published VTraceOutput lists (errors,
 // pg_advantage, q_estimate).  rlego itself is absent, so this order is an unpinned assumption
 // pinned only by the reference's own call sites.
+//
+// Gradient semantics (IMPALA_VTRACE_SG_*, include/impala_hip.h).  learning.py:148-155 detaches
+// neither rho nor the advantage; what is constant depends on rlego:
+//   SG_ADVANTAGE (0)  targets and pg advantages constant (the IMPALA paper's estimator)
+//   SG_TARGETS   (1)  rlax stop_target_gradients=True: targets constant, the advantage
+//                     rho_pg (q - v_tm1) live -- through min(rho_pg, rho) into log pi(a), into
+//                     v_tm1 and, via q's bootstrap, into v_t[L-1] ((1 - lambda) v_tm1[t+1])
+//   SG_NONE      (2)  stop_target_gradients=False: also through the targets, i.e. the scan
 // =========================================================================================
-DEV float seg_rev_scan(float a, float b, int t, int L, int S) {
-  for (int d = 1; d < S; d <<= 1) {
-    const float a2 = __shfl_down(a, d, 64);
-    const float b2 = __shfl_down(b, d, 64);
-    if (t + d < L) {
-      b = fmaf(a, b2, b);
-      a = a * a2;
-    }
+enum : int { VT_SG_ADVANTAGE = 0, VT_SG_TARGETS = 1, VT_SG_NONE = 2 };
+
+DEV float seq_rev_scan(float a, float b, int t, int L) {
+#pragma clang fp contract(off)
+  const bool live = t < L, nxt = t + 1 < L;
+  float e = 0.f;
+  for (int k = 0; k < L; ++k) {
+    const float en = shift_down1(e);
+    e = live ? b + a * (nxt ? en : 0.f) : 0.f;
   }
-  return b;
+  return e;
+}
+// the adjoint of seq_rev_scan: E_t = b_t + a_{t-1} E_{t-1}, E_0 = b_0 (forward in t)
+DEV float seq_fwd_scan(float a, float b, int t, int L) {
+  const bool live = t < L, prv = t >= 1;
+  float E = 0.f;
+  for (int k = 0; k < L; ++k) {
+    const float p = shift_up1(a * E);
+    E = live ? b + (prv ? p : 0.f) : 0.f;
+  }
+  return E;
+}
+
+struct VtLane {
+  float a, td, e, tgt, err, q, adv;
+};
+// v = v_tm1[t], vt = v_t[t], vnx = v_tm1[t + 1] (only read for t < L - 1); lanes t >= L
+// produce zeros.  In the learner v_t = values[:, 1:], so vt == vnx == the next lane's v.
+DEV VtLane vtrace_lane(float v, float vt, float vnx, float r, float g, float rho, int t, int L,
+                       float lam, float crho, float cpg) {
+#pragma clang fp contract(off)
+  const bool in = t < L;
+  VtLane o;
+  o.td = in ? fminf(crho, rho) * (r + g * vt - v) : 0.f;
+  o.a = in ? g * (fminf(1.f, rho) * lam) : 0.f;
+  o.e = seq_rev_scan(o.a, o.td, t, L);
+  o.tgt = o.e + v;
+  o.err = o.tgt - v;
+  const float tgt_n = shift_down1(o.tgt);
+  const float boot = (t < L - 1) ? lam * tgt_n + (1.f - lam) * vnx : vt;
+  o.q = r + g * boot;
+  o.adv = fminf(cpg, rho) * (o.q - v);
+  return o;
+}
+
+// d loss / d log pi(a_t) and d loss / d v_t of the lane's frame t (t = 0 .. L, the last frame
+// only through the bootstrap) for
+//   loss = -c_pg sum_t log pi(a_t) adv_t + c_pg sum_t err_t^2 + (entropy term, elsewhere),
+// c_pg = 1 / (B (T - 1)) (learning.py:155-159).  Every lane of the wavefront calls it.
+struct VtGrad {
+  float dlogpa, dv;
+};
+DEV VtGrad vtrace_grad_lane(const VtLane& o, int mode, float v, float vt, float r, float g,
+                            float rho, float logpa, int t, int L, float lam, float crho,
+                            float cpg, float c_pg) {
+  const bool in = t < L;
+  VtGrad d;
+  d.dlogpa = in ? -c_pg * o.adv : 0.f;
+  float dv = 0.f, dv_nx = 0.f, rbar = 0.f;  // -> v_t, -> v_{t+1}, -> rho_t
+  if (mode != VT_SG_NONE) dv = in ? -2.f * c_pg * o.err : 0.f;  // err = sg(target) - v
+  if (mode != VT_SG_ADVANTAGE) {
+    const float abar = in ? -c_pg * logpa : 0.f;  // d loss / d adv_t
+    const float qbar = fminf(cpg, rho) * abar;    // d loss / d q_t
+    if (rho <= cpg) rbar += abar * (o.q - v);     // adv = min(cpg, rho) (q - v)
+    dv -= qbar;
+    dv_nx += (t < L - 1) ? (1.f - lam) * g * qbar : g * qbar;  // q's bootstrap
+    if (mode == VT_SG_NONE) {
+      // target_t = e_t + v_t enters err_t (whose own -v_t cancels target's +v_t) and q_{t-1}
+      const float tq = shift_up1((t < L - 1) ? lam * g * qbar : 0.f);  // from q_{t-1}
+      dv += (in && t >= 1) ? tq : 0.f;
+      const float ebar = in ? 2.f * c_pg * o.err + (t >= 1 ? tq : 0.f) : 0.f;
+      const float E = seq_fwd_scan(o.a, ebar, t, L);  // total adjoint of e_t
+      // e_t = td_t + a_t e_{t+1};  td_t = min(crho, rho) (r + g v_{t+1} - v_t);
+      // a_t = g min(1, rho) lambda
+      const float rc = fminf(crho, rho);
+      dv -= rc * E;
+      dv_nx += rc * g * E;
+      if (rho <= crho) rbar += E * (r + g * vt - v);
+      const float e_n = shift_down1(o.e);
+      if (rho <= 1.f) rbar += E * ((t + 1 < L) ? e_n : 0.f) * g * lam;
+    }
+    d.dlogpa += in ? rbar * rho : 0.f;  // rho = exp(log pi(a) - log mu(a))
+  }
+  const float from_prev = shift_up1(in ? dv_nx : 0.f);
+  d.dv = (in ? dv : 0.f) + (t >= 1 && t <= L ? from_prev : 0.f);
+  return d;
 }
 
 // Standalone batched V-trace on [B][L] inputs (impala_vtrace).
@@ -49,17 +142,11 @@ __global__ __launch_bounds__(256) void vtrace_kernel(const float* __restrict__ v
   const size_t i = (size_t)traj * L + t;
   const float v = in ? v_tm1[i] : 0.f, vt = in ? v_t[i] : 0.f, r = in ? r_t[i] : 0.f,
               g = in ? g_t[i] : 0.f, rho = in ? rho_t[i] : 0.f;
-  const float td = in ? fminf(crho, rho) * (r + g * vt - v) : 0.f;
-  const float aa = in ? g * (lam * fminf(1.f, rho)) : 0.f;
-  const float e = seg_rev_scan(aa, td, t, L, S);
-  const float tgt = e + v;
-  const float tgt_n = shift_down1(tgt), v_n = shift_down1(v);
-  const float boot = (t < L - 1) ? lam * tgt_n + (1.f - lam) * v_n : vt;
-  const float qq = r + g * boot;
+  const VtLane o = vtrace_lane(v, vt, shift_down1(v), r, g, rho, in ? t : L, L, lam, crho, cpg);
   if (in) {
-    err[i] = tgt - v;
-    q[i] = qq;
-    adv[i] = fminf(cpg, rho) * (qq - v);
+    err[i] = o.err;
+    q[i] = o.q;
+    adv[i] = o.adv;
   }
 }
 
@@ -67,18 +154,18 @@ __global__ __launch_bounds__(256) void vtrace_kernel(const float* __restrict__ v
 // Fused loss head (agents/impala/learning.py:144-170): per (b,t) lane: log-softmax of the
 // policy and behaviour logits, log pi(a), rho, entropy, KL; per trajectory: V-trace scan over
 // T-1 (the last step is dropped from pg/value, kept for entropy/KL/ratio, learning.py:150-157);
-// analytic d loss / d logits and d loss / d value with rlax stop-gradient semantics
-// (targets and advantages are constants):
+// analytic d loss / d logits and d loss / d value under the V-trace gradient mode vt_mode
+// (VT_SG_*, vtrace_grad_lane):
 //   loss = -mean_{B,T-1}(log pi(a) adv) + mean_{B,T-1}(err^2) - c_ent * mean_{B,T} H(pi)
-//   dlogit_j = c_ent/(BT) pi_j (log pi_j + H)  -  [t<T-1] adv/(B(T-1)) (1[j=a] - pi_j)
-//   dvalue   = -[t<T-1] 2 err/(B(T-1))
+//   dlogit_j = c_ent/(BT) pi_j (log pi_j + H)  +  kappa_t (1[j=a] - pi_j),
+//   kappa_t = d loss / d log pi(a_t)  (= -[t<T-1] adv/(B(T-1)) with the advantage constant)
 // Per-workgroup partial sums of (log pi(a) adv, err^2, H, KL, rho) go to `partials`.
 // =========================================================================================
 struct LossArgs {
   const float* logits; int lg_ld;
   const float* values; int v_ld;
   const int64_t* act; const float* rew; const float* disc; const float* mu;
-  int B, T, A, S;
+  int B, T, A, S, vt_mode;
   float lam, crho, cpg, ent_coef;
   float* partials;  // [gridDim.x][8]
   float* dbg_adv; float* dbg_err; float* dbg_q; float* dbg_rho;
@@ -153,31 +240,27 @@ __global__ __launch_bounds__(256) void loss_head_kernel(const LossArgs a, TO* __
     rho = expf(logpa - logmua);
   }
   // ---- V-trace over the first T-1 steps of each trajectory segment ----
+  const int tv = valid ? t : 64;     // lanes of missing trajectories are dead in the scans
   const float v_n = shift_down1(v);  // values[:, 1:]
-  const float td = inL ? fminf(a.crho, rho) * (r + g * v_n - v) : 0.f;
-  const float aa = inL ? g * (a.lam * fminf(1.f, rho)) : 0.f;
-  const float e = seg_rev_scan(aa, td, t, L, S);
-  const float tgt = e + v;
-  const float err = tgt - v;
-  const float tgt_n = shift_down1(tgt);
-  const float boot = (t < L - 1) ? a.lam * tgt_n + (1.f - a.lam) * v_n : v_n;
-  const float qq = r + g * boot;
-  const float adv = fminf(a.cpg, rho) * (qq - v);
+  const VtLane o = vtrace_lane(v, v_n, v_n, r, g, rho, tv, L, a.lam, a.crho, a.cpg);
+  const float err = o.err, qq = o.q, adv = o.adv;
+  const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T);
+  const VtGrad gr = vtrace_grad_lane(o, a.vt_mode, v, v_n, r, g, rho, logpa, tv, L, a.lam,
+                                     a.crho, a.cpg, c_pg);
 
   if (valid) {
-    const float c_pg = 1.f / (float)(a.B * L), c_ent = 1.f / (float)(a.B * T);
-    const float ke = a.ent_coef * c_ent, kp = inL ? c_pg * adv : 0.f;
+    const float ke = a.ent_coef * c_ent, kp = gr.dlogpa;
 #pragma unroll
     for (int j = 0; j < MAX_A; ++j) {
       if (j < A) {
         const float p = expf(logp[j]);
-        const float d = ke * p * (logp[j] + H) - kp * ((j == act ? 1.f : 0.f) - p);
+        const float d = ke * p * (logp[j] + H) + kp * ((j == act ? 1.f : 0.f) - p);
         dl[n * dl_ld + j] = (TO)d;
       } else if (j < zero_to) {
         dl[n * dl_ld + j] = (TO)0.f;
       }
     }
-    dv[n * dv_ld] = (TO)(inL ? -2.f * c_pg * err : 0.f);
+    dv[n * dv_ld] = (TO)gr.dv;
     if (a.dbg_rho) a.dbg_rho[n] = rho;
     if (inL && a.dbg_adv) {
       const size_t k = (size_t)traj * L + t;
@@ -851,6 +934,7 @@ struct FusedSync {
   const float* part;   // partials written by earlier launches (direct-mode weight gradients)
 };
 
+#if IMPALA_AB  // reduce_adam_kernel: measured slower, A/B builds only
 template <typename T>
 __global__ __launch_bounds__(256) void reduce_adam_kernel(const RedArgs a, const AdamArgs aa,
                                                           const FusedSync fs) {
@@ -986,6 +1070,7 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const RedArgs a, const
       write_shadow<T>(aa.sp, aa.cn, aa.sh, (size_t)c, p[j][i]);
     }
 }
+#endif  // IMPALA_AB
 
 // heads output [n][16] -> logits [n][A], values [n]
 __global__ void split_heads_kernel(const float* __restrict__ heads, int n, int A,
@@ -1107,6 +1192,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   }
 }
 
+#if IMPALA_AB  // wgrad23r_kernel: measured slower, A/B builds only
 // conv3 + conv2 weight gradients (wgrad23_kernel's blocks) plus the reduction units of the
 // slabs that are already final when they start -- conv1 / LayerNorm (the per-frame backward)
 // and FC / heads -- as extra blocks, one unit per 256-thread quarter: the conv weight
@@ -1137,3 +1223,4 @@ __global__ __launch_bounds__(256 * G) void wgrad23r_kernel(
                                                          reinterpret_cast<T*>(lds));
   }
 }
+#endif  // IMPALA_AB

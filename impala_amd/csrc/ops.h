@@ -117,6 +117,7 @@ namespace fcsk {
 constexpr int ROWS = 64, COLS = 80, NS = 4, KS = FLAT / NS, LDB = KS + 4, PART = ROWS * COLS;
 constexpr int NCF = COLS / 16, NKB = KS / 16;
 }  // namespace fcsk
+#if IMPALA_AB  // fc_fwd_splitk_f32 / fc_fwd_wsplit_f32: measured slower, A/B builds only
 // PUB (publish form): 1 = write-through (sc1) slab stores and sc1 slab loads, no fences
 // (the default); 0 = plain stores, agent release before the ticket, agent acquire in the
 // reducer; 2 = measurement knock-out (partials stored, no combine: wrong results).
@@ -300,6 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
 }
+#endif  // IMPALA_AB
 
 // actor ‖ critic heads fused into one 16-row GEMM (models/models.py:69-70, 76).
 template <typename T> struct HeadsFwd {
@@ -522,6 +524,7 @@ __global__ __launch_bounds__(256 * G) void wgrad23_kernel(const Conv3Wgrad<T> o3
                                                          g2x, 1, g2z, smem);
 }
 
+#if IMPALA_AB  // fwd_chain_kernel: measured slower, A/B builds only
 // The trunk forward and the FC forward in ONE launch (bf16, conv3 tail on): blocks [0, n_conv)
 // run the per-frame conv1 / conv2 / conv3+LayerNorm body and publish a flag each; the FC tile
 // blocks after them (64 hidden units x 32 frames, 8 waves, one tile per block) wait only for
@@ -583,3 +586,4 @@ __global__ __launch_bounds__(512) void fwd_chain_kernel(
   __syncthreads();
   gemm_tile_body<T, C::FR, C::FC, C::FK, C::FWR, C::FWC, FcFwd<T>>(fc, n_rt, vb, vg, smem);
 }
+#endif  // IMPALA_AB

@@ -3,10 +3,10 @@
 Trajectories are independent and every loss term is a mean over (B, T-1) or (B, T), so with
 equal shards the mean of the replicas' gradients IS the full-batch gradient.
 
-Default on RCCL groups: the library's own communicator (``Engine.dp_init``,
+Default: the torch.distributed path below.  Opt-in on RCCL groups (IMPALA_DP_NATIVE=1,
+``native_dp_enabled``): the library's own communicator (``Engine.dp_init``,
 ``impala_dp_train_step``) enqueues the whole step -- backward, in-place ncclAllReduce of the
-gradient buckets on its side stream, update -- with no host round trip (``native_dp_enabled``).
-The torch.distributed path below stays for gloo groups and IMPALA_DP_NATIVE=0.  Each replica:
+gradient buckets on its side stream, update -- with no host round trip.  Each replica:
 ``impala_compute_grads`` (the whole backward) -> ``all_reduce(sum)`` of the flat fp32 gradient
 (bucketed variants: ``compute_grads_allreduced``) -> ``impala_apply_update`` (x 1/world,
 global-norm clip on the reduced gradient -- identical on every replica -- and Adam).  Weights therefore stay bit-identical
@@ -101,11 +101,14 @@ def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None,
 
 
 def native_dp_enabled(group=None) -> bool:
-    """The library's own RCCL communicator (``Engine.dp_init`` / ``dp_train_step``) drives the
-    data-parallel step when the group is an RCCL (``nccl``) group, unless IMPALA_DP_NATIVE=0
-    selects the torch.distributed (c10d) all-reduce of ``compute_grads_allreduced``."""
+    """Opt-in (IMPALA_DP_NATIVE=1, RCCL groups only): the library's own RCCL communicator
+    (``Engine.dp_init`` / ``dp_train_step``) drives the data-parallel step.  The default is the
+    torch.distributed (c10d) all-reduce of ``compute_grads_allreduced``: the native path has
+    run on one rank only (bitwise equal to ``train_step`` there), and stays opt-in until a
+    multi-GPU run shows its replicas bit-identical to each other and to the c10d step
+    (``bench.py --gpus N`` records both checks, ``dp_variants``)."""
     import torch.distributed as dist
-    if os.environ.get("IMPALA_DP_NATIVE", "1") == "0":
+    if os.environ.get("IMPALA_DP_NATIVE", "0") != "1":
         return False
     return dist.get_backend(group) == "nccl"
 

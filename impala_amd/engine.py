@@ -25,7 +25,7 @@ class Engine:
                  max_grad_norm: float = 0.5, entropy_coeff: float = 0.01, world_size: int = 1,
                  vtrace_lambda: float = 1.0, clip_rho_threshold: float = 1.0,
                  clip_pg_rho_threshold: float = 1.0, inference_only: bool = False,
-                 algo: str = "impala", ppo_clip: float = 0.1):
+                 algo: str = "impala", ppo_clip: float = 0.1, vtrace_grad_mode=None):
         if model.flat.device.type != "cuda":
             raise RuntimeError("the IMPALA learner runs on the HIP path only (cuda device)")
         self.model = model
@@ -58,6 +58,7 @@ class Engine:
         cfg.world_size = int(world_size)
         cfg.algo = _lib.IMPALA_ALGO_PPO if algo == "ppo" else _lib.IMPALA_ALGO_IMPALA
         cfg.ppo_clip = float(ppo_clip)
+        cfg.vtrace_grad_mode = _lib.vtrace_grad_mode(vtrace_grad_mode)
         self.cfg = cfg
         h = C.c_void_p()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -276,6 +277,13 @@ class Engine:
         check(_lib.lib().impala_dp_init(self._h, ptr(uid), world, rank), "impala_dp_init")
         self._dp = True
 
+    @property
+    def dp_nranks(self) -> int:
+        """Rank count of the handle's RCCL communicator (ncclCommCount; 0 before dp_init)."""
+        n = C.c_int()
+        check(_lib.lib().impala_dp_nranks(self._h, C.byref(n)), "impala_dp_nranks")
+        return int(n.value)
+
     def dp_train_step(self, *batch, buckets: int = 1, stream=None):
         """The whole data-parallel step on the handle's communicator (impala_dp_train_step):
         local gradients, in-place RCCL all-reduce (sum) on the compute stream -- ``buckets=2``:
@@ -378,8 +386,9 @@ def vtrace(v_tm1, v_t, r_t, discount_t, rho_tm1, lambda_=1.0, clip_rho_threshold
 
 
 def loss_head(logits, values, actions, rewards, discounts, mu, entropy_coeff=0.01, lambda_=1.0,
-              clip_rho=1.0, clip_pg_rho=1.0, stream=None):
-    """Fused loss head (learning.py:144-170) on device tensors; returns a dict."""
+              clip_rho=1.0, clip_pg_rho=1.0, grad_mode=None, stream=None):
+    """Fused loss head (learning.py:144-170) on device tensors; returns a dict.  ``grad_mode``:
+    the V-trace gradient semantics (``_lib.VTRACE_GRAD_MODES``, default "sg_advantage")."""
     B, T, A = logits.shape
     dev = logits.device
     f = lambda t: t.contiguous().to(torch.float32)  # noqa: E731
@@ -392,7 +401,8 @@ def loss_head(logits, values, actions, rewards, discounts, mu, entropy_coeff=0.0
     err, q = torch.empty_like(adv), torch.empty_like(adv)
     rho = torch.empty(B, T, dtype=torch.float32, device=dev)
     check(_lib.lib().impala_loss_head(ptr(lg), ptr(v), ptr(a), ptr(r), ptr(g), ptr(m), B, T, A,
-                                      entropy_coeff, lambda_, clip_rho, clip_pg_rho, ptr(dl),
+                                      entropy_coeff, lambda_, clip_rho, clip_pg_rho,
+                                      _lib.vtrace_grad_mode(grad_mode), ptr(dl),
                                       ptr(dv), ptr(met), ptr(adv), ptr(err), ptr(q), ptr(rho),
                                       stream_ptr(stream)), "impala_loss_head")
     return dict(dlogits=dl, dvalues=dv, metrics=met, adv=adv, err=err, q=q, rho=rho)

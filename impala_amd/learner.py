@@ -64,7 +64,14 @@ class ImpalaLearner(Learner):
                  max_grad_norm: float = 0.5, entropy_coeff: float = 0.01,
                  learning_starts: Optional[int] = None, model_push_period: int = 4,
                  rollout_length: int = 20, dtype: Optional[str] = None,
-                 process_group=None, world_size: Optional[int] = None):
+                 process_group=None, world_size: Optional[int] = None,
+                 vtrace_grad_mode: Optional[str] = None):
+        """The reference's constructor (learning.py:88-96) plus keyword-only extensions:
+        ``rollout_length``, ``dtype`` ("fp32" | "bf16"), the data-parallel ``process_group`` /
+        ``world_size``, and ``vtrace_grad_mode`` -- what the V-trace backward treats as constant
+        (``_lib.VTRACE_GRAD_MODES``; default "sg_advantage": targets and pg advantages constant,
+        SURVEY.md §8(c); "sg_targets" / "sg_none" for rlax's stop_target_gradients=True / False
+        with the advantage live)."""
         self._model = model
         self._replay_buffer = replay_buffer
         if optimizer is None:
@@ -93,7 +100,8 @@ class ImpalaLearner(Learner):
         self._engine = Engine(model, batch_size=batch_size, rollout_length=rollout_length,
                               dtype=dtype, lr=optimizer.lr, eps=optimizer.eps,
                               betas=optimizer.betas, max_grad_norm=max_grad_norm,
-                              entropy_coeff=entropy_coeff, world_size=self._world_size)
+                              entropy_coeff=entropy_coeff, world_size=self._world_size,
+                              vtrace_grad_mode=vtrace_grad_mode)
         model._train_engine = self._engine
 
     @property
@@ -183,9 +191,10 @@ class ImpalaLearner(Learner):
             from .distributed import (compute_grads_allreduced, native_dp_buckets,
                                       native_dp_enabled)
             if self._native_dp is None:
-                self._native_dp = native_dp_enabled(self._pg)
-                if self._native_dp:
-                    e.dp_init(self._pg)
+                native = native_dp_enabled(self._pg)
+                if native:
+                    e.dp_init(self._pg)  # raises before the path is chosen if RCCL fails
+                self._native_dp = native
             if self._native_dp:
                 e.dp_train_step(*batch, buckets=native_dp_buckets())
             else:

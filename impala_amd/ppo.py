@@ -137,9 +137,10 @@ class PPOLearner(Learner):
             from .distributed import (compute_grads_allreduced, native_dp_buckets,
                                       native_dp_enabled)
             if self._native_dp is None:
-                self._native_dp = native_dp_enabled(self._pg)
-                if self._native_dp:
-                    e.dp_init(self._pg)
+                native = native_dp_enabled(self._pg)
+                if native:
+                    e.dp_init(self._pg)  # raises before the path is chosen if RCCL fails
+                self._native_dp = native
             if self._native_dp:
                 e.dp_train_step(*batch, buckets=native_dp_buckets())
             else:

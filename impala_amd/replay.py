@@ -117,6 +117,12 @@ class DeviceReplayBuffer(ReplayBuffer):
         # queued gather still reads (gathers run in order on the learner's stream, so waiting
         # for the latest one covers every earlier read)
         self._last_read: Optional[torch.cuda.Event] = None
+        # page-locked ring for the sampled slot indices: their H2D is a true asynchronous copy
+        # (from pageable memory it would wait behind the learner stream's queued work while
+        # sample() holds the lock); a ring entry is reused after its copy has run
+        self._idx_buf: List[Optional[torch.Tensor]] = [None] * 4
+        self._idx_ev: List[Optional[torch.cuda.Event]] = [None] * 4
+        self._idx_next = 0
 
     def append(self, item: Sequence[torch.Tensor]) -> int:
         s, a, r, g, mu = item
@@ -155,6 +161,28 @@ class DeviceReplayBuffer(ReplayBuffer):
             self._cv.notify_all()
             return key
 
+    def _indices_to_device(self, idx: np.ndarray, stream) -> torch.Tensor:
+        """Slot indices -> a device int64 tensor, copied on `stream` from a page-locked ring
+        entry (asynchronous: nothing here waits for the stream's queued work)."""
+        k = self._idx_next
+        self._idx_next = (k + 1) % len(self._idx_buf)
+        ev = self._idx_ev[k]
+        if ev is not None:
+            ev.synchronize()  # the entry's previous copy (4 samples ago) has run
+        n = len(idx)
+        buf = self._idx_buf[k]
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(n, dtype=torch.int64, pin_memory=torch.cuda.is_available())
+            self._idx_buf[k] = buf
+        host = buf[:n]
+        host.copy_(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)))
+        with torch.cuda.stream(stream):
+            dev = host.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self._idx_ev[k] = ev
+        return dev
+
     def sample(self, batch_size: int, stream=None):
         """-> (keys, (obs, act, rew, disc, mu) collated on the device, probs).
 
@@ -171,7 +199,7 @@ class DeviceReplayBuffer(ReplayBuffer):
             pending, self._pending = self._pending, []
             for ev in pending:  # the learner's stream waits for every staged H2D
                 cur.wait_event(ev)
-            idx_t = torch.from_numpy(idx.astype(np.int64)).to(self.device, non_blocking=True)
+            idx_t = self._indices_to_device(idx, cur)
             batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx_t,
                                     stream)
             read = torch.cuda.Event()

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define IMPALA_ABI_VERSION 2
+#define IMPALA_ABI_VERSION 3
 
 #define IMPALA_OK 0
 #define IMPALA_E_INVALID 1001   /* bad argument / shape */
@@ -72,6 +72,20 @@ extern "C" {
 #define IMPALA_ALGO_IMPALA 0    /* V-trace actor-critic (agents/impala/learning.py:140-177) */
 #define IMPALA_ALGO_PPO 1       /* PPO clipped surrogate (agents/ppo/learning.py:131-143) */
 
+/* V-trace gradient semantics.  learning.py:148-155 detaches neither rho nor
+ * the advantage it multiplies into pg_loss; which V-trace quantities are constants is decided
+ * inside the third-party rlego.vtrace_td_error_and_advantage (absent, unpinned).  Forward values
+ * do not depend on the mode.
+ *   SG_ADVANTAGE targets and pg advantages constant (default): SURVEY.md §8(c)'s restatement,
+ *                the IMPALA paper's estimator
+ *   SG_TARGETS   rlax vtrace_td_error_and_advantage(stop_target_gradients=True) taken literally
+ *                with the reference's un-detached advantage: extra terms through
+ *                min(clip_pg_rho, rho), v_tm1 and the bootstrap v_t[-1]
+ *   SG_NONE      stop_target_gradients=False: gradients through the whole V-trace scan */
+#define IMPALA_VTRACE_SG_ADVANTAGE 0
+#define IMPALA_VTRACE_SG_TARGETS 1
+#define IMPALA_VTRACE_SG_NONE 2
+
 typedef struct impala_learner impala_learner;
 
 typedef struct {
@@ -88,6 +102,7 @@ typedef struct {
   int world_size;              /* data-parallel replicas (gradient average divisor)          */
   int algo;                    /* IMPALA_ALGO_*; PPO needs rollout_length 1 (flat transitions) */
   float ppo_clip;              /* losses.py:131 clip_coeff 0.1                               */
+  int vtrace_grad_mode;        /* IMPALA_VTRACE_SG_*, default IMPALA_VTRACE_SG_ADVANTAGE      */
 } impala_config;
 
 typedef struct {
@@ -191,6 +206,9 @@ size_t impala_grad_bucket_offset_fc(const impala_learner* h);
 #define IMPALA_DP_ID_BYTES 128
 int impala_dp_unique_id(void* out);
 int impala_dp_init(impala_learner* h, const void* unique_id, int nranks, int rank);
+/* *nranks = the rank count of the handle's RCCL communicator (ncclCommCount), 0 before
+ * impala_dp_init: the bench records it so a multi-GPU result shows RCCL saw every rank. */
+int impala_dp_nranks(const impala_learner* h, int* nranks);
 /* buckets 1: the whole backward, then one in-place ncclAllReduce(sum) of the flat gradient on
  * `stream`, then the update.  buckets 2: part 2 (forward, heads step, FC gradients), whose FC +
  * heads gradient (1.07 MB) is all-reduced on the handle's side stream while part 6 (the
@@ -243,13 +261,14 @@ int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const 
                   float* q_estimate, void* stream);
 
 /* Standalone fused loss head given network outputs: logits [B][T][A], values [B][T].
- * Writes dlogits [B][T][A], dvalues [B][T], metrics[6] (loss, entropy, td, pg, kl, ratio),
- * and optionally (nullable) adv/err/q [B][T-1], rho [B][T]. */
+ * Writes dlogits [B][T][A], dvalues [B][T] (under vtrace_grad_mode, IMPALA_VTRACE_SG_*),
+ * metrics[6] (loss, entropy, td, pg, kl, ratio), and optionally (nullable) adv/err/q [B][T-1],
+ * rho [B][T]. */
 int impala_loss_head(const float* logits, const float* values, const int64_t* actions,
                      const float* rewards, const float* discounts, const float* behaviour_logits,
                      int B, int T, int A, float entropy_coeff, float lambda_, float clip_rho,
-                     float clip_pg_rho, float* dlogits, float* dvalues, float* metrics6,
-                     float* adv, float* err, float* q, float* rho, void* stream);
+                     float clip_pg_rho, int vtrace_grad_mode, float* dlogits, float* dvalues,
+                     float* metrics6, float* adv, float* err, float* q, float* rho, void* stream);
 
 /* Standalone PPO loss head (losses.py:131-155) given outputs: logits [N][A], values [N].
  * Writes dlogits [N][A], dvalues [N] and metrics7 (loss, entropy, td, pg, kl, ratio, target). */

@@ -31,7 +31,7 @@ try:  # functorch.vmap as at agents/impala/learning.py:15-18
 except Exception:  # pragma: no cover
     _vmap = None
 
-from oracle.vtrace import vtrace_td_error_and_advantage
+from oracle.vtrace import DEFAULT_GRAD_MODE, mode_kwargs, vtrace_td_error_and_advantage
 
 # state_dict key order == flat parameter order
 PARAM_SPECS: List[Tuple[str, Tuple[int, ...]]] = [
@@ -153,12 +153,14 @@ def collate(batch: Sequence[Sequence[torch.Tensor]]):
 
 def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
                max_grad_norm: float = 0.5, entropy_coeff: float = 0.01,
-               collated: bool = False, capture: Optional[dict] = None) -> Dict[str, torch.Tensor]:
+               collated: bool = False, capture: Optional[dict] = None,
+               grad_mode: str = DEFAULT_GRAD_MODE) -> Dict[str, torch.Tensor]:
     """agents/impala/learning.py:140-177 restated. ``batch`` = list of B trajectories
     ``[s u8 (T,3,64,64), a i64 (T,1), r f32 (T,1), g f32 (T,1), mu f32 (T,A)]``
     (format of ``ImpalaActor._make_replay``, learning.py:77-80), or already-collated
     ``(s, a, r, g, mu)`` tensors when ``collated``.  ``capture`` (a dict) receives the step's
-    intermediate values: logits, values, rho, and the V-trace adv / err / q."""
+    intermediate values: logits, values, rho, and the V-trace adv / err / q.  ``grad_mode``:
+    the V-trace gradient semantics (oracle/vtrace.py GRAD_MODES)."""
     optimizer.zero_grad(set_to_none=True)
     s, a, r, discount_t, pi_ref = batch if collated else collate(batch)
     pi, values = model.forward(s.flatten(0, 1))
@@ -168,7 +170,7 @@ def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
     pi_ref = torch.distributions.Categorical(logits=pi_ref)
     rho_tm1 = torch.exp(pi.log_prob(a) - pi_ref.log_prob(a))
     adv, err, q = batched_vtrace(values[:, :-1], values[:, 1:], r[:, :-1],
-                                 discount_t[:, :-1], rho_tm1[:, :-1])
+                                 discount_t[:, :-1], rho_tm1[:, :-1], **mode_kwargs(grad_mode))
     if capture is not None:
         capture.update(logits=pi.logits.detach().clone(), values=values.detach().clone(),
                        rho=rho_tm1.detach().clone(), adv=adv.detach().clone(),
@@ -193,7 +195,7 @@ def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
 
 
 def train_step_fp64(flat: np.ndarray, batch_np, A: int = 15, steps: int = 1,
-                    capture: Optional[dict] = None):
+                    capture: Optional[dict] = None, grad_mode: str = DEFAULT_GRAD_MODE):
     """The same step in float64 (model, batch floats, autograd, Adam): the exact-arithmetic
     yardstick against which both the fp32 oracle and the HIP fp32 path are measured.
     -> (final flat params, flat post-clip grads (p.grad after clip_grad_norm_) of the last step, metrics of the last step)."""
@@ -213,7 +215,7 @@ def train_step_fp64(flat: np.ndarray, batch_np, A: int = 15, steps: int = 1,
              torch.from_numpy(rew.astype(np.float64)), torch.from_numpy(disc.astype(np.float64)),
              torch.from_numpy(mu.astype(np.float64))]
         for _ in range(steps):
-            met = train_step(ref, opt, b, collated=True, capture=capture)
+            met = train_step(ref, opt, b, collated=True, capture=capture, grad_mode=grad_mode)
         grads = torch.cat([p.grad.detach().reshape(-1) for p in ref.parameters()]).numpy().copy()
         params = torch.cat([p.detach().reshape(-1) for p in ref.parameters()]).numpy().copy()
         return params, grads, {k: float(v) for k, v in met.items()}
@@ -221,7 +223,8 @@ def train_step_fp64(flat: np.ndarray, batch_np, A: int = 15, steps: int = 1,
         torch.set_default_dtype(prev)
 
 
-def local_grads(model: nn.Module, batch_collated, entropy_coeff: float = 0.01) -> np.ndarray:
+def local_grads(model: nn.Module, batch_collated, entropy_coeff: float = 0.01,
+                grad_mode: str = DEFAULT_GRAD_MODE) -> np.ndarray:
     """Loss + backward only (learning.py:141-160), no clip / Adam: the per-replica gradient of
     the data-parallel learner (mean over the LOCAL batch)."""
     model.zero_grad(set_to_none=True)
@@ -232,7 +235,7 @@ def local_grads(model: nn.Module, batch_collated, entropy_coeff: float = 0.01) -
     pim = torch.distributions.Categorical(logits=pi_ref)
     rho = torch.exp(pi.log_prob(a) - pim.log_prob(a))
     adv, err, _ = batched_vtrace(values[:, :-1], values[:, 1:], r[:, :-1], discount_t[:, :-1],
-                                 rho[:, :-1])
+                                 rho[:, :-1], **mode_kwargs(grad_mode))
     loss = -(pi.log_prob(a)[:, :-1] * adv).mean() + err.pow(2).mean() \
         - entropy_coeff * pi.entropy().mean()
     loss.backward()
@@ -271,22 +274,24 @@ def forward_numpy(model: nn.Module, obs_u8: np.ndarray):
 
 
 def loss_from_outputs(logits, values, act, rew, disc, mu, entropy_coeff=0.01,
-                      lambda_=1.0, clip_rho=1.0, clip_pg_rho=1.0):
+                      lambda_=1.0, clip_rho=1.0, clip_pg_rho=1.0, grad_mode=DEFAULT_GRAD_MODE,
+                      dtype=torch.float32):
     """Head-only restatement (learning.py:144-159) given the network outputs, returning
     every intermediate plus the analytic gradient w.r.t. (logits, values) via autograd.
     Used to check the fused V-trace/loss kernel in isolation."""
-    lg = torch.tensor(logits, dtype=torch.float32, requires_grad=True)
-    v = torch.tensor(values, dtype=torch.float32, requires_grad=True)
+    npd = np.float64 if dtype == torch.float64 else np.float32
+    lg = torch.tensor(np.asarray(logits, npd), dtype=dtype, requires_grad=True)
+    v = torch.tensor(np.asarray(values, npd), dtype=dtype, requires_grad=True)
     a = torch.from_numpy(np.asarray(act, dtype=np.int64))
-    r = torch.from_numpy(np.asarray(rew, dtype=np.float32))
-    g = torch.from_numpy(np.asarray(disc, dtype=np.float32))
-    pr = torch.from_numpy(np.asarray(mu, dtype=np.float32))
+    r = torch.from_numpy(np.asarray(rew, dtype=npd))
+    g = torch.from_numpy(np.asarray(disc, dtype=npd))
+    pr = torch.from_numpy(np.asarray(mu, dtype=npd))
     pi = torch.distributions.Categorical(logits=lg)
     pim = torch.distributions.Categorical(logits=pr)
     rho = torch.exp(pi.log_prob(a) - pim.log_prob(a))
     adv, err, q = batched_vtrace(v[:, :-1], v[:, 1:], r[:, :-1], g[:, :-1], rho[:, :-1],
                                  lambda_=lambda_, clip_rho_threshold=clip_rho,
-                                 clip_pg_rho_threshold=clip_pg_rho)
+                                 clip_pg_rho_threshold=clip_pg_rho, **mode_kwargs(grad_mode))
     pg = (pi.log_prob(a)[:, :-1] * adv).mean()
     vl = err.pow(2).mean()
     ent = pi.entropy().mean()

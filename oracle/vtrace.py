@@ -17,6 +17,20 @@ rlego is a PyTorch port of rlax building blocks, so this restates rlax's publish
 from the reference's four consistent unpackings ``adv, err, _`` (``learning.py:150``,
 ``losses.py:38,73,106``): ``(pg_advantage, td_error, q_estimate)``.
 
+Gradient semantics (forward values do not depend on them).  rlax's function
+stops gradients through the TARGETS only (``stop_target_gradients``); its pg advantage
+``min(clip_pg_rho, rho) * (q - v_tm1)`` stays differentiable, and learning.py:148-155 detaches
+neither rho nor the advantage.  ``GRAD_MODES`` names the three semantics the HIP learner
+implements (``IMPALA_VTRACE_SG_*``); ``mode_kwargs`` maps a name to this function's flags:
+
+* ``sg_advantage`` -- the default: ``stop_target_gradients=True`` and
+  ``stop_advantage_gradients=True`` (the latter is not an rlax flag): targets and advantages
+  constant, SURVEY.md §8(c)'s restatement (``adv_t = sg(...)``) and the IMPALA paper's
+  estimator
+* ``sg_targets``   -- ``stop_target_gradients=True`` alone (rlax's function taken literally,
+  with the advantage learning.py:155 multiplies in left live)
+* ``sg_none``      -- ``stop_target_gradients=False``
+
 Per trajectory, t = 0 .. L-1 (L = T-1 in the learner)::
 
     c_t      = lambda * min(1, rho_t)
@@ -26,7 +40,7 @@ Per trajectory, t = 0 .. L-1 (L = T-1 in the learner)::
     err_t    = target_t - v_tm1[t]
     q_t      = r_t + g_t * (lambda * target_{t+1} + (1 - lambda) * v_tm1[t+1])   t < L-1
     q_{L-1}  = r_{L-1} + g_{L-1} * v_t[L-1]
-    adv_t    = sg(min(clip_pg_rho, rho_t) * (q_t - v_tm1[t]))
+    adv_t    = min(clip_pg_rho, rho_t) * (q_t - v_tm1[t])     (sg only in sg_advantage)
 
 Parity status: forward values are pinned only by this restatement (SURVEY.md §8(c):
 "parity unpinned at the rlego boundary"); everything around it is pinned by the
@@ -38,10 +52,24 @@ import numpy as np
 import torch
 
 
+GRAD_MODES = ("sg_advantage", "sg_targets", "sg_none")
+DEFAULT_GRAD_MODE = "sg_advantage"
+
+
+def mode_kwargs(mode: str) -> dict:
+    """Gradient-mode name (GRAD_MODES) -> flags of vtrace_td_error_and_advantage."""
+    if mode not in GRAD_MODES:
+        raise ValueError(f"unknown V-trace gradient mode {mode!r}")
+    return {"sg_targets": dict(stop_target_gradients=True),
+            "sg_advantage": dict(stop_target_gradients=True, stop_advantage_gradients=True),
+            "sg_none": dict(stop_target_gradients=False)}[mode]
+
+
 def vtrace_td_error_and_advantage(v_tm1, v_t, r_t, discount_t, rho_tm1,
                                   lambda_=1.0, clip_rho_threshold=1.0,
                                   clip_pg_rho_threshold=1.0,
-                                  stop_target_gradients=True):
+                                  stop_target_gradients=True,
+                                  stop_advantage_gradients=False):
     """Single trajectory (1-D tensors of length L).  torch, vmap-compatible.
 
     Returns ``(pg_advantage, td_error, q_estimate)`` (order per learning.py:150).
@@ -63,7 +91,7 @@ def vtrace_td_error_and_advantage(v_tm1, v_t, r_t, discount_t, rho_tm1,
     boot = torch.cat([lam * target[1:] + (1.0 - lam) * v_tm1[1:], v_t[-1:]], dim=0)
     q = r_t + discount_t * boot
     adv = torch.clamp(rho_tm1, max=clip_pg_rho_threshold) * (q - v_tm1)
-    if stop_target_gradients:
+    if stop_advantage_gradients:
         adv = adv.detach()
     err = target - v_tm1
     return adv, err, q

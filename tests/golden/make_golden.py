@@ -15,16 +15,21 @@ provided by the oracle's restatement ``oracle/vtrace.py`` — so the V-trace ari
 the reference's own code (``agents/impala/learning.py:140-177``,
 ``models/models.py:61-76``, ``models/common.py:108-158``).
 
+The rlego stub runs under one of the V-trace gradient modes (``oracle/vtrace.py``
+``GRAD_MODES``: what rlego's function holds constant -- the forward values are the same in all
+three), and the gradient-carrying fixtures are written once per mode, each from the reference
+learner running with the matching stub.
+
 Fixtures written (all float32 unless stated):
 
 * ``vtrace_random.npz``  G1: B=64, L=19 random V-trace inputs (rho in [0.1,3], ~5% zero
   discounts) for lambda 1.0 and 0.95, outputs from the float64 numpy restatement.
 * ``model_forward.npz``  G2: reference ``AtariPPOModel`` (seed-0 init) flat params, obs
   (2*20 frames), logits, values.
-* ``train_step.npz``     G3/G4: reference ``ImpalaLearner`` with Adam(1e-4, 1e-5), B=2, T=20:
-  three consecutive ``_train_step`` calls on three batches; metrics per step, flat
+* ``train_step_<mode>.npz``  G3/G4: reference ``ImpalaLearner`` with Adam(1e-4, 1e-5), B=2,
+  T=20: three consecutive ``_train_step`` calls on three batches; metrics per step, flat
   post-clip grads and flat params after step 1, flat params after step 3.
-* ``head_loss.npz``      the loss head alone (learning.py:144-159) at B=64,T=20 on random
+* ``head_loss_<mode>.npz``   the loss head alone (learning.py:144-159) at B=64,T=20 on random
   logits/values, with d(loss)/d(logits), d(loss)/d(values) from the reference's autograd.
 """
 from __future__ import annotations
@@ -85,7 +90,13 @@ def _install_stubs():
                              map_nested=map_nested, unbatch_nested=unbatch_nested)
     mod("moolib", Batcher=object)
     mod("envs", EnvSpec=object)
-    mod("rlego", vtrace_td_error_and_advantage=ovt.vtrace_td_error_and_advantage)
+    def rlego_vtrace(*args, **kw):  # rlego.vtrace_td_error_and_advantage under _MODE
+        return ovt.vtrace_td_error_and_advantage(*args, **{**ovt.mode_kwargs(_MODE[0]), **kw})
+
+    mod("rlego", vtrace_td_error_and_advantage=rlego_vtrace)
+
+
+_MODE = [ovt.DEFAULT_GRAD_MODE]  # the stub's gradient mode (read at every call)
 
 
 def _import_reference():
@@ -173,7 +184,7 @@ def _traj(obs, act, rew, disc, mu):
              torch.from_numpy(mu[b])] for b in range(obs.shape[0])]
 
 
-def gen_model_and_step(out, dm, il):
+def gen_model_and_step(out, dm, il, mode):
     A = 15
     torch.manual_seed(0)
     model = dm.AtariPPOModel((3, 64, 64), A)
@@ -182,9 +193,10 @@ def gen_model_and_step(out, dm, il):
     obs, *_ = _synthetic(2, 20, A, 99)
     with torch.no_grad():
         lg, v = model(torch.from_numpy(obs.reshape(-1, 3, 64, 64)))
-    np.savez_compressed(os.path.join(out, "model_forward.npz"), params=params0,
-                        obs=obs.reshape(-1, 3, 64, 64), logits=lg.numpy(), values=v.numpy(),
-                        keys=np.array(keys))
+    if mode == ovt.DEFAULT_GRAD_MODE:
+        np.savez_compressed(os.path.join(out, "model_forward.npz"), params=params0,
+                            obs=obs.reshape(-1, 3, 64, 64), logits=lg.numpy(),
+                            values=v.numpy(), keys=np.array(keys))
 
     B, T = 2, 20
     batches = [_synthetic(B, T, A, 1234 + i) for i in range(3)]
@@ -204,12 +216,12 @@ def gen_model_and_step(out, dm, il):
     arrays = {f"obs{i}": b[0] for i, b in enumerate(batches)}
     for i, b in enumerate(batches):
         arrays[f"act{i}"], arrays[f"rew{i}"], arrays[f"disc{i}"], arrays[f"mu{i}"] = b[1:]
-    np.savez_compressed(os.path.join(out, "train_step.npz"), params0=params0,
+    np.savez_compressed(os.path.join(out, f"train_step_{mode}.npz"), params0=params0,
                         **arrays, **{k: np.asarray(v, dtype=np.float32) if isinstance(v, list)
                                      else v for k, v in res.items()})
 
 
-def gen_head_loss(out, il):
+def gen_head_loss(out, il, mode):
     """learning.py:144-159 given network outputs; autograd grads of the loss."""
     rng = np.random.default_rng(11)
     B, T, A = 64, 20, 15
@@ -233,7 +245,7 @@ def gen_head_loss(out, il):
     loss = -pg + vl - 0.01 * ent
     loss.backward()
     kl = torch.distributions.kl_divergence(pi, pi_ref).mean()
-    np.savez_compressed(os.path.join(out, "head_loss.npz"), logits=logits, values=values,
+    np.savez_compressed(os.path.join(out, f"head_loss_{mode}.npz"), logits=logits, values=values,
                         act=act, rew=rew, disc=disc, mu=mu, adv=adv.detach().numpy(),
                         err=err.detach().numpy(), q=q.detach().numpy(),
                         rho=rho_tm1.detach().numpy(),
@@ -246,8 +258,10 @@ def main():
     torch.set_num_threads(max(1, min(8, os.cpu_count() or 1)))
     dm, il = _import_reference()
     gen_vtrace(HERE)
-    gen_head_loss(HERE, il)
-    gen_model_and_step(HERE, dm, il)
+    for mode in ovt.GRAD_MODES:
+        _MODE[0] = mode
+        gen_head_loss(HERE, il, mode)
+        gen_model_and_step(HERE, dm, il, mode)
     print("golden fixtures written to", HERE)
 
 

@@ -57,3 +57,67 @@ def test_multi_gpu_spawns_child_and_relays_status(monkeypatch):
 def test_host_cpu_budget():
     h = bench.host_cpu_info()
     assert 1 <= h["baseline_threads"] <= h["physical_cores_allowed"] <= h["cpus_allowed"]
+
+
+def test_dp_variant_record_shape():
+    """The N-GPU sub-record: every arrangement timed, the native ones with the
+    communicator's rank count, each with the cross-rank and cross-variant bitwise checks."""
+    assert [v[0] for v in bench.DP_VARIANTS] == ["c10d_1bucket", "native_1bucket",
+                                                 "native_2bucket"]
+    rec = bench.dp_variant_record("native_1bucket", 0.05, 200, 1280, 8, nranks=8,
+                                  replicas_equal=True, equal_to_default=True)
+    assert rec == {"ms_per_step": 0.25, "value": 8 * 1280 * 200 / 0.05,
+                   "replicas_bitwise_equal": True, "rccl_nranks": 8,
+                   "bitwise_equal_to_c10d_1bucket": True}
+    base = bench.dp_variant_record("c10d_1bucket", 0.05, 200, 1280, 8, replicas_equal=True)
+    assert "rccl_nranks" not in base and "bitwise_equal_to_c10d_1bucket" not in base
+
+
+def test_frac_mix_of_the_executed_instruction_mix():
+    """conv1's FLOPs count three times at the bf16 rate in the fp32 step, the
+    rest at the fp32 rate; the step's floor is ~108 us at C2 (84.3 ns per frame)."""
+    w = bench.kernel_work(4)
+    mix = bench.kernel_mix("ln_conv3_conv2_dgrad_conv1_wgrad", w, "fp32")
+    assert mix["bf16"] == 3 * bench.CONV1_FLOPS
+    assert mix["fp32"] + bench.CONV1_FLOPS == w["ln_conv3_conv2_dgrad_conv1_wgrad"][0]
+    assert abs(bench.mix_floor_s(mix, 1280) * 1e6 - 33.13) < 0.05
+    assert bench.kernel_mix("fc_fwd", w, "fp32") == {"fp32": w["fc_fwd"][0], "bf16": 0}
+    assert bench.kernel_mix("fc_fwd", bench.kernel_work(2), "bf16")["fp32"] == 0
+    sr = bench.step_roofline(5.08e6, bench.STEP_FLOPS_PER_FRAME, "fp32")
+    assert abs(sr["mix_per_frame"]["floor_us_per_frame"] * 1280 - 107.9) < 0.2
+    assert abs(sr["frac_mix"] - 0.428) < 0.002
+
+
+def _fingerprint_worker(rank, world, port, q):
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = torch.arange(1000, dtype=torch.float32) / 7
+    same = bench.replicas_bitwise_equal(x, dist)
+    if rank == 1:
+        x[123] = torch.nextafter(x[123], torch.tensor(1e9))
+    differ = bench.replicas_bitwise_equal(x, dist)
+    q.put((rank, same, differ))
+    dist.destroy_process_group()
+
+
+def test_replicas_bitwise_equal_over_gloo():
+    """The cross-rank check the N-GPU record carries, at world size 2 on the CPU: equal
+    buffers agree, a one-ulp difference on one rank is caught."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_fingerprint_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert res == [(0, True, False), (1, True, False)]

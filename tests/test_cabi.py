@@ -35,13 +35,14 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     lib = _lib.lib()
-    assert lib.impala_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.impala_abi_version() == _lib.ABI_VERSION == 3
     assert _lib.param_count(15) == 344496
     assert _lib.param_count(6) == 344496 - 9 * 257
     cfg = _lib.default_config()
     assert (cfg.batch_size, cfg.rollout_length, cfg.num_actions) == (8, 20, 15)
     assert abs(cfg.lr - 1e-4) < 1e-9 and abs(cfg.adam_eps - 1e-5) < 1e-12
     assert abs(cfg.max_grad_norm - 0.5) < 1e-9 and abs(cfg.entropy_coeff - 0.01) < 1e-9
+    assert cfg.vtrace_grad_mode == _lib.VTRACE_GRAD_MODES["sg_advantage"] == 0
     names = [lib.impala_kernel_name(i).decode() for i in range(lib.impala_kernel_count())]
     assert "conv2_dgrad_conv1_wgrad" in names and "adam" in names and len(names) == len(set(names))
 
@@ -49,7 +50,8 @@ def test_host_only_entry_points():
 @pytest.mark.parametrize("field,value", [("batch_size", 0), ("rollout_length", 1),
                                          ("rollout_length", 65), ("num_actions", 16),
                                          ("num_actions", 0), ("dtype", 7), ("world_size", 0),
-                                         ("algo", 5), ("ppo_clip", 1.5)])
+                                         ("algo", 5), ("ppo_clip", 1.5),
+                                         ("vtrace_grad_mode", 3), ("vtrace_grad_mode", -1)])
 def test_create_rejects_bad_config_without_touching_the_device(field, value):
     lib = _lib.lib()
     cfg = _lib.default_config()
@@ -67,7 +69,9 @@ def test_kernel_entry_points_validate_before_launch():
                              None, None) == 1001
     assert lib.impala_vtrace(None, None, None, None, None, 4, 65, 1.0, 1.0, 1.0, None, None,
                              None, None) == 1001
-    assert lib.impala_loss_head(*([None] * 6), 2, 1, 15, 0.01, 1.0, 1.0, 1.0,
+    assert lib.impala_loss_head(*([None] * 6), 2, 1, 15, 0.01, 1.0, 1.0, 1.0, 1,
+                                *([None] * 8)) == 1001
+    assert lib.impala_loss_head(*([None] * 6), 2, 20, 15, 0.01, 1.0, 1.0, 1.0, 9,
                                 *([None] * 8)) == 1001
     assert lib.impala_train_step(None, None, None) == 1001
     assert lib.impala_forward(None, None, 1, None, None, None) == 1001

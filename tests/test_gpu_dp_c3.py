@@ -144,8 +144,57 @@ def test_native_rccl_world1_step_is_bitwise_train_step(dtype, buckets, tmp_path)
     side stream) at world size 1: the in-place all-reduces are the identity, so three steps
     must equal impala_train_step bit for bit (params, Adam moments, grads, metrics)."""
     _dev()
-    _launch(tmp_path, NATIVE_WORKER, 1, {"DTYPE": dtype, "BUCKETS": str(buckets)})
+    _launch(tmp_path, NATIVE_WORKER, 1, {"DTYPE": dtype, "BUCKETS": str(buckets),
+                                         "IMPALA_DP_NATIVE": "1"})
     res = json.load(open(tmp_path / "native.json"))
+    assert all(res.values()), res
+
+
+PPO_NATIVE_WORKER = r"""
+import os, sys, json, numpy as np, torch
+sys.path.insert(0, os.environ["IMPALA_ROOT"])
+import torch.distributed as dist
+from oracle import ref_cpu
+from impala_amd.distributed import init_process_group
+from impala_amd.engine import Engine
+from impala_amd.model import AtariPPOModel
+group = init_process_group("nccl")
+dev = torch.device("cuda:0")
+buckets = int(os.environ["BUCKETS"])
+N = 256
+batches = [[torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+            for x in ref_cpu.synthetic_ppo_batch(N, 15, seed=90 + s)] for s in range(3)]
+def make():
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+    e = Engine(m, batch_size=N, algo="ppo")
+    m._train_engine = e
+    return m, e
+m1, e1 = make()
+m2, e2 = make()
+e2.dp_init(group)
+for b in batches:
+    e1.train_step(*b)
+    e2.dp_train_step(*b, buckets=buckets)
+torch.cuda.synchronize()
+res = {"params_equal": bool(torch.equal(m1.flat, m2.flat)),
+       "metrics_equal": bool(torch.equal(e1.metrics, e2.metrics)),
+       "grads_equal": bool(torch.equal(m1.flat_grad, m2.flat_grad)),
+       "moments_equal": bool(torch.equal(e1.exp_avg, e2.exp_avg) and
+                             torch.equal(e1.exp_avg_sq, e2.exp_avg_sq))}
+json.dump(res, open(os.path.join(os.environ["OUT"], "ppo_native.json"), "w"))
+e2.close()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("buckets", [1, 2])
+def test_native_rccl_world1_ppo_step_is_bitwise_train_step(buckets, tmp_path):
+    """The PPO learner (BASELINE config 4) through impala_dp_train_step at world size 1:
+    three steps bit-identical to impala_ppo_train_step (the PPO data-parallel
+    step through the native communicator was untested)."""
+    _dev()
+    _launch(tmp_path, PPO_NATIVE_WORKER, 1, {"BUCKETS": str(buckets), "IMPALA_DP_NATIVE": "1"})
+    res = json.load(open(tmp_path / "ppo_native.json"))
     assert all(res.values()), res
 
 

@@ -41,8 +41,9 @@ def test_seed0_init_matches_reference():
     np.testing.assert_allclose(ref_cpu.flat_params(m), d["params"], rtol=1e-6, atol=1e-9)
 
 
-def test_train_steps_match_reference():
-    d = _load("train_step.npz")
+@pytest.mark.parametrize("mode", ovt.GRAD_MODES)
+def test_train_steps_match_reference(mode):
+    d = _load(f"train_step_{mode}.npz")
     m = ref_cpu.RefModel()
     ref_cpu.load_flat(m, d["params0"])
     opt = ref_cpu.make_optimizer(m)
@@ -50,7 +51,7 @@ def test_train_steps_match_reference():
     for i in range(3):
         batch = ref_cpu.to_trajectories(d[f"obs{i}"], d[f"act{i}"], d[f"rew{i}"],
                                         d[f"disc{i}"], d[f"mu{i}"])
-        met = ref_cpu.train_step(m, opt, batch)
+        met = ref_cpu.train_step(m, opt, batch, grad_mode=mode)
         got = np.array([float(met["train/" + k]) for k in names])
         exp = np.array([d[k][i] for k in names])
         np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-6)
@@ -60,10 +61,11 @@ def test_train_steps_match_reference():
     np.testing.assert_allclose(ref_cpu.flat_params(m), d["params3"], rtol=0, atol=1e-7)
 
 
-def test_head_loss_matches_reference():
-    d = _load("head_loss.npz")
+@pytest.mark.parametrize("mode", ovt.GRAD_MODES)
+def test_head_loss_matches_reference(mode):
+    d = _load(f"head_loss_{mode}.npz")
     out = ref_cpu.loss_from_outputs(d["logits"], d["values"], d["act"], d["rew"], d["disc"],
-                                    d["mu"])
+                                    d["mu"], grad_mode=mode)
     for k in ("adv", "err", "q", "rho", "dlogits", "dvalues"):
         np.testing.assert_allclose(out[k], d[k], rtol=1e-5, atol=1e-7, err_msg=k)
     got = [out[k] for k in ("loss", "entropy", "td", "pg", "kl", "ratio")]
@@ -80,6 +82,19 @@ def test_vtrace_golden(tag, lam):
     np.testing.assert_allclose(adv, d[f"adv_{tag}"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(err, d[f"err_{tag}"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(q, d[f"q_{tag}"], rtol=1e-5, atol=1e-6)
+
+
+def test_grad_modes_forward_identical_gradients_differ():
+    """The gradient mode changes only what the backward holds constant: the fixtures of the
+    three modes share every forward value and differ in the gradients."""
+    ds = {m: _load(f"head_loss_{m}.npz") for m in ovt.GRAD_MODES}
+    a = ds[ovt.GRAD_MODES[0]]
+    for m, d in ds.items():
+        for k in ("adv", "err", "q", "rho", "scalars"):
+            np.testing.assert_array_equal(d[k], a[k], err_msg=(m, k))
+    for k in ("dlogits", "dvalues"):
+        assert not np.array_equal(ds["sg_targets"][k], ds["sg_advantage"][k]), k
+        assert not np.array_equal(ds["sg_none"][k], ds["sg_targets"][k]), k
 
 
 def test_vtrace_known_answers():
