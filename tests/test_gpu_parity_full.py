@@ -96,8 +96,9 @@ def _run(B, mode=DEFAULT_GRAD_MODE, T=20, A=15, seed=1234):
           "native": _oracle32(flat0, batch, A, native=True, mode=mode)}
     cap64 = {}
     p64, g64, met64 = ref_cpu.train_step_fp64(flat0, batch, A, capture=cap64, grad_mode=mode)
+    p64_3, _, _ = ref_cpu.train_step_fp64(flat0, batch, A, steps=3, grad_mode=mode)
     ys["fp64"] = {"met": met64, "cap": {k: v.numpy() for k, v in cap64.items()}, "grad": g64,
-                  "p": [p64]}
+                  "p": [p64, p64_3]}
     m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32")
     m.load_flat(flat0)
     e = Engine(m, batch_size=B, rollout_length=T, vtrace_grad_mode=mode)
@@ -223,20 +224,34 @@ def test_step_gradients_and_params_match_oracle(B, mode):
         checks.append((name, rl2, bound))
     for name, rl2, bound in checks:
         assert rl2 <= bound, (name, rl2, bound)
-    for name in ("fp64", "native"):
-        d = np.abs(hip["p"][0] - ys[name]["p"][0])
-        assert d.max() <= 1e-6, (name, d.max())
-    # after 3 steps against the native oracle (another fp32 rounding path): Adam turns a
-    # rounding-level difference in a near-zero gradient element into an O(lr) move (conv1 runs
-    # as three exact bf16 MFMA passes since round 3: its gradient is as close to float64 as
-    # before -- rel-L2 1.05e-6 at C2 -- but 29 of the 344,496 parameters landed 1e-6..2.1e-5
-    # from this oracle in round 3).  Bounds pinned near the measured values: max 5e-5 and at
-    # most 100 parameters (0.03 %) beyond 1e-6.
-    d3 = np.abs(hip["p"][1] - ys["native"]["p"][1])
+    # parameters after 1 step: within 1e-6 of float64; of the native fp32 oracle within 1e-6
+    # or twice its own distance from float64 (its gradient with the targets live, sg_none, is
+    # ~1e-4 from float64 where the kernels' is ~1e-6)
+    p64 = ys["fp64"]["p"]
+    d1 = np.abs(hip["p"][0] - p64[0])
+    own1 = float(np.abs(ys["native"]["p"][0] - p64[0]).max())
+    dn1 = float(np.abs(hip["p"][0] - ys["native"]["p"][0]).max())
+    print(f"B={B} {mode} params step 1: max vs fp64 {d1.max():.2e}, vs native {dn1:.2e} "
+          f"(native vs fp64 {own1:.2e})")
+    assert d1.max() <= 1e-6, d1.max()
+    assert dn1 <= max(1e-6, 2 * own1), (dn1, own1)
+    # after 3 steps: Adam turns a rounding-level difference in a near-zero gradient element into
+    # an O(lr) move (conv1 runs as three exact bf16 MFMA passes since round 3, the weight
+    # gradients since round 4: in round 3, 29 of the 344,496 parameters landed 1e-6..2.1e-5 from
+    # the native oracle).  Bounds pinned near the measured values: against float64 max 5e-5 and
+    # at most 100 parameters (0.03 %) beyond 1e-6; against native the same or twice native's
+    # own distance from float64.
+    d3 = np.abs(hip["p"][1] - p64[1])
     n3 = int(np.sum(d3 > 1e-6))
-    print(f"B={B} {mode} params step 3 vs native: max {d3.max():.2e}, n > 1e-6 {n3}")
+    dn3 = np.abs(hip["p"][1] - ys["native"]["p"][1])
+    own3 = np.abs(ys["native"]["p"][1] - p64[1])
+    nn3, nown3 = int(np.sum(dn3 > 1e-6)), int(np.sum(own3 > 1e-6))
+    print(f"B={B} {mode} params step 3: vs fp64 max {d3.max():.2e}, n > 1e-6 {n3}; vs native max "
+          f"{dn3.max():.2e}, n > 1e-6 {nn3} (native vs fp64: max {own3.max():.2e}, n {nown3})")
     assert d3.max() <= 5e-5, d3.max()
     assert n3 <= 100, n3
+    assert dn3.max() <= max(5e-5, 2 * own3.max()), (dn3.max(), own3.max())
+    assert nn3 <= max(100, 2 * nown3), (nn3, nown3)
     # against torch's default fp32 (its conv gradients off by ~1e-3 at C2): Adam's first
     # steps move a parameter by ~lr * sign(m), so a gradient element near 0 can flip: one lr
     # step everywhere; away from 1e-6 no more often than fp32 itself is away from float64
