@@ -92,49 +92,14 @@ template <> struct Frag<__bf16> {
   }
 };
 
-// ---------------------------------------------------------------------------------------
-// fp32 contractions as exact bf16 MFMA passes.  An fp32 value splits exactly into three bf16
-// terms x = hi + mid + lo (round-to-nearest 8-bit pieces of its 24-bit significand: the
-// residual after hi has <= 16 significant bits, after mid <= 8).  The nine products of two
-// such splits are each exact in fp32 (8 x 8 bits), so nine v_mfma_f32_16x16x32_bf16 (16 cycles
-// per 32 k) compute the fp32 products of a 32-deep k-step -- only the grouping of the fp32
-// additions differs from a v_mfma_f32_16x16x4_f32 chain -- at 9 x 16 = 144 cycles against the
-// 8 x 32 = 256 of the fp32 MFMAs: 1.78x the fp32 MFMA rate, the same arithmetic class as
-// conv1's three passes (one of whose operands is exact in bf16 already).
-// ---------------------------------------------------------------------------------------
-struct X3 {
-  Frag<__bf16>::vec h, m, l;
-};
+// An fp32 value split exactly into three bf16 terms x = hi + mid + lo (round-to-nearest 8-bit
+// pieces of its 24-bit significand: the residual after hi has <= 16 significant bits, after
+// mid <= 8); a product of a term with a bf16-exact value (conv1's image bytes) is exact in fp32.
 DEV void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
   h = (__bf16)x;
   const float r1 = x - (float)h;
   m = (__bf16)r1;
   l = (__bf16)(r1 - (float)m);
-}
-DEV X3 split3_8(const float (&x)[8]) {
-  X3 s;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    __bf16 h, m, l;
-    split3(x[c], h, m, l);
-    s.h[c] = h;
-    s.m[c] = m;
-    s.l[c] = l;
-  }
-  return s;
-}
-// the nine exact partial products into one fp32 accumulator, smallest terms first
-DEV f32x4 mma_x3(const X3& a, const X3& b, f32x4 c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.l, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.m, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.l, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.m, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
-  return c;
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.  Remap a linear

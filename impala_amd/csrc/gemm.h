@@ -322,37 +322,20 @@ template <class Op> struct wg_direct<Op, decltype(void(Op::DIRECT))> {
 // bf16 rows are stored bit-2/3 swapped (wg_row) at a pitch of BR / BC + 16 (conflict-free
 // transposing fragment reads); fp32 rows in order at + 4.
 template <typename T> constexpr int wg_pad() { return sizeof(T) == 2 ? 16 : 4; }
-// fp32 (exact bf16x3 split arithmetic, mma_x3): the X chunk is stored as its three bf16 planes
-// (rows of BR + 16 bf16, bit-2/3 swapped like the bf16 tiles: conflict-free transposing reads),
-// the Y chunk as fp32 rows of BC + 4 whose 16-byte column groups are XOR-swizzled by row bit 4
-// (x3_ycol), so the B fragment's eight ds_read_b32 (rows 8 g + j, g = lane >> 4) hit 4
-// disjoint 16-bank ranges.  Sizes in floats.
-template <int BR> constexpr int x3_xplane() { return 32 * (BR + 16) / 2; }
-template <typename T, int BR, int BC, int BM>
-constexpr int gemm_wg_stage() {
-  if constexpr (sizeof(T) == 4) return 3 * (BM / 32) * x3_xplane<BR>() + BM * (BC + 4);
-  return BM * (BR + wg_pad<T>()) + BM * (BC + wg_pad<T>());
-}
 template <typename T, int BR, int BC, int BM, int G>
 constexpr int gemm_wg_smem() {
-  return gemm_wg_stage<T, BR, BC, BM>() * 2 * G;
+  return (BM * (BR + wg_pad<T>()) + BM * (BC + wg_pad<T>())) * 2 * G;
 }
-DEV int x3_ycol(int row, int c) { return c ^ (((row >> 4) & 1) << 4); }
 template <typename T, int BR, int BC, int WR, int WC, int BM, int G, class Op, int PD = 2>
 DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict__ slab_bias,
                       int m_per_split, int lin, int gx, int gy, int gz, T* __restrict__ smem) {
   using F = Frag<T>;
   typedef typename F::vec V;  // 16 bytes of T
-  constexpr bool X3M = sizeof(T) == 4;  // fp32: exact bf16x3 split passes (mma_x3)
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int LDX = BR + wg_pad<T>(), LDY = BC + wg_pad<T>();
-  constexpr int LDXB = BR + 16;  // X3M: bf16 X plane row
-  constexpr int KSTEP = X3M ? 32 : F::KSTEP;
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NACC = TRW * TCW * 4;
-  constexpr int STAGE = gemm_wg_stage<T, BR, BC, BM>();  // elements of T per buffer
-  // X3M: the X planes (plane p of k-step kb at float offset (3 kb + p) * x3_xplane), then Y
-  constexpr int YOFF = X3M ? 3 * (BM / 32) * x3_xplane<BR>() : BM * LDX;
+  constexpr int STAGE = BM * LDX + BM * LDY;  // elements of T per buffer
   constexpr int NXV = BM * (BR / VEC);
   constexpr int NX = (NXV + 255) / 256;
   // Y staging: vector v = t + i*256 of a chunk is row v / (BC/VEC), column vector v % (BC/VEC),
@@ -366,7 +349,7 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
   static_assert(256 % BM == 0, "Y staging");
   static_assert(WR * WC == 4, "4 waves per group");
   static_assert(TRW >= 1 && TCW >= 1 && BR % 16 == 0 && BC % 16 == 0, "tile");
-  static_assert(BM % KSTEP == 0, "chunk");
+  static_assert(BM % F::KSTEP == 0, "chunk");
   static_assert(PD >= 1, "prefetch depth");
   static_assert((size_t)STAGE * 2 * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
                 "LDS reuse for the group reduction");
@@ -422,39 +405,16 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
     }
   };
   auto stash = [&](int d, T* Xs) {
-    T* Ys = Xs + YOFF;
+    T* Ys = Xs + BM * LDX;
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       const int e = tid + i * 256, mm = e / (BR / VEC), rr = (e % (BR / VEC)) * VEC;
-      if constexpr (X3M) {
-        if (e < NXV) {
-          bf16x4 o[3];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            __bf16 h, m, l;
-            split3(rx[d][i][q], h, m, l);
-            o[0][q] = h;
-            o[1][q] = m;
-            o[2][q] = l;
-          }
-          __bf16* xb = reinterpret_cast<__bf16*>(Xs) + (mm >> 5) * 6 * x3_xplane<BR>() +
-                       wg_row(mm & 31) * LDXB + rr;
-#pragma unroll
-          for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x4*>(xb + p * 2 * x3_xplane<BR>()) = o[p];
-        }
-      } else {
-        if (e < NXV) *reinterpret_cast<V*>(Xs + wg_prow<T>(mm) * LDX + rr) = rx[d][i];
-      }
+      if (e < NXV) *reinterpret_cast<V*>(Xs + wg_prow<T>(mm) * LDX + rr) = rx[d][i];
     }
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
       const int v = tid + i * 256;
-      if constexpr (X3M) {
-        const int row = v / YV;
-        if (v < NYV) *reinterpret_cast<V*>(Ys + row * LDY + x3_ycol(row, (v % YV) * VEC)) = ry[d][i];
-      } else {
-        if (v < NYV) *reinterpret_cast<V*>(Ys + wg_prow<T>(v / YV) * LDY + (v % YV) * VEC) = ry[d][i];
-      }
+      if (v < NYV) *reinterpret_cast<V*>(Ys + wg_prow<T>(v / YV) * LDY + (v % YV) * VEC) = ry[d][i];
     }
   };
   const int n_it = (m_end - m_beg + BM * G - 1) / (BM * G);
@@ -476,7 +436,7 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
       const int m0 = m_beg + (it * G + grp) * BM;
       const bool active = m0 < m_end;
       T* Xs = smem + (grp * 2 + (it & 1)) * STAGE;
-      const T* Ys = Xs + YOFF;
+      const T* Ys = Xs + BM * LDX;
       stash(d, Xs);
       __syncthreads();
       fetch(d, it + PD);  // in flight under the next PD - 1 chunks
@@ -487,61 +447,22 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
           const int rch = tid % BR, rg = tid / BR;
           float s0 = 0.f;
 #pragma unroll
-          for (int mm = rg; mm < BM; mm += RG) {
-            if constexpr (X3M) {  // hi + mid + lo is x exactly (each partial sum is exact)
-              const __bf16* xb = reinterpret_cast<const __bf16*>(Xs) + (mm >> 5) * 6 * x3_xplane<BR>() +
-                                 wg_row(mm & 31) * LDXB + rch;
-              s0 += ((float)xb[0] + (float)xb[2 * x3_xplane<BR>()]) + (float)xb[4 * x3_xplane<BR>()];
-            } else {
-              s0 += (float)Xs[wg_prow<T>(mm) * LDX + rch];
-            }
-          }
+          for (int mm = rg; mm < BM; mm += RG) s0 += (float)Xs[wg_prow<T>(mm) * LDX + rch];
           bias_acc += s0;
         }
-        if constexpr (X3M) {
 #pragma unroll
-          for (int kb = 0; kb < BM / 32; ++kb) {
-            const __bf16* xp = reinterpret_cast<const __bf16*>(Xs) + kb * 6 * x3_xplane<BR>();
-            X3 a[TRW], b[TCW];
+        for (int kk = 0; kk < BM; kk += F::KSTEP) {
+          V a[TRW], b[TCW];
 #pragma unroll
-            for (int i = 0; i < TRW; ++i) {
-              const int c0 = (wr * TRW + i) * 16;
-              a[i].h = lds_frag_k_sw(xp + c0, LDXB, lane);
-              a[i].m = lds_frag_k_sw(xp + 2 * x3_xplane<BR>() + c0, LDXB, lane);
-              a[i].l = lds_frag_k_sw(xp + 4 * x3_xplane<BR>() + c0, LDXB, lane);
-            }
+          for (int i = 0; i < TRW; ++i)
+            a[i] = lds_frag_k_sw(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
 #pragma unroll
-            for (int j = 0; j < TCW; ++j) {
-              // B fragment: Y rows 32 kb + 8 g + jj (g = lane >> 4), column c, split exactly
-              const int c = (wc * TCW + j) * 16 + (lane & 15);
-              float yv[8];
+          for (int j = 0; j < TCW; ++j)
+            b[j] = lds_frag_k_sw(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
 #pragma unroll
-              for (int jj = 0; jj < 8; ++jj) {
-                const int row = 32 * kb + 8 * (lane >> 4) + jj;
-                yv[jj] = Ys[row * LDY + x3_ycol(row, c)];
-              }
-              b[j] = split3_8(yv);
-            }
+          for (int i = 0; i < TRW; ++i)
 #pragma unroll
-            for (int i = 0; i < TRW; ++i)
-#pragma unroll
-              for (int j = 0; j < TCW; ++j) acc[i][j] = mma_x3(a[i], b[j], acc[i][j]);
-          }
-        } else {
-#pragma unroll
-          for (int kk = 0; kk < BM; kk += F::KSTEP) {
-            V a[TRW], b[TCW];
-#pragma unroll
-            for (int i = 0; i < TRW; ++i)
-              a[i] = lds_frag_k_sw(Xs + kk * LDX + (wr * TRW + i) * 16, LDX, lane);
-#pragma unroll
-            for (int j = 0; j < TCW; ++j)
-              b[j] = lds_frag_k_sw(Ys + kk * LDY + (wc * TCW + j) * 16, LDY, lane);
-#pragma unroll
-            for (int i = 0; i < TRW; ++i)
-#pragma unroll
-              for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
-          }
+            for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
         }
       }
     }

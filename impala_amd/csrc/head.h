@@ -3,12 +3,12 @@
 // heads' weight-gradient partial -- one workgroup per group of whole trajectories.
 //
 //   phase 1  stage h[F][256] of the group's F frames in LDS; heads = Wh . h + bh (MFMA)
-//   phase 2a all 4 waves, one 16-lane row per frame, one lane per action: log-softmax of the
-//            policy and behaviour logits, entropy, KL, log pi(a), rho (row reductions by DPP)
-//   phase 2b wave 0: one lane per (trajectory, t); V-trace in the reference's sequential order
-//            (kernels.h vtrace_lane) -> d loss / d value and the per-frame policy-gradient
-//            coefficient d loss / d log pi(a) under the gradient mode (vtrace_grad_lane)
-//   phase 2c all 4 waves, frame x action lanes again: d loss / d logits -> dH[F][32] in LDS
+//   phase 2  wave 0, one lane per (trajectory, t) = one frame: log-softmax of the policy and
+//            behaviour logits over the actions in registers, entropy, KL, log pi(a), rho; the
+//            V-trace in the reference's sequential order (kernels.h vtrace_lane) -> d loss /
+//            d value and d loss / d log pi(a) under the gradient mode (vtrace_grad_lane); the
+//            frame's d loss / d heads row -> dH[F][32] in LDS.  (Frame x action lanes with DPP
+//            row reductions took 4k cycles for the statistics alone: headstamps4, r04c.)
 //   phase 3  dz[f][j] = gelu'(z[f][j]) * sum_o' dH[f][o'] Wh[o'][j]        (MFMA, K = 32;
 //            gelu'(z) comes precomputed from the FC forward epilogue)
 //   phase 4  dWh[o'][j] += sum_f dH[f][o'] h[f][j]  (MFMA over frames, LDS transpose reads)
@@ -70,7 +70,9 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   __shared__ float lg_s[64][HEADS + 1];
   __shared__ __attribute__((aligned(16))) float zs[64 * (HEAD_JC + 4)];  // z slice (phase 3)
   __shared__ float bred[4][HEADS];
-  __shared__ float fsc[5][64];  // per frame: rho, entropy, KL, log pi(a), dH coefficient kappa
+  // the heads weights [16][256 + VEC], staged once per workgroup (each wave used to load all 16
+  // KB of fragments itself: 64 KB of the ~155 KB a workgroup loaded, headstamps4 r04c)
+  __shared__ __attribute__((aligned(16))) T whs[HEADS * LDH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T_ = a.T, S = a.S;
   const int traj0 = blockIdx.x * a.TPW;
@@ -86,24 +88,16 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   const bool valid = wave == 0 && tl < ntraj && t < T_;
   const bool inL = valid && t < L;
   const int fl = valid ? tl * T_ + t : 0;
-  float r = 0.f, g = 0.f;
+  // (reward, discount, action and the frame's behaviour logits)
+  float r = 0.f, g = 0.f, mub[MAX_A];
+  int act = 0;
   if (wave == 0) {
     const size_t n = f0 + fl;
     r = a.rew[n];
     if constexpr (!PPO) g = a.disc[n];
-  }
-  // phase 2a/2c lanes: frame f = 16 p + 4 wave + (lane >> 4) in pass p, action ja = lane & 15.
-  // The behaviour logits and actions of every pass are loaded now (clamped addresses, values
-  // selected later) so their latency overlaps phase 1.
-  constexpr int NPASS = 4;
-  const int ja = lane & 15;
-  float muv[NPASS];
-  int actv[NPASS];
+    act = (int)a.act[n];
 #pragma unroll
-  for (int p = 0; p < NPASS; ++p) {
-    const size_t n = f0 + min(16 * p + 4 * wave + (lane >> 4), nf - 1);
-    muv[p] = a.mu[n * A + min(ja, A - 1)];
-    actv[p] = (int)a.act[n];
+    for (int j = 0; j < MAX_A; ++j) mub[j] = a.mu[n * A + min(j, A - 1)];
   }
   // ---- every global load of the kernel is issued here, in one round trip: h rows, this
   // workgroup's z slice, the heads weights (both orientations) and bias ----
@@ -123,12 +117,13 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     zv[i] = f < nf ? *reinterpret_cast<const f32x4*>(a.zg + (f0 + f) * HID + jw + c)
                    : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  V whf[NKH], wtf[NKT];
+  constexpr int NWV = HEADS * (HID / VEC) / 256;  // 16-byte vectors of Wh per thread
+  V whv[NWV], wtf[NKT];
   {
     const T* wh = reinterpret_cast<const T*>(a.wh);
     const T* wht = reinterpret_cast<const T*>(a.wht);
 #pragma unroll
-    for (int ks = 0; ks < NKH; ++ks) whf[ks] = F::load(wh + (lane & 15) * HID + ks * F::KSTEP + kl);
+    for (int i = 0; i < NWV; ++i) whv[i] = F::load(wh + (size_t)(tid + i * 256) * VEC);
 #pragma unroll
     for (int ks = 0; ks < NKT; ++ks)
       wtf[ks] = F::load(wht + (jw + wave * 16 + (lane & 15)) * HPAD + ks * F::KSTEP + kl);
@@ -147,69 +142,88 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     const int e = tid + i * 256, f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
     *reinterpret_cast<f32x4*>(zs + f * (HEAD_JC + 4) + c) = zv[i];
   }
+#pragma unroll
+  for (int i = 0; i < NWV; ++i) {
+    const int e = tid + i * 256, r = e / (HID / VEC), c = (e % (HID / VEC)) * VEC;
+    *reinterpret_cast<V*>(whs + r * LDH + c) = whv[i];
+  }
   for (int e = tid; e < 64 * LDD / VEC; e += 256) *reinterpret_cast<V*>(dHs + e * VEC) = F::zero();
   __syncthreads();
   {
+    // four accumulators over interleaved k-steps (ks % 4), summed in a fixed order: the MFMAs
+    // issue back to back instead of waiting on one accumulator's dependent latency
     const int f = wave * 16 + (lane & 15);
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int NA = NKH >= 4 ? 4 : 1;
+    f32x4 acc[NA];
 #pragma unroll
-    for (int ks = 0; ks < NKH; ++ks)
-      acc = F::mma(whf[ks], *reinterpret_cast<const V*>(hs + f * LDH + ks * F::KSTEP + kl), acc);
+    for (int u = 0; u < NA; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) lg_s[f][4 * (lane >> 4) + q] = acc[q] + bhv[q];
+    for (int k4 = 0; k4 < NKH; k4 += NA) {
+      V w[NA], hf[NA];
+#pragma unroll
+      for (int u = 0; u < NA; ++u) {
+        w[u] = *reinterpret_cast<const V*>(whs + (lane & 15) * LDH + (k4 + u) * F::KSTEP + kl);
+        hf[u] = *reinterpret_cast<const V*>(hs + f * LDH + (k4 + u) * F::KSTEP + kl);
+      }
+#pragma unroll
+      for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+        for (int u = 0; u < NA; ++u) acc[u] = F::mma_e(e, w[u], hf[u], acc[u]);
+    }
+    f32x4 hsum = acc[0];
+    if constexpr (NA == 4) hsum = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lg_s[f][4 * (lane >> 4) + q] = hsum[q] + bhv[q];
   }
   __syncthreads();
   if (a.heads_out && lead) {
     for (int e = tid; e < nf * HEADS; e += 256)
       a.heads_out[(f0 + e / HEADS) * HEADS + e % HEADS] = lg_s[e / HEADS][e % HEADS];
   }
-  // ---- phase 2a: per-frame log-softmax statistics, frame x action lanes ----
-  const float ke = a.ent_coef * (1.f / (float)(a.B * T_));  // d(-ent_coef * mean H) / d H per frame
-  float pv[NPASS], lpv[NPASS], Hv[NPASS];
-#pragma unroll
-  for (int p = 0; p < NPASS; ++p) {
-    if (16 * p >= nf) continue;  // workgroup-uniform
-    const int f = 16 * p + 4 * wave + (lane >> 4);
-    const bool on = ja < A;
-    const float lgv = on ? lg_s[f][ja] : -INFINITY;
-    const float mv = on ? muv[p] : -INFINITY;
-    const float m = row16_max(lgv), mm = row16_max(mv);
-    const float e = on ? fast_exp(lgv - m) : 0.f, em = on ? fast_exp(mv - mm) : 0.f;
-    const float s = row16_sum(e), sm = row16_sum(em);
-    const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm);
-    const float logp = on ? lgv - lse : 0.f, pp = e * (1.f / s), lmu = on ? mv - lse_mu : 0.f;
-    const float H = -row16_sum(pp * logp);
-    const float kld = row16_sum(pp * (logp - lmu));
-    // log pi(a), log mu(a): the taken action's logit from LDS (one address per row) and its
-    // behaviour logit from the row's lane a (ds_bpermute)
-    const int aa = min(actv[p], A - 1);
-    const float logpa = lg_s[f][aa] - lse;
-    const float muA = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
-        4 * ((lane & 48) + aa), __builtin_bit_cast(int, mv)));
-    const float logmua = muA - lse_mu;
-    pv[p] = pp; lpv[p] = logp; Hv[p] = H;
-    if (ja == 0 && f < nf) {
-      fsc[0][f] = fast_exp(logpa - logmua);
-      fsc[1][f] = H;
-      fsc[2][f] = kld;
-      fsc[3][f] = logpa;
-    }
-  }
-  __syncthreads();
-  // ---- phase 2b: loss head on wave 0 (one lane per (trajectory, t)) ----
+  // ---- phase 2: one lane per frame of wave 0 ----
   if (wave == 0) {
     const int f = fl;
-    float rho = valid ? fsc[0][f] : 0.f, H = valid ? fsc[1][f] : 0.f;
-    const float kld = valid ? fsc[2][f] : 0.f, logpa = valid ? fsc[3][f] : 0.f;
-    float v = valid ? lg_s[f][VCOL] : 0.f;
-    if (!valid) { r = 0.f; g = 0.f; }
+    const float ke = a.ent_coef * (1.f / (float)(a.B * T_));  // d(-ent_coef * mean H) / d H
+    float lg[MAX_A], ex[MAX_A];
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) lg[j] = lg_s[f][min(j, A - 1)];
+    float m = -INFINITY, mm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j)
+      if (j < A) {
+        m = fmaxf(m, lg[j]);
+        mm = fmaxf(mm, mub[j]);
+      }
+    float s = 0.f, sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j) {
+      ex[j] = j < A ? fast_exp(lg[j] - m) : 0.f;
+      s += ex[j];
+      sm += j < A ? fast_exp(mub[j] - mm) : 0.f;
+    }
+    const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm), inv = 1.f / s;
+    const int aa = min(act, A - 1);
+    float H = 0.f, kld = 0.f, logpa = 0.f, logmua = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_A; ++j)
+      if (j < A) {
+        const float logp = lg[j] - lse, pp = ex[j] * inv, lmu = mub[j] - lse_mu;
+        H -= pp * logp;
+        kld += pp * (logp - lmu);
+        if (j == aa) {
+          logpa = logp;
+          logmua = lmu;
+        }
+      }
+    float rho = valid ? fast_exp(logpa - logmua) : 0.f;
+    if (!valid) { H = 0.f; kld = 0.f; logpa = 0.f; r = 0.f; g = 0.f; }
+    const float v = valid ? lg_s[f][VCOL] : 0.f;
+    float kappa = 0.f, dv = 0.f;  // d loss / d log pi(a), d loss / d value of this frame
     if constexpr (PPO) {
       const PpoFrame pf = ppo_frame(rho, v, r, a.clip_lo, a.clip_hi);
-      if (valid) {
-        const float c = 1.f / (float)a.B;
-        fsc[4][f] = c * pf.dr * rho;
-        dHs[f * LDD + VCOL] = (T)(-pf.adv * c);
-      }
+      const float c = 1.f / (float)a.B;
+      kappa = c * pf.dr * rho;
+      dv = -pf.adv * c;
       float q[6] = {valid ? pf.pgl : 0.f, valid ? pf.adv * pf.adv : 0.f, H, kld, rho, r};
 #pragma unroll
       for (int k = 0; k < 6; ++k) q[k] = wave_sum(q[k]);
@@ -226,19 +240,17 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
       const float c_pg = 1.f / (float)(a.B * L);
       const VtGrad gr = vtrace_grad_lane(o, a.vt_mode, v, v_n, r, g, rho, logpa, tv, L, a.lam,
                                          a.crho, a.cpg, c_pg);
+      kappa = gr.dlogpa;
+      dv = gr.dv;
       if (a.vt_dbg && lead && valid) {
-        const size_t BL = (size_t)a.B * L, o = (size_t)(traj0 + tl) * L + t;
+        const size_t BL = (size_t)a.B * L, ob = (size_t)(traj0 + tl) * L + t;
         if (inL) {
-          a.vt_dbg[o] = adv;
-          a.vt_dbg[BL + o] = err;
-          a.vt_dbg[2 * BL + o] = qq;
+          a.vt_dbg[ob] = adv;
+          a.vt_dbg[BL + ob] = err;
+          a.vt_dbg[2 * BL + ob] = qq;
         }
         a.vt_dbg[3 * BL + f0 + fl] = rho;
         a.vt_dbg[3 * BL + (size_t)a.B * T_ + f0 + fl] = v;
-      }
-      if (valid) {
-        fsc[4][f] = gr.dlogpa;
-        dHs[f * LDD + VCOL] = (T)gr.dv;
       }
       float s0 = inL ? logpa * adv : 0.f, s1 = inL ? err * err : 0.f;
       s0 = wave_sum(s0); s1 = wave_sum(s1);
@@ -247,15 +259,17 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         float* pp = a.partials + blockIdx.x * 8;
         pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
       }
-    }  // V-trace loss
-  }
-  __syncthreads();
-  // ---- phase 2c: dH[f][j] = ke p_j (log p_j + H) + kappa_f ([j == a] - p_j) ----
+    }
+    // dH[f][j] = ke p_j (log p_j + H) + kappa ([j == a] - p_j); dH[f][value] = dv
+    if (valid) {
 #pragma unroll
-  for (int p = 0; p < NPASS; ++p) {
-    const int f = 16 * p + 4 * wave + (lane >> 4);
-    if (16 * p < nf && f < nf && ja < A)
-      dHs[f * LDD + ja] = (T)(ke * pv[p] * (lpv[p] + Hv[p]) + fsc[4][f] * ((ja == actv[p] ? 1.f : 0.f) - pv[p]));
+      for (int j = 0; j < MAX_A; ++j)
+        if (j < A) {
+          const float pp = ex[j] * inv, logp = lg[j] - lse;
+          dHs[f * LDD + j] = (T)(ke * pp * (logp + H) + kappa * ((j == aa ? 1.f : 0.f) - pp));
+        }
+      dHs[f * LDD + VCOL] = (T)dv;
+    }
   }
   __syncthreads();
   // ---- phase 3: dz = gelu'(z) * (dH . Wh)   rows j (256: wave w -> 4 row tiles), cols f ----

@@ -213,13 +213,17 @@ def test_step_gradients_and_params_match_oracle(B, mode):
     g = hip["grad"]
     x64 = ys["fp64"]["grad"]
     # float64 is the truth: 1e-5.  The two fp32 yardsticks carry their own rounding (torch's
-    # oneDNN convolution gradients ~1e-3 at C2; with the advantage or the targets live the
-    # gradient also sums terms that cancel): 1e-5 or twice their own distance from float64.
+    # oneDNN convolution gradients ~1e-3 at C2): against them 1e-5 or twice their own distance
+    # from float64.  (The gradient is piecewise in the forward values -- ReLU masks -- and with
+    # the targets live (sg_none) a pre-activation within fp32 rounding of zero moves it: native
+    # fp32 lands 1.0e-4 from float64 at C2, and so did a conv2 run as bf16x3 passes, r04d; the
+    # f32-MFMA kernels round that unit as float64 does, 8e-7.)
+    own = {n: _rel_l2(ys[n]["grad"], x64) for n in ("native", "fp32")}
     checks = []
     for name in ("fp64", "native", "fp32"):
         y = ys[name]
         rl2 = _rel_l2(g, y["grad"])
-        bound = GRAD_RL2 if name == "fp64" else max(GRAD_RL2, 2 * _rel_l2(y["grad"], x64))
+        bound = GRAD_RL2 if name == "fp64" else max(GRAD_RL2, 2 * own[name])
         print(f"B={B} {mode} grad vs {name}: rel-L2 {rl2:.2e} (bound {bound:.1e})")
         checks.append((name, rl2, bound))
     for name, rl2, bound in checks:
