@@ -212,6 +212,15 @@ DEV float row16_max(float v) {
   v = fmaxf(v, dppf<DPP_ROW_HALF_MIRROR>(v));
   return fmaxf(v, dppf<DPP_ROW_MIRROR>(v));
 }
+// over the 4 lanes of each quad (all four get the bit-identical result)
+DEV float quad_sum(float v) {
+  v += dppf<DPP_QP_1032>(v);
+  return v + dppf<DPP_QP_2301>(v);
+}
+DEV float quad_max(float v) {
+  v = fmaxf(v, dppf<DPP_QP_1032>(v));
+  return fmaxf(v, dppf<DPP_QP_2301>(v));
+}
 DEV float wave_sum(float v) { return xor32_sum(xor16_sum(row16_sum(v))); }
 DEV float wave_max(float v) {
   v = fmaxf(v, dppf<DPP_QP_1032>(v));

@@ -3,12 +3,15 @@
 // heads' weight-gradient partial -- one workgroup per group of whole trajectories.
 //
 //   phase 1  stage h[F][256] of the group's F frames in LDS; heads = Wh . h + bh (MFMA)
-//   phase 2  wave 0, one lane per (trajectory, t) = one frame: log-softmax of the policy and
-//            behaviour logits over the actions in registers, entropy, KL, log pi(a), rho; the
-//            V-trace in the reference's sequential order (kernels.h vtrace_lane) -> d loss /
-//            d value and d loss / d log pi(a) under the gradient mode (vtrace_grad_lane); the
-//            frame's d loss / d heads row -> dH[F][32] in LDS.  (Frame x action lanes with DPP
-//            row reductions took 4k cycles for the statistics alone: headstamps4, r04c.)
+//   phase 2a all four waves, a quad of threads per frame, four actions per thread: log-softmax
+//            of the policy and behaviour logits, entropy, KL, log pi(a), rho (quad DPP sums)
+//   phase 2b wave 0, one lane per (trajectory, t) = one frame: the V-trace in the reference's
+//            sequential order (kernels.h vtrace_lane) -> d loss / d value and d loss / d log
+//            pi(a) under the gradient mode (vtrace_grad_lane), the loss partials
+//   phase 2c the quads again: the frame's d loss / d heads row -> dH[F][32] in LDS
+//            (the statistics on wave 0 alone, one lane per frame over all 15 actions, took
+//            6.3k cycles of one SIMD: hstamps5, r04f; frame x 16-action lanes with row
+//            reductions 4k cycles for the statistics alone: headstamps4, r04c)
 //   phase 3  dz[f][j] = gelu'(z[f][j]) * sum_o' dH[f][o'] Wh[o'][j]        (MFMA, K = 32;
 //            gelu'(z) comes precomputed from the FC forward epilogue)
 //   phase 4  dWh[o'][j] += sum_f dH[f][o'] h[f][j]  (MFMA over frames, LDS transpose reads)
@@ -73,34 +76,44 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   // the heads weights [16][256 + VEC], staged once per workgroup (each wave used to load all 16
   // KB of fragments itself: 64 KB of the ~155 KB a workgroup loaded, headstamps4 r04c)
   __shared__ __attribute__((aligned(16))) T whs[HEADS * LDH];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ f32x4 fst[64];    // per frame: H, KL, log pi(a), rho (phase 2a -> 2b)
+  __shared__ float kd[64][2];  // per frame: d loss / d log pi(a), d loss / d value (2b -> 2c)
+  // the wave index as a scalar: `wave == 0` branches are uniform (no exec-mask joins)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T_ = a.T, S = a.S;
   const int traj0 = blockIdx.x * a.TPW;
   const int ntraj = min(a.TPW, a.B - traj0);
-  const int nf = ntraj * T_;                       // valid frames of this workgroup
+  const int nf = ntraj * T_;                       // valid frames of this workgroup (>= 1)
   const size_t f0 = (size_t)traj0 * T_;            // first global frame
   const T* hg = reinterpret_cast<const T*>(a.h);
   const int jw = blockIdx.y * HEAD_JC;            // this workgroup's hidden-column slice
   const bool lead = blockIdx.y == 0;              // writes the per-group outputs
-  // wave 0's per-(trajectory, t) batch values, loaded first so their latency overlaps phase 1
   const int A = a.A, L = T_ - 1;
+  // wave 0, phase 2b: one lane per (trajectory, t)
   const int tl = lane / S, t = lane % S;
   const bool valid = wave == 0 && tl < ntraj && t < T_;
   const bool inL = valid && t < L;
   const int fl = valid ? tl * T_ + t : 0;
-  // (reward, discount, action and the frame's behaviour logits)
-  float r = 0.f, g = 0.f, mub[MAX_A];
-  int act = 0;
-  if (wave == 0) {
-    const size_t n = f0 + fl;
-    r = a.rew[n];
-    if constexpr (!PPO) g = a.disc[n];
-    act = (int)a.act[n];
+  // phases 2a / 2c: a quad of threads per frame fq, four actions 4 q .. 4 q + 3 each
+  const int fq = tid >> 2, q4 = (tid & 3) * 4;
+  const size_t nq = f0 + min(fq, nf - 1);
+  // ---- every global load of the kernel is issued here, unconditionally, in one round trip:
+  // the batch values, h rows, this workgroup's z slice, the heads weights (both orientations)
+  // and bias.  Row indices are clamped into the group: rows past the group's frames hold a
+  // copy of its last frame, which only meets zero dH rows (phase 4, bias sums) or outputs
+  // nobody stores.  (Guarded loads made the compiler wait for each one inside its branch:
+  // three serial round trips, 4.8k cycles before phase 1, hstamps5 r04f.)  The action is read
+  // as the low word of the int64 (actions are in [0, A)): a 64-bit load whose dead high half
+  // gets its register reused costs a wait for the load. ----
+  const int act_q = reinterpret_cast<const int*>(a.act)[2 * nq];
+  float mub[4];
 #pragma unroll
-    for (int j = 0; j < MAX_A; ++j) mub[j] = a.mu[n * A + min(j, A - 1)];
+  for (int u = 0; u < 4; ++u) mub[u] = a.mu[nq * A + min(q4 + u, A - 1)];
+  float r = 0.f, g = 0.f;
+  if (wave == 0) {
+    r = a.rew[f0 + fl];
+    if constexpr (!PPO) g = a.disc[f0 + fl];
   }
-  // ---- every global load of the kernel is issued here, in one round trip: h rows, this
-  // workgroup's z slice, the heads weights (both orientations) and bias ----
   constexpr int NHV = 64 * (HID / VEC) / 256, NZV = 64 * (HEAD_JC / 4) / 256;
   constexpr int NKH = HID / F::KSTEP, NKT = HPAD / F::KSTEP;
   const int kl = F::KPL * (lane >> 4);
@@ -108,14 +121,13 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   f32x4 zv[NZV];
 #pragma unroll
   for (int i = 0; i < NHV; ++i) {
-    const int e = tid + i * 256, f = e / (HID / VEC), c = (e % (HID / VEC)) * VEC;
-    hv[i] = f < nf ? *reinterpret_cast<const V*>(hg + (f0 + f) * HID + c) : F::zero();
+    const int e = tid + i * 256, f = min(e / (HID / VEC), nf - 1), c = (e % (HID / VEC)) * VEC;
+    hv[i] = *reinterpret_cast<const V*>(hg + (f0 + f) * HID + c);
   }
 #pragma unroll
   for (int i = 0; i < NZV; ++i) {
-    const int e = tid + i * 256, f = e / (HEAD_JC / 4), c = (e % (HEAD_JC / 4)) * 4;
-    zv[i] = f < nf ? *reinterpret_cast<const f32x4*>(a.zg + (f0 + f) * HID + jw + c)
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int e = tid + i * 256, f = min(e / (HEAD_JC / 4), nf - 1), c = (e % (HEAD_JC / 4)) * 4;
+    zv[i] = *reinterpret_cast<const f32x4*>(a.zg + (f0 + f) * HID + jw + c);
   }
   constexpr int NWV = HEADS * (HID / VEC) / 256;  // 16-byte vectors of Wh per thread
   V whv[NWV], wtf[NKT];
@@ -180,42 +192,68 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     for (int e = tid; e < nf * HEADS; e += 256)
       a.heads_out[(f0 + e / HEADS) * HEADS + e % HEADS] = lg_s[e / HEADS][e % HEADS];
   }
-  // ---- phase 2: one lane per frame of wave 0 ----
-  if (wave == 0) {
-    const int f = fl;
-    const float ke = a.ent_coef * (1.f / (float)(a.B * T_));  // d(-ent_coef * mean H) / d H
-    float lg[MAX_A], ex[MAX_A];
+  // ---- phase 2a: per-frame statistics, a quad of threads per frame (all four waves) ----
+  const int aa = min(act_q, A - 1);
+  float pq[4], lpq[4];  // this thread's p_j and log p_j, kept for phase 2c
+  float Hq;
+  {
+    float lg[4], ex[4];
+    bool in[4];
 #pragma unroll
-    for (int j = 0; j < MAX_A; ++j) lg[j] = lg_s[f][min(j, A - 1)];
+    for (int u = 0; u < 4; ++u) {
+      in[u] = q4 + u < A;
+      lg[u] = lg_s[fq][min(q4 + u, A - 1)];
+    }
     float m = -INFINITY, mm = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < MAX_A; ++j)
-      if (j < A) {
-        m = fmaxf(m, lg[j]);
-        mm = fmaxf(mm, mub[j]);
+    for (int u = 0; u < 4; ++u)
+      if (in[u]) {
+        m = fmaxf(m, lg[u]);
+        mm = fmaxf(mm, mub[u]);
       }
+    m = quad_max(m);
+    mm = quad_max(mm);
     float s = 0.f, sm = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAX_A; ++j) {
-      ex[j] = j < A ? fast_exp(lg[j] - m) : 0.f;
-      s += ex[j];
-      sm += j < A ? fast_exp(mub[j] - mm) : 0.f;
+    for (int u = 0; u < 4; ++u) {
+      ex[u] = in[u] ? fast_exp(lg[u] - m) : 0.f;
+      s += ex[u];
+      sm += in[u] ? fast_exp(mub[u] - mm) : 0.f;
     }
+    s = quad_sum(s);
+    sm = quad_sum(sm);
     const float lse = m + fast_log(s), lse_mu = mm + fast_log(sm), inv = 1.f / s;
-    const int aa = min(act, A - 1);
     float H = 0.f, kld = 0.f, logpa = 0.f, logmua = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAX_A; ++j)
-      if (j < A) {
-        const float logp = lg[j] - lse, pp = ex[j] * inv, lmu = mub[j] - lse_mu;
+    for (int u = 0; u < 4; ++u) {
+      const float logp = lg[u] - lse, pp = ex[u] * inv, lmu = mub[u] - lse_mu;
+      pq[u] = pp;
+      lpq[u] = logp;
+      if (in[u]) {
         H -= pp * logp;
         kld += pp * (logp - lmu);
-        if (j == aa) {
+        if (q4 + u == aa) {
           logpa = logp;
           logmua = lmu;
         }
       }
-    float rho = valid ? fast_exp(logpa - logmua) : 0.f;
+    }
+    // the one thread holding action a contributes log pi(a) / log mu(a), the others 0
+    H = quad_sum(H);
+    kld = quad_sum(kld);
+    logpa = quad_sum(logpa);
+    logmua = quad_sum(logmua);
+    Hq = H;
+    if ((tid & 3) == 0) fst[fq] = f32x4{H, kld, logpa, fast_exp(logpa - logmua)};
+  }
+  __syncthreads();
+  // ---- phase 2b: wave 0, one lane per frame: V-trace / PPO, d loss / d log pi(a), d loss /
+  // d value, the loss partials ----
+  if (wave == 0) {
+    const int f = fl;
+    const f32x4 st = fst[f];
+    float H = st[0], kld = st[1], logpa = st[2];
+    float rho = valid ? st[3] : 0.f;
     if (!valid) { H = 0.f; kld = 0.f; logpa = 0.f; r = 0.f; g = 0.f; }
     const float v = valid ? lg_s[f][VCOL] : 0.f;
     float kappa = 0.f, dv = 0.f;  // d loss / d log pi(a), d loss / d value of this frame
@@ -260,15 +298,24 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
         pp[0] = s0; pp[1] = s1; pp[2] = s2; pp[3] = s3; pp[4] = s4;
       }
     }
-    // dH[f][j] = ke p_j (log p_j + H) + kappa ([j == a] - p_j); dH[f][value] = dv
     if (valid) {
+      kd[f][0] = kappa;
+      kd[f][1] = dv;
+    }
+  }
+  __syncthreads();
+  // ---- phase 2c: dH[f][j] = ke p_j (log p_j + H) + kappa ([j == a] - p_j), dH[f][value] = dv
+  // (quads again; rows of frames outside the group stay zero) ----
+  if (fq < nf) {
+    const float ke = a.ent_coef * (1.f / (float)(a.B * T_));  // d(-ent_coef * mean H) / d H
+    const float kappa = kd[fq][0], dv = kd[fq][1];
 #pragma unroll
-      for (int j = 0; j < MAX_A; ++j)
-        if (j < A) {
-          const float pp = ex[j] * inv, logp = lg[j] - lse;
-          dHs[f * LDD + j] = (T)(ke * pp * (logp + H) + kappa * ((j == aa ? 1.f : 0.f) - pp));
-        }
-      dHs[f * LDD + VCOL] = (T)dv;
+    for (int u = 0; u < 4; ++u) {
+      const int j = q4 + u;
+      if (j < A)
+        dHs[fq * LDD + j] = (T)(ke * pq[u] * (lpq[u] + Hq) + kappa * ((j == aa ? 1.f : 0.f) - pq[u]));
+      else if (j == VCOL)
+        dHs[fq * LDD + j] = (T)dv;
     }
   }
   __syncthreads();
