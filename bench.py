@@ -312,7 +312,12 @@ def _cpu_baseline(ref_cpu, B, T, A, seconds, warmup):
 def run_host_staged(eng, batch, args, dist, model, world):
     """The PCIe-inclusive rate (SURVEY.md §8(d) secondary bound; never `value`): every step's
     batch comes from page-locked host memory through the library's staging ring
-    (impala_stage, 2 slots), the H2D copies of step k+1 overlapping the update on step k."""
+    (impala_stage, 2 slots), the H2D copies of step k+1 overlapping the update on step k.
+    The loop is ImpalaLearner._stage_host's: before a slot is restaged the host waits for the
+    previous copy out of its host buffers (impala_stage_wait), which a producer refilling them
+    has to do.  (Without that wait the host runs ahead of the GPU and the runtime stalls the
+    SDMA copies for milliseconds every few dozen steps: 0.31-0.55 ms per step against a steady
+    0.30 ms; tools/hs_loop.py, profiles/r04hs.)"""
     from impala_amd.distributed import compute_grads_allreduced, native_dp_buckets
     hosts = [[t.cpu().pin_memory() for t in batch] for _ in range(2)]
     eng.stage_init(2)
@@ -322,6 +327,7 @@ def run_host_staged(eng, batch, args, dist, model, world):
         for k in range(n):
             s = k % 2
             if k + 1 < n:
+                eng.stage_wait(1 - s)
                 eng.stage(1 - s, *hosts[1 - s])
             b = eng.slot_batch(s)
             if dist is None:
@@ -353,7 +359,9 @@ def run_host_staged(eng, batch, args, dist, model, world):
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "h2d_bytes_per_step": nbytes,
             "h2d_GBps_per_gpu": round(nbytes * args.steps / elapsed / 1e9, 2),
             "note": "rollouts staged from page-locked host memory every step (impala_stage ring, "
-                    "2 slots, H2D overlapped with the previous update); not `value`"}
+                    "2 slots, obs over 2 SDMA streams, H2D overlapped with the previous update; "
+                    "the learner's loop: a slot's previous copy is waited for before restaging "
+                    "it); not `value`"}
 
 
 PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",

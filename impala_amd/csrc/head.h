@@ -326,6 +326,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
       const int j0 = jw + wave * 16;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
+        if (ct * 16 >= nf) break;  // frame tiles past the group's frames (uniform)
         const int f = ct * 16 + (lane & 15);
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -347,8 +348,9 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     const int c0 = jw + wave * 16;
 #pragma unroll
-    for (int kk = 0; kk < 64; kk += F::KSTEP)
-      acc = F::mma(lds_frag_k(dHs + kk * LDD, LDD, lane), lds_frag_k(hs + kk * LDH + c0, LDH, lane), acc);
+    for (int kk = 0; kk < 64; kk += F::KSTEP)  // k-steps past the group's frames: dH rows 0
+      if (kk < nf)
+        acc = F::mma(lds_frag_k(dHs + kk * LDD, LDD, lane), lds_frag_k(hs + kk * LDH + c0, LDH, lane), acc);
     float* sl = a.slab_h + (size_t)blockIdx.x * HEADS * HID;
 #pragma unroll
     for (int q = 0; q < 4; ++q) sl[(4 * (lane >> 4) + q) * HID + c0 + (lane & 15)] = acc[q];

@@ -200,14 +200,14 @@ struct impala_learner {
   StageSlot ring[kMaxStageSlots];
   int n_slots = 0;
   // copy streams: IMPALA_H2D_STREAMS > 1 splits the obs block over several streams (stream 0
-  // joins the others and signals `ready`).  Measured on MI355X one stream is fastest: 29.7 GB/s
-  // pinned H2D, against 12.8 GB/s with 4 and 8.1 GB/s with 8 (profiles/r01k)
+  // joins the others and signals `ready`); see impala_stage_init for the measured defaults
   static constexpr int kMaxH2D = 8;
   hipStream_t h2d_s[kMaxH2D] = {};
   hipEvent_t h2d_join[kMaxH2D] = {};
   int n_h2d = 0;
-  int h2d_pull_wg = 0;        // > 0: copy with h2d_pull_kernel on that many workgroups
+  int h2d_pull_wg = 0;        // > 0: copy everything with h2d_pull_kernel on that many workgroups
   int h2d_pull_threads = 256; // threads per pull workgroup (IMPALA_H2D_THREADS)
+  bool h2d_small_pull = true; // SDMA obs: the four small fields in one 1-workgroup pull launch
   hipStream_t h2d = nullptr;  // = h2d_s[0]
   // native data-parallel step (impala_dp_*): the library's own RCCL communicator, so the
   // gradient all-reduces are enqueued with no host round trip and no c10d bookkeeping; the FC +
@@ -1378,7 +1378,22 @@ int impala_stage_init(impala_learner* h, int nslots) {
   CK(hipSetDevice(h->device));
   free_ring(h);
   if (!h->n_h2d) {
-    int n = 1;
+    // Default: hipMemcpyAsync (SDMA) of obs split over 2 streams, the four small fields in one
+    // small pull launch.  Beside the fp32 step (tools/h2d_bw.py, r04hs / r04hs2) SDMA on
+    // 1 / 2 / 4 streams kept 41-43 / 46.4 / 43.9 GB/s, while the pull kernel (8 x 256 threads,
+    // 45-48 GB/s alone and the round-1 default) fell to 36 GB/s and slowed the trunk forward it
+    // shares CUs with from 63 to 190-210 us (rocprofv3 kernel trace, r04hs).
+    // IMPALA_H2D_KERNEL=<workgroups> copies everything with the pull kernel instead.
+    // Data-parallel handles (world_size > 1) never use the pull kernel unless asked: whether
+    // every device of a node maps a rank's page-locked buffers is not something this library
+    // checks.
+    h->h2d_pull_wg = 0;
+    if (const char* e = std::getenv("IMPALA_H2D_KERNEL")) h->h2d_pull_wg = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("IMPALA_H2D_THREADS"))
+      h->h2d_pull_threads = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
+    h->h2d_small_pull = h->cfg.world_size == 1;
+    if (const char* e = std::getenv("IMPALA_H2D_SMALL_PULL")) h->h2d_small_pull = e[0] == '1';
+    int n = h->h2d_pull_wg > 0 ? 1 : 2;
     if (const char* e = std::getenv("IMPALA_H2D_STREAMS")) n = std::atoi(e);
     n = std::max(1, std::min(n, (int)impala_learner::kMaxH2D));
     for (int i = 0; i < n; ++i) {
@@ -1387,16 +1402,6 @@ int impala_stage_init(impala_learner* h, int nslots) {
       CK(hipEventCreateWithFlags(&h->h2d_join[i], hipEventDisableTiming));
     }
     h->h2d = h->h2d_s[0];
-    // pull kernel by default: 8 workgroups of 256 threads (one per XCD) reach 45.4 GB/s pinned
-    // H2D on MI355X, against 28.9 GB/s for hipMemcpyAsync (SDMA), 36.6 GB/s for blit copies and
-    // 37.9-41.5 GB/s for larger pull grids or blocks (profiles/r01k)
-    // Data-parallel handles (world_size > 1) keep hipMemcpyAsync unless IMPALA_H2D_KERNEL asks
-    // for the pull kernel: it is validated on one GPU, and whether every device of a node maps
-    // a rank's page-locked buffers is not something this library checks.
-    h->h2d_pull_wg = h->cfg.world_size == 1 ? 8 : 0;
-    if (const char* e = std::getenv("IMPALA_H2D_KERNEL")) h->h2d_pull_wg = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("IMPALA_H2D_THREADS"))
-      h->h2d_pull_threads = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
   }
   const size_t N = (size_t)h->N;
   size_t off = 0;
@@ -1441,50 +1446,58 @@ int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
   const int ns = h->n_h2d;
   for (int i = 0; i < ns; ++i)  // the steps that read the slot have run
     CK(hipStreamWaitEvent(h->h2d_s[i], s.done, 0));
-  // pull-copy kernel (IMPALA_H2D_KERNEL=<workgroups>): only for page-locked, device-mapped
-  // host fields (hipHostGetDevicePointer); anything else takes the hipMemcpyAsync path
-  bool pull = h->h2d_pull_wg > 0;
+  // the pull kernel reads page-locked, device-mapped host fields (hipHostGetDevicePointer);
+  // anything else takes hipMemcpyAsync
   const void* hsrc[5] = {b->obs, b->actions, b->rewards, b->discounts, b->behaviour_logits};
   const void* msrc[5] = {};
-  for (int f = 0; f < 5 && pull; ++f) {
+  bool mapped = h->h2d_pull_wg > 0 || h->h2d_small_pull;
+  for (int f = 0; f < 5 && mapped; ++f) {
     if (!hsrc[f]) continue;
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, const_cast<void*>(hsrc[f]), 0) != hipSuccess || !dp ||
         (((uintptr_t)dp) & 15) != 0) {
       (void)hipGetLastError();
-      pull = false;
+      mapped = false;
     }
     msrc[f] = dp;
   }
-  if (pull) {
+  void* dst[5] = {(void*)s.dev.obs, (void*)s.dev.actions, (void*)s.dev.rewards,
+                  (void*)s.dev.discounts, (void*)s.dev.behaviour_logits};
+  const size_t bytes[5] = {N * 3 * 64 * 64, N * 8, N * 4, N * 4, N * (size_t)h->A * 4};
+  auto pull = [&](int f_lo, int wgs, int threads) -> int {
     PullArgs pa{};
-    const void* const* src = msrc;
-    void* dst[5] = {(void*)s.dev.obs, (void*)s.dev.actions, (void*)s.dev.rewards,
-                    (void*)s.dev.discounts, (void*)s.dev.behaviour_logits};
-    const size_t bytes[5] = {N * 3 * 64 * 64, N * 8, N * 4, N * 4, N * (size_t)h->A * 4};
-    for (int f = 0; f < 5; ++f) {
-      if (!src[f]) continue;
-      pa.src[pa.nf] = (const char*)src[f];
+    for (int f = f_lo; f < 5; ++f) {
+      if (!msrc[f]) continue;
+      pa.src[pa.nf] = (const char*)msrc[f];
       pa.dst[pa.nf] = (char*)dst[f];
       pa.bytes[pa.nf] = (long long)bytes[f];
       ++pa.nf;
     }
-    h2d_pull_kernel<<<h->h2d_pull_wg, h->h2d_pull_threads, 0, h->h2d>>>(pa);
+    h2d_pull_kernel<<<wgs, threads, 0, h->h2d>>>(pa);
     CK_LAUNCH("h2d_pull");
+    return 0;
+  };
+  if (mapped && h->h2d_pull_wg > 0) {
+    if (int r = pull(0, h->h2d_pull_wg, h->h2d_pull_threads)) return r;
   } else {
-    // obs in ns contiguous chunks (one per copy stream), the small fields on stream 0
-    const size_t ob = N * 3 * 64 * 64, chunk = (ob / ns + 4095) & ~(size_t)4095;
+    // the small fields first on stream 0 (one pull launch, or four copies), then obs in ns
+    // contiguous chunks, one per copy stream
+    if (mapped && h->h2d_small_pull) {
+      // 8 workgroups, one per XCD: ~100 KB at PCIe latency (one workgroup took 37-42 us,
+      // delaying the obs chunk behind it on the stream; rocprofv3 trace, r04hs3)
+      if (int r = pull(1, 8, 256)) return r;
+    } else {
+      CK(hipMemcpyAsync(dst[1], b->actions, bytes[1], hipMemcpyDefault, h->h2d));
+      CK(hipMemcpyAsync(dst[2], b->rewards, bytes[2], hipMemcpyDefault, h->h2d));
+      if (b->discounts) CK(hipMemcpyAsync(dst[3], b->discounts, bytes[3], hipMemcpyDefault, h->h2d));
+      CK(hipMemcpyAsync(dst[4], b->behaviour_logits, bytes[4], hipMemcpyDefault, h->h2d));
+    }
+    const size_t ob = bytes[0], chunk = (ob / ns + 4095) & ~(size_t)4095;
     for (int i = 0; i < ns; ++i) {
       const size_t o0 = std::min(ob, (size_t)i * chunk), o1 = std::min(ob, o0 + chunk);
       if (o1 > o0)
         CK(hipMemcpyAsync((char*)s.dev.obs + o0, b->obs + o0, o1 - o0, hipMemcpyDefault, h->h2d_s[i]));
     }
-    CK(hipMemcpyAsync((void*)s.dev.actions, b->actions, N * 8, hipMemcpyDefault, h->h2d));
-    CK(hipMemcpyAsync((void*)s.dev.rewards, b->rewards, N * 4, hipMemcpyDefault, h->h2d));
-    if (b->discounts)
-      CK(hipMemcpyAsync((void*)s.dev.discounts, b->discounts, N * 4, hipMemcpyDefault, h->h2d));
-    CK(hipMemcpyAsync((void*)s.dev.behaviour_logits, b->behaviour_logits, N * (size_t)h->A * 4,
-                      hipMemcpyDefault, h->h2d));
   }
   for (int i = 1; i < ns; ++i) {
     CK(hipEventRecord(h->h2d_join[i], h->h2d_s[i]));

@@ -9,6 +9,14 @@ from oracle import ref_cpu
 pytestmark = pytest.mark.gpu
 
 
+# impala_stage copy paths: the default (obs over 2 SDMA streams, the small fields in one pull
+# launch), all SDMA copies, 3 obs streams, and the pull kernel for everything
+H2D_MODES = {"default": {},
+             "sdma_only": {"IMPALA_H2D_SMALL_PULL": "0"},
+             "sdma_3streams": {"IMPALA_H2D_STREAMS": "3"},
+             "pull8": {"IMPALA_H2D_KERNEL": "8"}}
+
+
 def _dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -101,13 +109,14 @@ def test_device_replay_gather_and_learn():
     assert np.isfinite(float(met["train/loss"]))
 
 
-@pytest.mark.parametrize("pull_wg", [0, 8])
-def test_host_staging_ring_matches_device_batches(pull_wg, monkeypatch):
+@pytest.mark.parametrize("h2d", sorted(H2D_MODES))
+def test_host_staging_ring_matches_device_batches(h2d, monkeypatch):
     """impala_stage ring (2 slots, copies of step k+1 enqueued before step k; hipMemcpyAsync or
     the PCIe pull kernel) gives bitwise the same weights and metrics as the same batches handed
     over already in HBM."""
     dev = _dev()
-    monkeypatch.setenv("IMPALA_H2D_KERNEL", str(pull_wg))
+    for k, v in H2D_MODES[h2d].items():
+        monkeypatch.setenv(k, v)
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
     B, T, A, steps = 4, 20, 15, 5
@@ -221,14 +230,15 @@ def test_optimizer_state_resume_matches_uninterrupted():
     torch.testing.assert_close(m_b.flat, m_full.flat, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("pull_wg", [0, 8])
-def test_learner_host_batches_distinct_per_step(pull_wg, monkeypatch):
+@pytest.mark.parametrize("h2d", sorted(H2D_MODES))
+def test_learner_host_batches_distinct_per_step(h2d, monkeypatch):
     """ImpalaLearner.train_step on host (list-of-trajectories) batches reuses two page-locked
     staging buffers in place; with a DIFFERENT batch every step (hipMemcpyAsync or the PCIe
     pull kernel) the weights and metrics are bitwise those of the same batches handed over
     already in HBM -- a stale or torn read of a reused host buffer would show here."""
     dev = _dev()
-    monkeypatch.setenv("IMPALA_H2D_KERNEL", str(pull_wg))
+    for k, v in H2D_MODES[h2d].items():
+        monkeypatch.setenv(k, v)
     from impala_amd.engine import Engine
     from impala_amd.learner import ImpalaLearner
     from impala_amd.model import AtariPPOModel

@@ -17,6 +17,14 @@ G = os.path.join(os.path.dirname(__file__), "golden")
 KEYS = ("loss", "entropy", "td", "pg", "kl", "ratio", "target")
 
 
+# impala_stage copy paths: the default (obs over 2 SDMA streams, the small fields in one pull
+# launch), all SDMA copies, 3 obs streams, and the pull kernel for everything
+H2D_MODES = {"default": {},
+             "sdma_only": {"IMPALA_H2D_SMALL_PULL": "0"},
+             "sdma_3streams": {"IMPALA_H2D_STREAMS": "3"},
+             "pull8": {"IMPALA_H2D_KERNEL": "8"}}
+
+
 def _load(name):
     return np.load(os.path.join(G, name), allow_pickle=False)
 
@@ -161,12 +169,13 @@ def test_ppo_grad_parts_match_whole():
     np.testing.assert_array_equal(e3.metrics.cpu().numpy(), met)
 
 
-@pytest.mark.parametrize("pull_wg", [0, 8])
-def test_ppo_host_staging_ring_matches_device_batch(pull_wg, monkeypatch):
+@pytest.mark.parametrize("h2d", sorted(H2D_MODES))
+def test_ppo_host_staging_ring_matches_device_batch(h2d, monkeypatch):
     """impala_stage on a PPO handle (no discounts field): bitwise the same step as the batch
     handed over in HBM, with hipMemcpyAsync or the pull kernel."""
     dev = _dev()
-    monkeypatch.setenv("IMPALA_H2D_KERNEL", str(pull_wg))
+    for k, v in H2D_MODES[h2d].items():
+        monkeypatch.setenv(k, v)
     host = [torch.from_numpy(np.ascontiguousarray(x)) for x in ref_cpu.synthetic_ppo_batch(64, 6, seed=8)]
     m1, e1 = _setup(dev, 64, A=6)
     e1.train_step(*[t.to(dev) for t in host])
