@@ -817,7 +817,7 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   const size_t o_act1 = take((size_t)N * P1 * OC1 * es);
   const size_t o_act2 = take((size_t)N * P2 * OC2 * es);
   const size_t o_act3 = take((size_t)N * FLAT * es);
-  const size_t o_y = take((size_t)N * FLAT * es);
+  const size_t o_y = take((size_t)N * YLD * es);
   const size_t o_h = take((size_t)N * HID * es);
   const size_t o_dH = take((size_t)N * HPAD * es);
   const size_t o_dz = take((size_t)N * HID * es);

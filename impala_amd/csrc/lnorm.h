@@ -43,7 +43,7 @@ DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const 
 #pragma unroll
   for (int i = 0; i < 16; ++i) q += (v[i] - mean) * (v[i] - mean);
   const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / FLAT) + LN_EPS);
-  const size_t o = (size_t)frame * FLAT + lane * 16;
+  const size_t o = (size_t)frame * FLAT + lane * 16, oy = (size_t)frame * YLD + lane * 16;
 #pragma unroll
   for (int i = 0; i < 16; i += 4) {
     float yy[4];
@@ -54,10 +54,10 @@ DEV void ln_frame_epilogue(const float* et, int ldt, int frame, int lane, const 
     if constexpr (Y_SC1 && sizeof(T) == 2) {
       const unsigned long long w = (unsigned long long)(unsigned)pack_bf16x2(yy[0], yy[1]) |
                                    ((unsigned long long)(unsigned)pack_bf16x2(yy[2], yy[3]) << 32);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(y + o + i), w, __ATOMIC_RELAXED,
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(y + oy + i), w, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      store4(y + o + i, yy);
+      store4(y + oy + i, yy);
     }
   }
   if (lane == 0) {
@@ -100,7 +100,7 @@ DEV void ln_frames_epilogue(const float* et, int fstride, int ldt, const int (&f
   for (int m = 0; m < M; ++m) rstd[m] = 1.f / sqrtf(wave_sum(q[m]) * (1.f / FLAT) + LN_EPS);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    const size_t o = (size_t)frame[m] * FLAT + lane * 16;
+    const size_t o = (size_t)frame[m] * FLAT + lane * 16, oy = (size_t)frame[m] * YLD + lane * 16;
 #pragma unroll
     for (int i = 0; i < 16; i += 4) {
       float yy[4];
@@ -108,7 +108,7 @@ DEV void ln_frames_epilogue(const float* et, int fstride, int ldt, const int (&f
       for (int c = 0; c < 4; ++c)
         yy[c] = (v[m][i + c] - mean[m]) * rstd[m] * k.g[i + c] + k.e[i + c];
       store4(act3 + o + i, v[m] + i);
-      store4(y + o + i, yy);
+      store4(y + oy + i, yy);
     }
     if (lane == 0) {
       stats[2 * frame[m]] = mean[m];

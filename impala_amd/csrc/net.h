@@ -26,6 +26,9 @@ constexpr int OC3 = 64, KS3 = 3, ST3 = 1, H3 = 4, K3 = OC2 * KS3 * KS3;    // 57
 constexpr int P1 = H1 * H1, P2 = H2 * H2, P3 = H3 * H3;                   // 225, 36, 16
 constexpr int FLAT = OC3 * P3;                                             // 1024
 constexpr int HID = 256;
+// row stride (elements) of the LayerNorm output y [N][YLD], the FC layer's input: a padded
+// stride moves the rows of one 16-row fragment load off a common 4 KB alignment
+constexpr int YLD = FLAT;
 constexpr int HEADS = 16;     // actor rows 0..A-1, critic row 15
 constexpr int HPAD = 32;      // padded K of the heads dgrad GEMM
 constexpr int VCOL = 15;      // value column in the heads output

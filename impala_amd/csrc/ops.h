@@ -86,7 +86,7 @@ template <typename T> struct FcFwd {
   float* zg;  // gelu'(pre-activation), fp32: the GELU backward's factor (head_step phase 3)
   T* h;
   struct ColCtx { const T* p; };
-  DEV ColCtx col_ctx(int c) const { return ColCtx{y + (size_t)c * FLAT}; }
+  DEV ColCtx col_ctx(int c) const { return ColCtx{y + (size_t)c * YLD}; }
   DEV const T* a_row(int r, int) const { return w + r * K; }
   DEV typename Frag<T>::vec load_b(const ColCtx& cc, int k) const { return Frag<T>::load(cc.p + k); }
   struct Epi { float b[4]; };
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void fc_fwd_splitk_f32(const FcFwd<float> op, 
     const int col = i * 4 + wave, k = lane * 4;
     const int c = min(c0 + col, op.C - 1);  // frames past C: any valid row, results dropped
     *reinterpret_cast<f32x4*>(sb + col * LDB + k) =
-        *reinterpret_cast<const f32x4*>(op.y + (size_t)c * FLAT + k0 + k);
+        *reinterpret_cast<const f32x4*>(op.y + (size_t)c * YLD + k0 + k);
   }
   __syncthreads();
   f32x4 acc[NCF];
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float* bp[NCF];
 #pragma unroll
   for (int cf = 0; cf < NCF; ++cf)
-    bp[cf] = op.y + (size_t)min(c0 + cf * 16 + (lane & 15), op.C - 1) * FLAT + k0 + 4 * (lane >> 4);
+    bp[cf] = op.y + (size_t)min(c0 + cf * 16 + (lane & 15), op.C - 1) * YLD + k0 + 4 * (lane >> 4);
   f32x4 acc[NCF];
 #pragma unroll
   for (int cf = 0; cf < NCF; ++cf) acc[cf] = Frag<float>::zero();
@@ -416,9 +416,9 @@ template <typename T> struct FcWgrad {  // dWfc[o][j] = sum_n dz[n][o] y[n][j]
   int x_ld = HID;
   const T* y;
   // Y gather as element offsets from y (buffer loads: out-of-range rows read as zero)
-  DEV int y_roff(int m) const { return m * FLAT; }
+  DEV int y_roff(int m) const { return m * YLD; }
   DEV int y_coff(int c) const { return c; }
-  DEV int y_bytes() const { return M * FLAT * (int)sizeof(T); }
+  DEV int y_bytes() const { return M * YLD * (int)sizeof(T); }
   DEV const T* ybase() const { return y; }
 };
 // The FC weight gradient over the whole batch in one split (gemm_wg direct mode): the tile is
