@@ -750,7 +750,12 @@ def main():
     if native_dp:
         out["config"]["rccl_nranks"] = eng.dp_nranks
     if dist is not None and not args.no_dp_variants:
-        out["dp_variants"] = dp_variants(args, B, T, A, dev, dist, world, batch)
+        # a sub-record: an error in it (raised on every rank alike, e.g. RCCL not loadable for
+        # the native communicator) is recorded instead of losing the line
+        try:
+            out["dp_variants"] = dp_variants(args, B, T, A, dev, dist, world, batch)
+        except Exception as ex:  # noqa: BLE001
+            out["dp_variants"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     if not args.no_host_staged:
         out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
