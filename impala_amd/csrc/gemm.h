@@ -132,7 +132,12 @@ constexpr int gemm_tile_smem() {
   constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + tile_pad<T>()) : BR * LD;
   return 2 * (ASZ + BC * LD);
 }
-template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
+// PF: K chunks held in registers ahead of the one being computed (1: the next chunk; 2: the
+// next two, for a K loop whose chunks are too short to cover the L2 latency of one fetch).
+// KACC: accumulator chains per output fragment over alternating k-steps, their elements
+// interleaved (Frag::mma_e) so consecutive MFMAs never wait on each other's result (a lone
+// 16x16x4 fp32 chain issues every 40 cycles instead of 32); summed in chain order at the end.
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1>
 DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __restrict__ smem) {
   constexpr int NT = 64 * WR * WC;
   constexpr bool AK = Op::A_KMAJOR;
@@ -150,6 +155,8 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   static_assert((WR * WC == 4 || (WR * WC == 8 && !Op::TILE_EPI)) && TRW >= 1 && TCW >= 1, "tile");
   static_assert(BR * KV % NT == 0 && BC * KV % NT == 0, "staging");
   static_assert(Op::K % BK == 0 && BK % F::KSTEP == 0, "K chunking");
+  static_assert((PF == 1 || PF == 2) && (KACC == 1 || KACC == 2) && (BK / F::KSTEP) % KACC == 0, "PF / KACC");
+  static_assert(PF == 1 || NK % 2 == 0, "two chunks ahead: an even chunk count per tile");
   constexpr int SMEM = 2 * (ASZ + BC * LD);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
@@ -174,40 +181,41 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 #pragma unroll
     for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(fc0 + srow(i), op.C - 1));
   };
-  V ra[NA], rb[NB];
-  auto fetch = [&](int k0) {
+  V ra[PF][NA], rb[PF][NB];
+  auto fetch = [&](int k0, int sl) {
     if constexpr (AK) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int e = tid + i * NT, kr = e / RV, rv = e % RV;
-        ra[i] = F::load(op.a_kptr(k0 + kr, fr0 + rv * VEC, fcw));
+        ra[sl][i] = F::load(op.a_kptr(k0 + kr, fr0 + rv * VEC, fcw));
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) ra[i] = F::load(arow[i] + k0 + skv(i) * VEC);
+      for (int i = 0; i < NA; ++i) ra[sl][i] = F::load(arow[i] + k0 + skv(i) * VEC);
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = op.load_b(bctx[i], k0 + skv(i) * VEC);
+    for (int i = 0; i < NB; ++i) rb[sl][i] = op.load_b(bctx[i], k0 + skv(i) * VEC);
   };
-  auto stash = [&](int buf) {
+  auto stash = [&](int buf, int sl) {
     T* As = smem + buf * (ASZ + BC * LD);
     T* Bs = As + ASZ;
     if constexpr (AK) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int e = tid + i * NT, kr = e / RV, rv = e % RV;
-        *reinterpret_cast<V*>(As + wg_prow<T>(kr) * LDA + rv * VEC) = ra[i];
+        *reinterpret_cast<V*>(As + wg_prow<T>(kr) * LDA + rv * VEC) = ra[sl][i];
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + srow(i) * LD + skv(i) * VEC) = ra[i];
+      for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + srow(i) * LD + skv(i) * VEC) = ra[sl][i];
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + srow(i) * LD + skv(i) * VEC) = rb[i];
+    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + srow(i) * LD + skv(i) * VEC) = rb[sl][i];
   };
   const int kl = F::KPL * (lane >> 4);
   set_ctx(ft);
-  fetch(0);
+  fetch(0, 0);
+  if constexpr (PF == 2) fetch(BK, 1);
   [[maybe_unused]] typename EpiTypes<Op>::EpiConst econst{};
   if constexpr (Op::TILE_EPI) econst = op.epi_const(tid);
   for (int t = ft; t < n_tiles; t += vgrid) {
@@ -222,27 +230,34 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
           ep[i][j] = op.epi(cr0 + (wr * TRW + i) * 16 + 4 * (lane >> 4),
                             min(cc0 + (wc * TCW + j) * 16 + (lane & 15), op.C - 1));
     }
-    f32x4 acc[TRW][TCW];
+    f32x4 acc[TRW][TCW], acc2[KACC > 1 ? TRW : 1][KACC > 1 ? TCW : 1];
 #pragma unroll
     for (int i = 0; i < TRW; ++i)
 #pragma unroll
       for (int j = 0; j < TCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (KACC > 1) {
+#pragma unroll
+      for (int i = 0; i < TRW; ++i)
+#pragma unroll
+        for (int j = 0; j < TCW; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int kc = 0; kc < NK; ++kc) {
       const int buf = kc & 1;  // NK is even or the next tile restarts at buffer 0 after a sync
-      stash(buf);
+      // PF == 2: chunk kc sits in register slot kc & 1 (NK is even: a tile starts at slot 0)
+      const int sl = PF == 2 ? (kc & 1) : 0;
+      stash(buf, sl);
       __syncthreads();
-      if (kc + 1 < NK) {
-        fetch((kc + 1) * BK);
+      if (kc + PF < NK) {
+        fetch((kc + PF) * BK, sl);
       } else if (t + vgrid < n_tiles) {
-        set_ctx(t + vgrid);  // prefetch the next tile's first chunk under this compute
-        fetch(0);
+        // prefetch the next tile's first chunk(s) under this compute
+        if (kc + PF == NK) set_ctx(t + vgrid);
+        fetch((kc + PF - NK) * BK, sl);
       }
       const T* As = smem + buf * (ASZ + BC * LD);
       const T* Bs = As + ASZ;
-#pragma unroll
-      for (int kk = 0; kk < BK; kk += F::KSTEP) {
-        V a[TRW], b[TCW];
+      auto frags = [&](int kk, V (&a)[TRW], V (&b)[TCW]) {
 #pragma unroll
         for (int i = 0; i < TRW; ++i) {
           if constexpr (AK)
@@ -253,11 +268,40 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 #pragma unroll
         for (int j = 0; j < TCW; ++j)
           b[j] = *reinterpret_cast<const V*>(Bs + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
+      };
+      if constexpr (KACC == 1) {
 #pragma unroll
-        for (int i = 0; i < TRW; ++i)
+        for (int kk = 0; kk < BK; kk += F::KSTEP) {
+          V a[TRW], b[TCW];
+          frags(kk, a, b);
 #pragma unroll
-          for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+          for (int i = 0; i < TRW; ++i)
+#pragma unroll
+            for (int j = 0; j < TCW; ++j) acc[i][j] = F::mma(a[i], b[j], acc[i][j]);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 2 * F::KSTEP) {
+          V a[TRW], b[TCW], a2[TRW], b2[TCW];
+          frags(kk, a, b);
+          frags(kk + F::KSTEP, a2, b2);
+#pragma unroll
+          for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+            for (int i = 0; i < TRW; ++i)
+#pragma unroll
+              for (int j = 0; j < TCW; ++j) {
+                acc[i][j] = F::mma_e(e, a[i], b[j], acc[i][j]);
+                acc2[i][j] = F::mma_e(e, a2[i], b2[j], acc2[i][j]);
+              }
+        }
       }
+    }
+    if constexpr (KACC > 1) {
+#pragma unroll
+      for (int i = 0; i < TRW; ++i)
+#pragma unroll
+        for (int j = 0; j < TCW; ++j) acc[i][j] += acc2[i][j];
     }
     if constexpr (Op::TILE_EPI) {
       // workgroup epilogue: fp32 tile [BC][BR+4] in (reused) LDS, then op.tile_epilogue
@@ -292,10 +336,10 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   }
 }
 
-template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1>
 __global__ __launch_bounds__(64 * WR * WC) void gemm_tile(const Op op, int n_rtiles) {
   __shared__ __attribute__((aligned(16))) T smem[gemm_tile_smem<T, BR, BC, BK, WR, WC, Op>()];
-  gemm_tile_body<T, BR, BC, BK, WR, WC, Op>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
+  gemm_tile_body<T, BR, BC, BK, WR, WC, Op, PF, KACC>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
 }
 
 // Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split

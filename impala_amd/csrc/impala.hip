@@ -75,6 +75,10 @@ struct Split {
 };
 // direct (one-split) FC weight-gradient tile: BR x BC outputs, WR x WC waves, G 4-wave groups
 constexpr int FCD_BR = 32, FCD_BC = 64, FCD_WR = 2, FCD_WC = 2, FCD_G = 4, FCD_PD = 2;
+// fp32 FC forward K loop: chunks held ahead, accumulator chains (gemm.h gemm_tile_body).
+// PF / KACC 1 / 1: 13.97 us, 2 / 1: 13.40, 1 / 2: 14.20, 2 / 2: 13.67-13.69 (r04v2,
+// tools/var_specs/fcpf.py); 2 / 1 keeps the summation order, so the output bits are unchanged
+constexpr int FCF_PF = 2, FCF_KACC = 1;
 Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
   Split s;
   const long chunks = (M + chunk - 1) / chunk;
@@ -336,8 +340,10 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
 #endif
   {
     FcFwd<T> op{n, sw + sh.wfc, vv + Vecs::bfc, (const T*)h->y, h->zg, (T*)h->h};
-    // 32 x 32 tiles: 320 workgroups (5.9 vs 6.7 us for 64 x 32, tools/var_specs/fcfwd.py)
-    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 32, 32, BK(256), 2, 2, FcFwd<T>>,
+    // 32 x 32 tiles: 320 workgroups (5.9 vs 6.7 us for 64 x 32, tools/var_specs/fcfwd.py);
+    // fp32: two K chunks in registers ahead of the MFMAs (FCF_PF / FCF_KACC)
+    constexpr int PF = sizeof(T) == 4 ? FCF_PF : 1, KA = sizeof(T) == 4 ? FCF_KACC : 1;
+    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 32, 32, BK(256), 2, 2, FcFwd<T>, PF, KA>,
                         dim3(persist_grid(h, (long)cdiv(n, 32) * (HID / 32))), dim3(256), st, op,
                         HID / 32))
       return r;

@@ -234,7 +234,12 @@ int impala_gather_rows(const void* const* src, void* const* dst, const size_t* r
  *   impala_slot_batch     make `stream` wait for the slot's copies; *out = its device views,
  *                         to pass to impala_train_step / impala_compute_grads*
  *   impala_slot_release   record on `stream` that the steps reading the slot are enqueued
- * With two slots, staging batch k+1 overlaps the step on batch k. */
+ * With two slots, staging batch k+1 overlaps the step on batch k.  The copies are SDMA
+ * (hipMemcpyAsync) of obs over 2 streams, plus one small pull-kernel launch for the other
+ * four fields when they are page-locked and device-mapped (IMPALA_H2D_STREAMS,
+ * IMPALA_H2D_SMALL_PULL, IMPALA_H2D_KERNEL select other paths).  Call
+ * impala_stage_wait on a slot before restaging it, as a producer refilling its host buffers
+ * must: a host that stages without ever waiting runs ahead and the runtime stalls the copies. */
 int impala_stage_init(impala_learner* h, int nslots);
 int impala_stage(impala_learner* h, const impala_batch* host, int slot);
 int impala_stage_wait(impala_learner* h, int slot);
