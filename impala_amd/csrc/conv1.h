@@ -108,7 +108,10 @@ DEV void c1_stash_frame_rot(T* img, int tid, const uint4 v[3]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = (j + xq) & 3;
-      const uint32_t u = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+      // word q selected with masks: the nested select compiled to a divergent branch per
+      // value of q (12 x 4 exec-masked blocks, 1.7-2.2k clocks per frame; fwdstash32 r04v4)
+      const uint32_t u = (w[0] & -(uint32_t)(q == 0)) | (w[1] & -(uint32_t)(q == 1)) |
+                         (w[2] & -(uint32_t)(q == 2)) | (w[3] & -(uint32_t)(q == 3));
       T* dst = img + (Y * c1::GRID + 4 * xq + q) * LDI + ci * 16 + b * 4;
       if constexpr (sizeof(T) == 4) {
         *reinterpret_cast<f32x4*>(dst) = f32x4{(float)(u & 255u), (float)((u >> 8) & 255u),
@@ -339,6 +342,10 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // biases: 16-byte loads issued with the frame, ahead of the weights (waiting for the weights
   // then covers them: loads retire in order)
   float bb1[2][4], bb2[4];
+  // fp32: the conv2 bias of this lane's 4x4x1-block output channel (loaded in the frame loop, it
+  // cost a wait for every load in flight there, the next frame's image included: 0.7-1.3k
+  // clocks per frame, tools/var_specs/fwdstash32.py r04v4)
+  const float bb2q = b2[16 * wave + 4 * ((lane >> 2) & 3) + (lane >> 4)];
   {
     const f32x4 u0 = *reinterpret_cast<const f32x4*>(b1 + 4 * (lane >> 4));
     const f32x4 u1 = *reinterpret_cast<const f32x4*>(b1 + 16 + 4 * (lane >> 4));
@@ -421,6 +428,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   for (int q = 0; q < 4; ++q) {
     asm volatile("" ::"v"(bb1[0][q]), "v"(bb1[1][q]), "v"(bb2[q]));
   }
+  asm volatile("" ::"v"(bb2q));
   const int n_it = (f1 - f0 + G - 1) / G;
   // conv1 pixel tiles of this wave: rows oy = wave, wave + 4, wave + 8, wave + 12 of the 15x15
   // output (lane & 15 = ox; ox = 15 and wave 3's oy = 15 are pad lanes / a pad tile).  The tiles
@@ -584,7 +592,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         // over k-phase g; ((g0 + g1) + (g2 + g3)) of reg q lands on row q (rows_sum4), so lane
         // 16 q + 4 og + j stores one value
         const int pc = 32 + (lane & 3), oc = 16 * wave + 4 * ((lane >> 2) & 3) + (lane >> 4);
-        const float v = fmaxf(rows_sum4(acc[2][0], acc[2][1], acc[2][2], acc[2][3]) + b2[oc], 0.f);
+        const float v = fmaxf(rows_sum4(acc[2][0], acc[2][1], acc[2][2], acc[2][3]) + bb2q, 0.f);
         act2[((size_t)f * P2 + pc) * OC2 + oc] = (T)v;
         if (tail) {
           const int cy = pc / H2, cx = pc - cy * H2;

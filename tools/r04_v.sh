@@ -2,6 +2,7 @@
 # Round 4: bench lines (200 steps, fp32 C2) of the product and every build_variants/*.so,
 # product first and last (box drift); variants that print stamp lines show them.
 set -o pipefail
+shopt -s nullglob
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r04v}
 mkdir -p $O
