@@ -1069,7 +1069,9 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
               bsum[q] += v[q];
             }
           }
-          if (pv) *reinterpret_cast<f32x4*>(dyt + (iy * 16 + ix) * LDX + 4 * cg) = v;
+          // branch-free: a lane off the 15 x 15 grid holds v = +0 (its Z reads took the zero
+          // row, its mask is 0) and stores it into pad row 15 (iy 0, ix 15), which stays zero
+          *reinterpret_cast<f32x4*>(dyt + (pv ? iy * 16 + ix : 15) * LDX + 4 * cg) = v;
           __builtin_amdgcn_sched_barrier(0);
         }
         // half 1 reads back the partial sums this wave stored (LDS order per wave)
