@@ -531,9 +531,17 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
     const bool active = f < f1;
+    V ar0[3];  // fp32: conv2's first W2 fragments, loaded under this frame's conv1
     if (active) {
       // ---- conv1 -> act1 (HBM + LDS) and its ReLU bit mask ----
       f32x4 accA[2][2], accB[2][2];
+      // issued here, 4.6k clocks ahead of their use: loaded at the top of the conv2 loop, the
+      // first MFMA of every frame waited a whole L2 round trip (forward 60.2 -> 58.8 us,
+      // tools/var_specs/w2early.py r04v7)
+      if constexpr (!W2REG) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) ar0[d] = F::load(w2row + d * KS);
+      }
       c1_mma(accA, 0);
       c1_mma(accB, 2);
       c1_epi(accA, 0, f);
@@ -550,10 +558,11 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       // fp32: the W2 fragments stream from L2 in a ring PD2 k-steps ahead of their MFMAs (the
       // order pinned by scheduling barriers; the compiler kept them one step ahead)
       constexpr int PD2 = W2REG ? 1 : 4;
+      static_assert(W2REG || PD2 - 1 == 3, "ar0 holds the ring's first PD2 - 1 fragments");
       V ar[PD2];
       if constexpr (!W2REG) {
 #pragma unroll
-        for (int d = 0; d < PD2 - 1; ++d) ar[d] = F::load(w2row + d * KS);
+        for (int d = 0; d < PD2 - 1; ++d) ar[d] = ar0[d];
       }
 #pragma unroll
       for (int ks = 0; ks < NKS2; ++ks) {
