@@ -953,6 +953,54 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
       }
     }
   };
+  // group B's staging split in two for its loop: the loads issued at the top of a step, under
+  // its weight-gradient MFMAs, the LDS stores after them (loads followed at once by their stores
+  // exposed 1.3-2.7k clocks of load latency per step on the bottleneck group: 72.3 -> 70.0 us,
+  // tools/var_specs/bstage.py r04v8)
+  struct StRegs {
+    uint4 nv[3];
+    f32x4 nd2[ND2];
+    uint32_t nmk;
+  };
+  auto stage_ld = [&](int fi, int fd, StRegs& r) {
+    r.nmk = 0;
+    if (fi >= 0) c1_load_frame<float>(x + (size_t)fi * IMG, tid, r.nv);
+    if (fd >= 0) {
+      const float* src = dy2 + (size_t)fd * P2 * OC2;
+#pragma unroll
+      for (int i = 0; i < ND2; ++i) {
+        const int e = tid + i * 256;
+        r.nd2[i] = e < D2V ? *reinterpret_cast<const f32x4*>(src + e * 4) : F::zero();
+      }
+      if (tid < c1::NPIX) r.nmk = mask1[(size_t)fd * c1::NPIX + tid];
+    }
+  };
+  auto stage_st = [&](int fi, int bi, int fd, int bd, const StRegs& r) {
+    if (fd >= 0) {
+      float* d2s = d2s_buf(bd);
+#pragma unroll
+      for (int i = 0; i < ND2; ++i) {
+        const int e = tid + i * 256;
+        if (e < D2V) *reinterpret_cast<f32x4*>(d2s + ((e * 4) / OC2) * LDD + (e * 4) % OC2) = r.nd2[i];
+      }
+      if (tid < c1::NPIX) msk_buf(bd)[tid] = r.nmk;
+    }
+    if (fi < 0) return;
+    uint8_t* img = img_buf(bi);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int vi = tid + i * 256, ci = vi >> 8, yy = (vi & 255) >> 2, xq = vi & 3;
+      const int Y = yy >> 2, bb = yy & 3;
+      const uint32_t w[4] = {r.nv[i].x, r.nv[i].y, r.nv[i].z, r.nv[i].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t |= ((w[q] >> (8 * d)) & 255u) << (8 * q);
+        *reinterpret_cast<uint32_t*>(img + (Y * c1::CH + ci * 16 + bb * 4 + d) * XP + 4 * xq) = t;
+      }
+    }
+  };
   if (is_a && nF > 0 && load_w2) c12_load_w2(w2t, wb, wave, lane);
   // zero once: each half-Z tile's row 36, and the dY1 pad rows (ix = 15) of both buffers
   if (is_a && lane < OC1 / 2) *reinterpret_cast<f32x4*>(zw + P2 * LDZ + 4 * lane) = F::zero();
@@ -1095,6 +1143,8 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     stage(nF > 0 ? f0 : -1, 0, nF > 1 ? f0 + 1 : -1, 1);
     __syncthreads();
     for (int it = 1; it <= nF; ++it) {
+      StRegs sr;
+      stage_ld(it < nF ? f0 + it : -1, it + 1 < nF ? f0 + it + 1 : -1, sr);
       // ---- conv1 weight gradient of frame it - 1, as three exact bf16 MFMA passes: A = dY1
       // (rows oc, k = pixel) split exactly into hi + mid + lo bf16 terms (truncation: the top 8
       // significand bits of x, then of the remainder, then the <= 8 bits left -- each term's fp32
@@ -1188,7 +1238,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
 #pragma unroll
             for (int i = 0; i < 2; ++i) acc[i][j] = FB::mma(fa[i][tm], fb[j], acc[i][j]);
       }
-      stage(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1);
+      stage_st(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1, sr);
       __syncthreads();
     }
   }

@@ -1,3 +1,4 @@
+# ADOPTED in round 4 (conv1.h stage_ld / stage_st); kept as the record of the A/B edit.
 # fp32 backward, group B: the next frame's staging loads (image bytes, dY2, mask) issued at the
 # top of B's step, under its conv1 weight-gradient MFMAs, and stored to LDS after them, instead
 # of loads immediately followed by their LDS stores after the weight gradient (1.3-2.7k clocks

@@ -1,3 +1,4 @@
+# ADOPTED in round 4 (conv1.h ar0); kept as the record of the A/B edit.
 # fp32 forward: the W2 ring's first three fragments of conv2 loaded at the start of the frame's
 # conv1 phase (4.6k clocks earlier) instead of at the top of the conv2 loop, whose first MFMA
 # otherwise waits a full L2 round trip every frame.
