@@ -70,6 +70,14 @@ def main(tag, src_root="gpurun_out", dst_root="profiles"):
         for r in csv.DictReader(open(p)):
             if r["Counter_Name"] == cname:
                 ctr[r["Kernel_Name"]][cname].append(float(r["Counter_Value"]))
+    # per-launch durations from the kernel trace: the median and the mean of the second half of
+    # the launches (the run's first launches run at a lower clock: ~77 vs ~71 us for the fused
+    # backward in r04zc, so the all-launch mean sits above the bench's steady-state timing)
+    durs = collections.defaultdict(list)
+    tp = os.path.join(src, "stats", "run_kernel_trace.csv")
+    if os.path.exists(tp):
+        for r in csv.DictReader(open(tp)):
+            durs[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = []
     total_ns = sum(float(r["TotalDurationNs"]) for r in stats)
     for r in stats:
@@ -79,8 +87,12 @@ def main(tag, src_root="gpurun_out", dst_root="profiles"):
         write = c.get("WRITE_SIZE")
         fb = 2 * 1024 * sum(fetch) / len(fetch) if fetch else None
         wb = 1024 * sum(write) / len(write) if write else None
+        dd = durs.get(name, [])
+        med = sorted(dd)[len(dd) // 2] if dd else None
+        late = sum(dd[len(dd) // 2:]) / len(dd[len(dd) // 2:]) if dd else None
         out.append({"kernel": short(name), "name": name[:200], "calls": int(r["Calls"]),
-                    "avg_us": float(r["AverageNs"]) / 1e3, "pct": float(r["Percentage"]),
+                    "avg_us": float(r["AverageNs"]) / 1e3, "median_us": med, "late_half_avg_us": late,
+                    "pct": float(r["Percentage"]),
                     "hbm_read_bytes": fb, "hbm_write_bytes": wb,
                     "hbm_bytes": (fb or 0) + (wb or 0) if (fb is not None or wb is not None) else None})
     for k in ("bench_stats.json",):
@@ -101,15 +113,19 @@ def main(tag, src_root="gpurun_out", dst_root="profiles"):
               open(os.path.join(dst, "summary.json"), "w"), indent=1)
     with open(os.path.join(dst, "summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary `{tag}`\n\n`tools/profile.sh {tag}` = `rocprofv3 --kernel-trace --stats` "
-                "over `bench.py --steps 20 --warmup 3` (every launch of the run: warmup, kernel selection, the "
+                "over `bench.py --steps 20 --warmup 20` (r04zc and earlier: `--warmup 3`; every launch of the run: warmup, kernel selection, the "
                 "timed and the stamped steps), then separate `--pmc FETCH_SIZE` "
                 "and `--pmc WRITE_SIZE` passes. HBM bytes per launch: FETCH_SIZE×1024×2 (gfx950 half-count "
-                "correction) + WRITE_SIZE×1024.\n\n")
-        f.write("| kernel | calls | avg µs | % time | HBM read MB | HBM write MB |\n|---|---|---|---|---|---|\n")
+                "correction) + WRITE_SIZE×1024. Median and second-half mean per launch from the kernel "
+                "trace (the first launches of a run are clocked lower).\n\n")
+        f.write("| kernel | calls | avg µs | median µs | 2nd-half avg µs | % time | HBM read MB | HBM write MB |\n"
+                "|---|---|---|---|---|---|---|---|\n")
         for o in out:
             rd = f"{o['hbm_read_bytes'] / 1e6:.2f}" if o["hbm_read_bytes"] is not None else "-"
             wr = f"{o['hbm_write_bytes'] / 1e6:.2f}" if o["hbm_write_bytes"] is not None else "-"
-            f.write(f"| {o['kernel']} | {o['calls']} | {o['avg_us']:.2f} | {o['pct']:.2f} | {rd} | {wr} |\n")
+            md = f"{o['median_us']:.2f}" if o["median_us"] is not None else "-"
+            lt = f"{o['late_half_avg_us']:.2f}" if o["late_half_avg_us"] is not None else "-"
+            f.write(f"| {o['kernel']} | {o['calls']} | {o['avg_us']:.2f} | {md} | {lt} | {o['pct']:.2f} | {rd} | {wr} |\n")
     print(open(os.path.join(dst, "summary.md")).read())
 
 
