@@ -125,11 +125,18 @@ template <class Op> struct EpiTypes<Op, true> {
 // conflict-free (row step 8 mod 64 dwords; + 8 is 2.0x by tools/ldsbank.py), and the k-major
 // A tile also stores its rows bit-2/3 swapped for the transposing read (wg_row).
 template <typename T> DEV int wg_prow(int r) { if constexpr (sizeof(T) == 2) return wg_row(r); else return r; }
-template <typename T> constexpr int tile_pad() { return sizeof(T) == 2 ? 16 : 4; }
+// fp32 k-contiguous rows (LD = BK + 8 floats: the row step is 2 16-byte slots mod the 256-byte
+// bank row, so each of ds_read_b128's 16-lane groups -- lanes {0-3, 12-15, 20-27} etc., rows
+// lane & 15 at k offset 4 (lane >> 4) -- reads 16 distinct slots; at + 4 floats (1 slot per
+// row) rows r, g and r - 1, g + 1 shared a slot: 33 % of the FC forward's LDS cycles were
+// conflicts, profiles/r04pmc).  The k-major A tile keeps + 4.
+constexpr int F32_ROW_PAD = 8;
+template <typename T> constexpr int tile_pad() { return sizeof(T) == 2 ? 16 : F32_ROW_PAD; }
+template <typename T> constexpr int tile_pad_ak() { return sizeof(T) == 2 ? 16 : 4; }
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
 constexpr int gemm_tile_smem() {
   constexpr int LD = BK + tile_pad<T>();
-  constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + tile_pad<T>()) : BR * LD;
+  constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + tile_pad_ak<T>()) : BR * LD;
   return 2 * (ASZ + BC * LD);
 }
 // PF: K chunks held in registers ahead of the one being computed (1: the next chunk; 2: the
@@ -149,7 +156,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
   constexpr int NA = BR * KV / NT, NB = BC * KV / NT;
   constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
-  constexpr int LDA = AK ? BR + tile_pad<T>() : LD;  // A tile row length (elements)
+  constexpr int LDA = AK ? BR + tile_pad_ak<T>() : LD;  // A tile row length (elements)
   constexpr int ASZ = AK ? BK * LDA : BR * LD;
   constexpr int NK = Op::K / BK;
   static_assert((WR * WC == 4 || (WR * WC == 8 && !Op::TILE_EPI)) && TRW >= 1 && TCW >= 1, "tile");
