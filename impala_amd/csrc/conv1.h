@@ -806,10 +806,26 @@ template <typename T> constexpr int c12_groups() { return 2; }
 // read) in [Y][channel][X] rows of XP bytes (4 consecutive X in one 32-bit word) x 2, dY1 in
 // pixel rows iy * 16 + ix (240: the conv1 weight gradient's 15 k-steps = the 15 pixel rows,
 // ix = 15 a zero pad) x 2, dY2 rows (36) x 2, one half-Z tile per stride-parity class (2 taps x 32 channels; row 36
-// stays zero: the gather's out-of-range taps read it), the mask words x 2
+// stays zero: the gather's out-of-range taps read it), the mask words x 2.
+// The Z rows are 64 floats = 16 chunks of 16 B, unpadded; chunk c of row r is stored at chunk
+// c ^ zswz(r) (ZSWZ).  The Z stores write 8 consecutive rows at one chunk per ds_write_b128 lane
+// group (bank = address mod 128 B: zswz(r) mod 8 is a permutation of r mod 8), and a gather
+// read's 16-lane group (ds_read_b128 groups, MI355X_MICROARCH.md §LDS) takes chunks 0..3 of row r,
+// 4..7 of rows r + 1 and r + 2, 0..3 of row r + 3 (+ 8 per tap j2), for any r: bit 3 and bit 2
+// of zswz follow the row's parity, so the four 64-byte pieces land in four different quarters of
+// the 256-byte bank row.  With the round-3 pitch (68 floats) the same reads overlapped by up to
+// 3 chunks (39 % of the backward's LDS cycles were conflict cycles, profiles/r04pmc).
 struct C12B32 {
+  static constexpr bool ZSWZ = true;
+  // group B's conv1 weight gradient split over k (WKS): wave w takes k-blocks 2 w, 2 w + 1 of
+  // all four taps (the dY1 split into bf16 terms done once per value, not once per tap), the
+  // partials summed in wave order at the end; else wave w takes tap w over all eight k-blocks
+  static constexpr bool WKS = true;
   static constexpr int XP = 20, LDX = c1::LB<float>::LDX;  // image row bytes (X 0..16), dY1 row
-  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = P2, LDZ = 2 * OC1 + 4, ZROWS = P2 + 1;
+  static constexpr int NROW = 240, LDD = OC2 + 4, DROWS = P2, LDZ = 2 * OC1 + (ZSWZ ? 0 : 4),
+                       ZROWS = P2 + 1;
+  static_assert(2 * OC1 == 64, "Z rows of 16 chunks");
+  __device__ static constexpr int zswz(int r) { return ZSWZ ? ((r & 1) * 12) | ((r >> 1) & 3) : 0; }
   static constexpr int IMGW = c1::GRID * c1::CH * XP / 4, DYW = NROW * LDX, D2W = DROWS * LDD;
   static constexpr int IMG = 0, DYT = IMG + 2 * IMGW, D2S = DYT + 2 * DYW;
   static constexpr int Z0 = D2S + 2 * D2W, ZSZ = ZROWS * LDZ, MSK = Z0 + 4 * ZSZ;
@@ -907,11 +923,15 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};    // A: conv1 bias partials of this lane's 4 channels
   // A: W2 fragments wb[tap j1*2+j2][k-step][ci tile] (c12_load_w2; loaded here if load_w2)
   // ---- group B state ----
-  f32x4 acc[2][3];                          // B: conv1 weight gradient, oc tile i x ch tile j
+  // B: conv1 weight gradient [tap (WKS) ][oc tile i][ch tile j]
+  constexpr int NTB = L::WKS ? 4 : 1;
+  f32x4 acc[NTB][2][3];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int t = 0; t < NTB; ++t)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // group B's staging, global loads then LDS stores (the latency runs under group A's work):
   // frame fi's image bytes -> IMG[bi] as [Y][channel c = ci * 16 + bb * 4 + d][X] bytes (a
   // 4 x 4 byte transpose of the 16 bytes a thread loads: 4 cells X x 4 columns d), frame fd's
@@ -1017,12 +1037,17 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   // the groups run separate loops with the same barrier count (nF + 1), so that the compiler
   // keeps each group's loop-carried registers (A: the W2 fragments; B: the accumulators) apart
   if (is_a) {
+    // the gather's Z chunk selectors: nibble d = cg ^ zswz(row) for rows = slot + d (mod 8)
+    uint32_t zsel = 0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) zsel |= (uint32_t)(cg ^ L::zswz((slot + d) & 7)) << (4 * d);
     for (int it = 0; it < nF; ++it) {
       const int b = it & 1;
       // the gather's lane offsets recomputed per frame (not hoisted out of the loop as ~50 live
       // VGPRs)
       int sl = slot;
-      asm volatile("" : "+v"(sl));
+      uint32_t zt8 = zsel;
+      asm volatile("" : "+v"(sl), "+v"(zt8));
       const float* d2s = d2s_buf(b);
       const uint32_t* msk = msk_buf(b);
       float* dyt = dyt_buf(b);
@@ -1067,7 +1092,8 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
           const int op = 16 * rt + (lane & 15);
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc)
-            *reinterpret_cast<f32x4*>(zw + op * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) + kl) = z[rt][cc];
+            *reinterpret_cast<f32x4*>(zw + op * LDZ + 4 * ((8 * (cc >> 1) + 4 * (cc & 1) + (kl >> 2)) ^
+                                                          L::zswz(lane & 7))) = z[rt][cc];
         }
         {
           // the k-phase sums of the four cc at once: row cc of t holds cc's (rows_sum4), lane
@@ -1076,8 +1102,9 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
 #pragma unroll
           for (int q = 0; q < 4; ++q) t[q] = rows_sum4(z4[0][q], z4[1][q], z4[2][q], z4[3][q]);
           const int cc = lane >> 4;
-          *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ + (cc >> 1) * OC1 + 16 * (cc & 1) +
-                                    4 * ((lane >> 2) & 3)) = t;
+          *reinterpret_cast<f32x4*>(zw + (32 + (lane & 3)) * LDZ +
+                                    4 * ((8 * (cc >> 1) + 4 * (cc & 1) + ((lane >> 2) & 3)) ^
+                                         L::zswz(32 + (lane & 3)))) = t;
         }
         // the wave's own Z stores are done before its gather reads them (LDS is in order per
         // wave; the wait + clobber keeps the compiler from moving the reads up)
@@ -1096,7 +1123,10 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
           for (int j2 = 0; j2 < 2; ++j2) {
             const int oy = qy - hf, ox = qx - j2;
             const bool ok = pv && oy >= 0 && oy < H2 && ox >= 0 && ox < H2;
-            zz[j2] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + j2 * OC1 + 4 * cg);
+            // chunk (8 j2 + cg) ^ zswz(row): row mod 8 = (sl + d) mod 8, nibble d of zt8
+            const int d = (oy * H2 - j2) & 7;
+            const int zc = (int)((zt8 >> (4 * d)) & 15u) ^ (8 * j2);
+            zz[j2] = *reinterpret_cast<const f32x4*>(zw + (ok ? oy * H2 + ox : P2) * LDZ + 4 * zc);
           }
           if (hf == 1) {
             zz[2] = *reinterpret_cast<const f32x4*>(dyt + (pv ? iy * 16 + ix : 0) * LDX + 4 * cg);
@@ -1161,82 +1191,175 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
       typedef FB::vec VB;
       constexpr int NKB = 8;
       const int g = lane >> 4, col = lane & 15;
-      struct Raw {
-        float a[2][8];     // dY1 of oc 16 i + col, pixels 8 g .. 8 g + 7
-        uint32_t w[3][3];  // image dwords at X = 8 (g & 1) + {0, 4, 8}, channel tile j
-      };
-      auto load = [&](int kb, Raw& r) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int pr = min(32 * kb + 8 * g + c, L::NROW - 1);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) r.a[i][c] = dyt[pr * LDX + 16 * i + col];
-        }
-        const int Y = min(2 * kb + (g >> 1) + ty, c1::GRID - 1);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + (Y * c1::CH + 16 * j + col) * XP + 8 * (g & 1));
-#pragma unroll
-          for (int q = 0; q < 3; ++q) r.w[j][q] = wp[q];
-        }
-      };
       // the high halves of two fp32 words as a bf16 pair (x0 low, x1 high)
       auto hi2 = [](uint32_t x0, uint32_t x1) { return __builtin_amdgcn_perm(x1, x0, 0x07060302u); };
-      Raw rr[2];
-      load(0, rr[0]);
+      if constexpr (L::WKS) {
+        // ---- conv1 weight gradient of frame it - 1, k-blocks kb = 2 wave, 2 wave + 1 of all four
+        // taps (ty, tx), as three exact bf16 MFMA passes (the dY1 split below; B = the image
+        // bytes of cell (iy + ty, ix + tx), exact in bf16).  Lane group g holds pixels 8 g ..
+        // 8 g + 7 of the k-block: dY1 rows (clamped to the 240 that exist) and, per ty, image
+        // bytes X = 8 (g & 1) .. + 8, converted once for both tx.  Image row 15 (kb = 7, g >= 2)
+        // is padding: its image bytes are taken as zero. ----
+        struct Raw {
+          float a[2][8];        // dY1 of oc 16 i + col, pixels 8 g .. 8 g + 7
+          uint32_t w[2][3][3];  // [ty][channel tile j] image dwords at X = 8 (g & 1) + {0, 4, 8}
+        };
+        auto load = [&](int kb, Raw& r) {
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        const Raw& r = rr[kb & 1];
-        // A: the three terms of the 16 dY1 values
-        VB fa[2][3];
+          for (int c = 0; c < 8; ++c) {
+            const int pr = min(32 * kb + 8 * g + c, L::NROW - 1);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          uint32_t th[4], tm[4], tl[4];
+            for (int i = 0; i < 2; ++i) r.a[i][c] = dyt[pr * LDX + 16 * i + col];
+          }
+          const bool pad = kb == NKB - 1 && g >= 2;  // image row 15: zero bytes
 #pragma unroll
-          for (int c = 0; c < 8; c += 2) {
-            uint32_t x[2], r1[2], r2[2];
+          for (int ty = 0; ty < 2; ++ty) {
+            const int Y = min(2 * kb + (g >> 1) + ty, c1::GRID - 1);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              x[u] = __builtin_bit_cast(uint32_t, r.a[i][c + u]);
-              const float f1 = r.a[i][c + u] - __builtin_bit_cast(float, x[u] & 0xffff0000u);
-              r1[u] = __builtin_bit_cast(uint32_t, f1);
-              r2[u] = __builtin_bit_cast(uint32_t, f1 - __builtin_bit_cast(float, r1[u] & 0xffff0000u));
+            for (int j = 0; j < 3; ++j) {
+              const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + (Y * c1::CH + 16 * j + col) * XP + 8 * (g & 1));
+#pragma unroll
+              for (int q = 0; q < 3; ++q) r.w[ty][j][q] = pad ? 0u : wp[q];
             }
-            th[c / 2] = hi2(x[0], x[1]);
-            tm[c / 2] = hi2(r1[0], r1[1]);
-            tl[c / 2] = hi2(r2[0], r2[1]);
           }
-          fa[i][0] = __builtin_bit_cast(VB, th);
-          fa[i][1] = __builtin_bit_cast(VB, tm);
-          fa[i][2] = __builtin_bit_cast(VB, tl);
-        }
-        // B: 8 image bytes per channel tile -> bf16 (exact), zero on the padding row
-        const bool pad = kb == NKB - 1 && g >= 2;
-        VB fb[3];
+        };
+        Raw rr[2];
+        load(2 * wave, rr[0]);
+        load(2 * wave + 1, rr[1]);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const uint32_t w0 = __builtin_amdgcn_alignbyte(r.w[j][1], r.w[j][0], tx);
-          const uint32_t w1 = __builtin_amdgcn_alignbyte(r.w[j][2], r.w[j][1], tx);
-          uint32_t t[4];
+        for (int kk = 0; kk < 2; ++kk) {
+          const int kb = 2 * wave + kk;
+          const Raw& r = rr[kk];
+          // A: the three terms of the 16 dY1 values (truncation: the top 8 significand bits of x,
+          // then of the remainder, then the <= 8 bits left; each term's fp32 bits are its bf16 in
+          // the high half, every product the fp32 product)
+          VB fa[2][3];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const uint32_t w = h ? w1 : w0;
-            const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)(w & 255u));
-            const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> 8) & 255u));
-            const uint32_t f2 = __builtin_bit_cast(uint32_t, (float)((w >> 16) & 255u));
-            const uint32_t f3 = __builtin_bit_cast(uint32_t, (float)(w >> 24));
-            t[2 * h] = pad ? 0u : hi2(f0, f1);
-            t[2 * h + 1] = pad ? 0u : hi2(f2, f3);
+          for (int i = 0; i < 2; ++i) {
+            uint32_t th[4], tm[4], tl[4];
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+              uint32_t x[2], r1[2], r2[2];
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                x[u] = __builtin_bit_cast(uint32_t, r.a[i][c + u]);
+                const float f1 = r.a[i][c + u] - __builtin_bit_cast(float, x[u] & 0xffff0000u);
+                r1[u] = __builtin_bit_cast(uint32_t, f1);
+                r2[u] = __builtin_bit_cast(uint32_t, f1 - __builtin_bit_cast(float, r1[u] & 0xffff0000u));
+              }
+              th[c / 2] = hi2(x[0], x[1]);
+              tm[c / 2] = hi2(r1[0], r1[1]);
+              tl[c / 2] = hi2(r2[0], r2[1]);
+            }
+            fa[i][0] = __builtin_bit_cast(VB, th);
+            fa[i][1] = __builtin_bit_cast(VB, tm);
+            fa[i][2] = __builtin_bit_cast(VB, tl);
           }
-          fb[j] = __builtin_bit_cast(VB, t);
+#pragma unroll
+          for (int ty = 0; ty < 2; ++ty) {
+            // B of taps (ty, 0) and (ty, 1), one channel tile j at a time: image bytes X = 0 .. 8
+            // (from 8 (g & 1)) -> fp32 (exact), pairs (X, X + 1) from X = tx as bf16 (the high
+            // halves; exact for bytes)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              uint32_t f[9];
+#pragma unroll
+              for (int k = 0; k < 9; ++k)
+                f[k] = __builtin_bit_cast(uint32_t, (float)((r.w[ty][j][k >> 2] >> (8 * (k & 3))) & 255u));
+              VB fb[2];
+#pragma unroll
+              for (int tx = 0; tx < 2; ++tx) {
+                uint32_t t[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) t[p] = hi2(f[2 * p + tx], f[2 * p + tx + 1]);
+                fb[tx] = __builtin_bit_cast(VB, t);
+              }
+#pragma unroll
+              for (int tx = 0; tx < 2; ++tx)
+#pragma unroll
+                for (int tm = 0; tm < 3; ++tm)
+#pragma unroll
+                  for (int i = 0; i < 2; ++i)
+                    acc[2 * ty + tx][i][j] = FB::mma(fa[i][tm], fb[tx], acc[2 * ty + tx][i][j]);
+            }
+          }
         }
-        if (kb + 1 < NKB) load(kb + 1, rr[(kb + 1) & 1]);
-#pragma unroll
-        for (int tm = 0; tm < 3; ++tm)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) acc[i][j] = FB::mma(fa[i][tm], fb[j], acc[i][j]);
+      } else {
+        struct Raw {
+          float a[2][8];     // dY1 of oc 16 i + col, pixels 8 g .. 8 g + 7
+          uint32_t w[3][3];  // image dwords at X = 8 (g & 1) + {0, 4, 8}, channel tile j
+        };
+        auto load = [&](int kb, Raw& r) {
+  #pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const int pr = min(32 * kb + 8 * g + c, L::NROW - 1);
+  #pragma unroll
+            for (int i = 0; i < 2; ++i) r.a[i][c] = dyt[pr * LDX + 16 * i + col];
+          }
+          const int Y = min(2 * kb + (g >> 1) + ty, c1::GRID - 1);
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + (Y * c1::CH + 16 * j + col) * XP + 8 * (g & 1));
+  #pragma unroll
+            for (int q = 0; q < 3; ++q) r.w[j][q] = wp[q];
+          }
+        };
+        Raw rr[2];
+        load(0, rr[0]);
+  #pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          const Raw& r = rr[kb & 1];
+          // A: the three terms of the 16 dY1 values
+          VB fa[2][3];
+  #pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            uint32_t th[4], tm[4], tl[4];
+  #pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+              uint32_t x[2], r1[2], r2[2];
+  #pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                x[u] = __builtin_bit_cast(uint32_t, r.a[i][c + u]);
+                const float f1 = r.a[i][c + u] - __builtin_bit_cast(float, x[u] & 0xffff0000u);
+                r1[u] = __builtin_bit_cast(uint32_t, f1);
+                r2[u] = __builtin_bit_cast(uint32_t, f1 - __builtin_bit_cast(float, r1[u] & 0xffff0000u));
+              }
+              th[c / 2] = hi2(x[0], x[1]);
+              tm[c / 2] = hi2(r1[0], r1[1]);
+              tl[c / 2] = hi2(r2[0], r2[1]);
+            }
+            fa[i][0] = __builtin_bit_cast(VB, th);
+            fa[i][1] = __builtin_bit_cast(VB, tm);
+            fa[i][2] = __builtin_bit_cast(VB, tl);
+          }
+          // B: 8 image bytes per channel tile -> bf16 (exact), zero on the padding row
+          const bool pad = kb == NKB - 1 && g >= 2;
+          VB fb[3];
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(r.w[j][1], r.w[j][0], tx);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(r.w[j][2], r.w[j][1], tx);
+            uint32_t t[4];
+  #pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t w = h ? w1 : w0;
+              const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)(w & 255u));
+              const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> 8) & 255u));
+              const uint32_t f2 = __builtin_bit_cast(uint32_t, (float)((w >> 16) & 255u));
+              const uint32_t f3 = __builtin_bit_cast(uint32_t, (float)(w >> 24));
+              t[2 * h] = pad ? 0u : hi2(f0, f1);
+              t[2 * h + 1] = pad ? 0u : hi2(f2, f3);
+            }
+            fb[j] = __builtin_bit_cast(VB, t);
+          }
+          if (kb + 1 < NKB) load(kb + 1, rr[(kb + 1) & 1]);
+  #pragma unroll
+          for (int tm = 0; tm < 3; ++tm)
+  #pragma unroll
+            for (int j = 0; j < 3; ++j)
+  #pragma unroll
+              for (int i = 0; i < 2; ++i) acc[0][i][j] = FB::mma(fa[i][tm], fb[j], acc[0][i][j]);
+        }
       }
       stage_st(it < nF ? f0 + it : -1, it & 1, it + 1 < nF ? f0 + it + 1 : -1, (it + 1) & 1, sr);
       __syncthreads();
@@ -1245,6 +1368,19 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   // conv1 bias: group A's 32 lanes of each channel group (8 per wave, 4 waves) in a fixed order
   float* bred = smem + L::Z0;
   if (is_a) *reinterpret_cast<f32x4*>(bred + 4 * tid) = f32x4{bsum[0], bsum[1], bsum[2], bsum[3]};
+  // WKS: group B's k-block partials of every tap -> the image / dY1 tiles' space (free now)
+  f32x4* wpart = reinterpret_cast<f32x4*>(smem + L::IMG);
+  static_assert(!L::WKS || 4 * 4 * 6 * 64 * 4 <= L::D2S - L::IMG, "partials fit");
+  if constexpr (L::WKS) {
+    if (!is_a) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) wpart[((wave * 4 + t) * 6 + 3 * i + j) * 64 + lane] = acc[t][i][j];
+    }
+  }
   __syncthreads();
   if (is_a && tid < OC1) {
     float bs = 0.f;
@@ -1253,6 +1389,18 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     slab_bias[(size_t)wg * OC1 + tid] = bs;
   }
   if (!is_a) {
+    // wave w writes tap w (WKS: the four waves' k-block partials of it, summed in wave order)
+    if constexpr (L::WKS) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          f32x4 v = wpart[((0 * 4 + wave) * 6 + 3 * i + j) * 64 + lane];
+#pragma unroll
+          for (int w = 1; w < 4; ++w) v += wpart[((w * 4 + wave) * 6 + 3 * i + j) * 64 + lane];
+          acc[0][i][j] = v;
+        }
+    }
     const size_t so = (size_t)wg * OC1 * K1;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1261,7 +1409,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
         const int col = wave * c1::CH + 16 * j + (lane & 15);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[i][j][q] * (1.f / 255.f);
+          slab[so + (size_t)(16 * i + 4 * (lane >> 4) + q) * K1 + col] = acc[0][i][j][q] * (1.f / 255.f);
       }
   }
 }
