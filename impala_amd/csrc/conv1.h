@@ -1183,7 +1183,9 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
       // half the cycles of 16x16x4 f32 for 8x the K.  k-block kb = pixel rows 32 kb .. 32 kb + 31
       // (image rows 2 kb, 2 kb + 1); lane group g holds pixels 8 g .. 8 g + 7 of it: dY1 rows
       // (clamped to the 240 that exist) and 8 consecutive image bytes (funnel-shifted by tx).
-      // The 16 pixels of image row 15 (kb = 7, g >= 2) are padding: their B operand is zero. ----
+      // The 16 pixels of image row 15 (kb = 7, g >= 2) are padding: their B operand is zero.
+      // WKS: each wave takes two k-blocks of all four taps; else tap (ty, tx) = wave over all
+      // eight k-blocks. ----
       const int b = (it - 1) & 1;
       const float* dyt = dyt_buf(b);
       const uint8_t* img = img_buf(b);
@@ -1194,12 +1196,8 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
       // the high halves of two fp32 words as a bf16 pair (x0 low, x1 high)
       auto hi2 = [](uint32_t x0, uint32_t x1) { return __builtin_amdgcn_perm(x1, x0, 0x07060302u); };
       if constexpr (L::WKS) {
-        // ---- conv1 weight gradient of frame it - 1, k-blocks kb = 2 wave, 2 wave + 1 of all four
-        // taps (ty, tx), as three exact bf16 MFMA passes (the dY1 split below; B = the image
-        // bytes of cell (iy + ty, ix + tx), exact in bf16).  Lane group g holds pixels 8 g ..
-        // 8 g + 7 of the k-block: dY1 rows (clamped to the 240 that exist) and, per ty, image
-        // bytes X = 8 (g & 1) .. + 8, converted once for both tx.  Image row 15 (kb = 7, g >= 2)
-        // is padding: its image bytes are taken as zero. ----
+        // k-blocks kb = 2 wave, 2 wave + 1 of all four taps: per ty, image bytes X = 8 (g & 1)
+        // .. + 8, converted once for both tx; padding pixels take zero image bytes
         struct Raw {
           float a[2][8];        // dY1 of oc 16 i + col, pixels 8 g .. 8 g + 7
           uint32_t w[2][3][3];  // [ty][channel tile j] image dwords at X = 8 (g & 1) + {0, 4, 8}
@@ -1228,8 +1226,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
         load(2 * wave + 1, rr[1]);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          const int kb = 2 * wave + kk;
-          const Raw& r = rr[kk];
+          const Raw& r = rr[kk];  // k-block 2 wave + kk
           // A: the three terms of the 16 dY1 values (truncation: the top 8 significand bits of x,
           // then of the remainder, then the <= 8 bits left; each term's fp32 bits are its bf16 in
           // the high half, every product the fp32 product)
