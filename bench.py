@@ -309,6 +309,68 @@ def _cpu_baseline(ref_cpu, B, T, A, seconds, warmup):
                       f"{med * 1e3:.1f} ms"}
 
 
+class StepClock:
+    """Per-step device times of a timed region (SURVEY.md §8(d) defines the metric on the
+    median step): a timing event recorded on the launch stream before every step and one after
+    the last, read once the region has ended (no host sync inside it).  Step i's time is
+    event i -> event i+1, so the steps tile the region's device time with no gaps.  Optionally
+    the host's own per-iteration times (enqueue + any host wait inside the loop body)."""
+
+    def __init__(self, n, host=False):
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        self.host = [] if host else None
+        self.i = 0
+        self._t = None
+
+    def mark(self):
+        self.ev[self.i].record()
+        self.i += 1
+        if self.host is not None:
+            t = time.perf_counter()
+            if self._t is not None:
+                self.host.append(t - self._t)
+            self._t = t
+
+    def summary(self, digits=4):
+        """-> per-step statistics in ms (call after the region's final synchronize)."""
+        n = self.i - 1
+        ms = np.array([self.ev[i].elapsed_time(self.ev[i + 1]) for i in range(n)])
+        med = float(np.median(ms))
+        out = {"ms_per_step_median": round(med, digits),
+               "ms_per_step_min": round(float(ms.min()), digits),
+               "ms_per_step_max": round(float(ms.max()), digits),
+               "ms_per_step_p90": round(float(np.percentile(ms, 90)), digits),
+               "slow_steps": [int(i) for i in np.nonzero(ms > 2 * med)[0]],
+               "events_sum_ms": round(float(ms.sum()), digits)}
+        if n <= 256:
+            out["step_ms"] = [round(float(x), digits) for x in ms]
+        if self.host:
+            h = np.array(self.host) * 1e3
+            out["host_ms_per_iter_median"] = round(float(np.median(h)), digits)
+            out["host_ms_per_iter_max"] = round(float(h.max()), digits)
+            if len(h) <= 256:
+                out["host_ms"] = [round(float(x), digits) for x in h]
+        return out
+
+
+def step_stats(clock, dist, dev):
+    """StepClock.summary(), with the per-step arrays taken as the element-wise max over ranks
+    (the slowest rank sets every step) when data parallel."""
+    s = clock.summary()
+    if dist is None or "step_ms" not in s:
+        return s
+    t = torch.tensor(s["step_ms"], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = t.cpu().numpy()
+    med = float(np.median(ms))
+    s.update({"ms_per_step_median": round(med, 4), "ms_per_step_max": round(float(ms.max()), 4),
+              "ms_per_step_min": round(float(ms.min()), 4),
+              "ms_per_step_p90": round(float(np.percentile(ms, 90)), 4),
+              "slow_steps": [int(i) for i in np.nonzero(ms > 2 * med)[0]],
+              "step_ms": [round(float(x), 4) for x in ms], "over_ranks": "max per step"})
+    return s
+
+
 def run_host_staged(eng, batch, args, dist, model, world):
     """The PCIe-inclusive rate (SURVEY.md §8(d) secondary bound; never `value`): every step's
     batch comes from page-locked host memory through the library's staging ring
@@ -322,7 +384,7 @@ def run_host_staged(eng, batch, args, dist, model, world):
     hosts = [[t.cpu().pin_memory() for t in batch] for _ in range(2)]
     eng.stage_init(2)
 
-    def run(n):
+    def run(n, clock=None):
         eng.stage(0, *hosts[0])
         for k in range(n):
             s = k % 2
@@ -330,6 +392,8 @@ def run_host_staged(eng, batch, args, dist, model, world):
                 eng.stage_wait(1 - s)
                 eng.stage(1 - s, *hosts[1 - s])
             b = eng.slot_batch(s)
+            if clock is not None:
+                clock.mark()
             if dist is None:
                 eng.train_step(b)
             elif getattr(eng, "_dp", False):
@@ -338,14 +402,18 @@ def run_host_staged(eng, batch, args, dist, model, world):
                 compute_grads_allreduced(eng, (b,), model.flat_grad)
                 eng.apply_update()
             eng.slot_release(s)
+        if clock is not None:
+            clock.mark()
 
     run(max(args.warmup, 2))
     torch.cuda.synchronize()
+    settled = settle(lambda: run(1), args.settle_ms)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    clock = StepClock(args.steps, host=True)
     t0 = time.perf_counter()
-    run(args.steps)
+    run(args.steps, clock)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -355,8 +423,12 @@ def run_host_staged(eng, batch, args, dist, model, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     nbytes = sum(t.numel() * t.element_size() for t in hosts[0])
+    st = step_stats(clock, dist, model.flat.device)
     return {"value": round(world * eng.frames * args.steps / elapsed, 1), "unit": "env-frames/s",
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "h2d_bytes_per_step": nbytes,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "value_at_median": round(world * eng.frames / (st["ms_per_step_median"] * 1e-3), 1),
+            **st, "settle": {"min_ms": args.settle_ms, "steps": settled},
+            "h2d_bytes_per_step": nbytes,
             "h2d_GBps_per_gpu": round(nbytes * args.steps / elapsed / 1e9, 2),
             "note": "rollouts staged from page-locked host memory every step (impala_stage ring, "
                     "2 slots, obs over 2 SDMA streams, H2D overlapped with the previous update; "
@@ -618,6 +690,11 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
                     help="operand precision of the headline step (fp32 = the reference's)")
     ap.add_argument("--roofline-kernel", default=None)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="untimed steps for at least this much wall time (device synced) right "
+                         "before each timed region, after the --warmup steps: the GPU clock "
+                         "ramps over tens of ms of steady work (profiles/r05b), which a "
+                         "20-step region would otherwise sample mid-ramp")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-seconds-1t", type=float, default=8.0,
                     help="sample length of the 1-thread CPU baseline leg")
@@ -707,7 +784,11 @@ def main():
     torch.cuda.synchronize()
     work = kernel_work(2 if args.dtype == "bf16" else 4)
     kernel_us, top = select_kernels(eng, step, work, args)
-    elapsed, _ = timed_steps(eng, step, [], args, dist, dev)  # the headline: no stamps
+    settled = settle(step, args.settle_ms)
+    clock = StepClock(args.steps)
+    elapsed, _ = timed_steps(eng, step, [], args, dist, dev, clock)  # the headline: no kernel stamps
+    steps_stat = step_stats(clock, dist, dev)
+    elapsed_nomark, _ = timed_steps(eng, step, [], args, dist, dev)
     elapsed_st, k_times = timed_steps(eng, step, top, args, dist, dev)
     met = eng.metrics.cpu().numpy()
     if not np.all(np.isfinite(met)):
@@ -741,7 +822,11 @@ def main():
         "roofline_top2": rooflines,
         "step_roofline": step_roofline(value / world, step_flops_pf, args.dtype),
         "kernel_us": kernel_us,
+        **steps_stat,
+        "value_at_median": round(world * B * T / (steps_stat["ms_per_step_median"] * 1e-3), 1),
+        "ms_per_step_unmarked": round(elapsed_nomark * 1e3 / args.steps, 4),
         "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
+        "settle": {"min_ms": args.settle_ms, "steps": settled},
     }
     if not args.no_alt_line:
         alt = "fp32" if args.dtype == "bf16" else "bf16"
@@ -818,10 +903,25 @@ def dp_variants(args, B, T, A, dev, dist, world, batch):
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
     out, finals = {}, {}
+
+    def all_ok(err):
+        """Every rank learns whether any rank failed its local part (MIN of the ok flags), so
+        that all ranks leave together instead of some entering a collective alone."""
+        ok = torch.tensor([0 if err else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        return bool(ok.item())
+
     for name, native, buckets in DP_VARIANTS:
-        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=args.dtype, seed=0)
-        e = Engine(m, batch_size=B, rollout_length=T, world_size=world, algo=args.algo)
-        m._train_engine = e
+        err = None
+        try:
+            m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=args.dtype, seed=0)
+            e = Engine(m, batch_size=B, rollout_length=T, world_size=world, algo=args.algo)
+            m._train_engine = e
+        except Exception as ex:  # noqa: BLE001 -- e.g. out of memory for the extra engine
+            err = f"{type(ex).__name__}: {ex}"[:300]
+        if not all_ok(err):
+            out[name] = {"error": err or "failed on another rank"}
+            break
         dist.broadcast(m.flat, 0)
         m.params_changed()
         if native:
@@ -876,17 +976,24 @@ def select_kernels(eng, step, work, args):
     return table, top
 
 
-def timed_steps(eng, step, kernels, args, dist, dev):
+def timed_steps(eng, step, kernels, args, dist, dev, clock=None):
     """The timed region: --steps steps between barriers + device syncs; the given kernels' own
-    durations are stamped live (hipExtLaunchKernel events on their launch stream)."""
+    durations are stamped live (hipExtLaunchKernel events on their launch stream).  With a
+    StepClock, a timing event is recorded before every step and after the last."""
     for k in kernels:
         eng.timer_start(k, args.steps)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if clock is None:
+        for _ in range(args.steps):
+            step()
+    else:
+        for _ in range(args.steps):
+            clock.mark()
+            step()
+        clock.mark()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -897,6 +1004,24 @@ def timed_steps(eng, step, kernels, args, dist, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, k_times
+
+
+def settle(step, min_ms, max_steps=20000):
+    """Untimed steps until `min_ms` of wall time has passed (device synced): the GPU's clocks
+    and the runtime's lazily created queues settle before a short timed region.  Returns the
+    number of steps run."""
+    if min_ms <= 0:
+        return 0
+    n = 0
+    t_end = time.perf_counter() + min_ms * 1e-3
+    while n < max_steps:
+        for _ in range(10):
+            step()
+        n += 10
+        torch.cuda.synchronize()
+        if time.perf_counter() >= t_end:
+            break
+    return n
 
 
 def kernel_roofline(k, timing, work, frames, dtype, algo):
@@ -962,11 +1087,16 @@ def alt_line(dtype, args, B, T, A, dev, dist, world, make_step, ppo):
     work = kernel_work(2 if dtype == "bf16" else 4)
     table, top = select_kernels(e, step, work, argparse.Namespace(steps=args.steps,
                                                                    roofline_kernel=None))
-    elapsed, _ = timed_steps(e, step, [], args, dist, dev)
+    settled = settle(step, args.settle_ms)
+    clock = StepClock(args.steps)
+    elapsed, _ = timed_steps(e, step, [], args, dist, dev, clock)
+    st = step_stats(clock, dist, dev)
     elapsed_st, k_times = timed_steps(e, step, top[:1], args, dist, dev)
     value = world * B * T * args.steps / elapsed
     out = {"dtype": dtype, "value": round(value, 1), "unit": "env-frames/s",
-           "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+           "ms_per_step": round(elapsed * 1e3 / args.steps, 4), **st,
+           "value_at_median": round(world * B * T / (st["ms_per_step_median"] * 1e-3), 1),
+           "settle": {"min_ms": args.settle_ms, "steps": settled},
            "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
            "step_roofline": step_roofline(value / world, STEP_FLOPS_PER_FRAME if not ppo
                                           else STEP_FLOPS_PER_FRAME_PPO, dtype),

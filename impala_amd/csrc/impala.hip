@@ -753,6 +753,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   // the measured-slower alternatives are compiled into A/B builds only (common.h IMPALA_AB)
   for (const char* v : {"IMPALA_FC_SPLITK", "IMPALA_FWD_CHAIN", "IMPALA_FUSED_UPDATE",
                         "IMPALA_EARLY_RED"}) {
+    // the split-K FC forward is an fp32-only variant: bf16 handles ignore the switch, as the
+    // A/B build does
+    if (cfg->dtype != IMPALA_DTYPE_F32 && std::string(v) == "IMPALA_FC_SPLITK") continue;
     const char* e = std::getenv(v);
     if (e && e[0] && e[0] != '0')
       return fail(IMPALA_E_UNSUPPORTED, std::string(v) + " selects an A/B variant this library "
@@ -1377,6 +1380,69 @@ int impala_gather_rows(const void* const* src, void* const* dst, const size_t* r
   return 0;
 }
 
+// Prime the copy path at init: the learner's staging loop (ImpalaLearner._stage_host) for
+// IMPALA_STAGE_PRIME rounds (default 24, 0 = off) on a page-locked scratch batch, with a
+// 250 us spin kernel on a private stream standing in for each step.  An H2D hipMemcpyAsync is
+// given an SDMA engine by the runtime at issue time (hsa_amd_memory_get_preferred_copy_engine /
+// copy_engine_status, then hsa_amd_memory_async_copy_on_engine), and the first copy given an
+// engine creates that engine's queue inside the call: a 6-9 ms host stall before the copy is
+// submitted (HIP + HSA API traces, profiles/r05d; hsa_queue_create alone takes 6-6.5 ms here).
+// Which engines a loop gets depends on what is in flight and waiting when it issues (copies
+// queued behind the previous step's events), so rounds of copies with nothing to wait for did
+// not reach them (r05c, r05e); in the driver's 20-step host-staged pass one such stall landed
+// in the timed steps (0.67 ms per step against a 0.30 ms median, profiles/r05a).
+int prime_copy_path(impala_learner* h) {
+  int rounds = 24;
+  if (const char* e = std::getenv("IMPALA_STAGE_PRIME")) rounds = std::max(0, std::atoi(e));
+  if (rounds == 0 || h->n_slots < 2) return 0;
+  const size_t N = (size_t)h->N;
+  const size_t sz[5] = {N * 3 * 64 * 64, N * 8, N * 4, N * 4, N * (size_t)h->A * 4};
+  size_t total = 0;
+  for (size_t b : sz) total += (b + 255) & ~(size_t)255;
+  char* scratch = nullptr;
+  CK(hipHostMalloc((void**)&scratch, total, hipHostMallocDefault));
+  std::memset(scratch, 0, total);
+  impala_batch hb{};
+  {
+    size_t o = 0;
+    const void* p[5];
+    for (int f = 0; f < 5; ++f) {
+      p[f] = scratch + o;
+      o += (sz[f] + 255) & ~(size_t)255;
+    }
+    hb = impala_batch{(const uint8_t*)p[0], (const int64_t*)p[1], (const float*)p[2],
+                      (const float*)p[3], (const float*)p[4]};
+  }
+  hipStream_t cs = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+  int r = e == hipSuccess ? impala_stage(h, &hb, 0) : (int)e;
+  for (int k = 0; k < rounds && r == 0 && e == hipSuccess; ++k) {
+    const int s = k & 1;
+    e = hipEventSynchronize(h->ring[1 - s].ready);             // stage_wait(1 - s)
+    if (e == hipSuccess) r = impala_stage(h, &hb, 1 - s);      // stage(1 - s)
+    if (r == 0 && e == hipSuccess) e = hipStreamWaitEvent(cs, h->ring[s].ready, 0);  // slot_batch(s)
+    if (r == 0 && e == hipSuccess) {
+      stage_prime_spin_kernel<<<1, 64, 0, cs>>>(25000);      // the "step" (250 us)
+      e = hipGetLastError();
+    }
+    if (r == 0 && e == hipSuccess) e = hipEventRecord(h->ring[s].done, cs);  // slot_release(s)
+  }
+  if (cs) {
+    const hipError_t es = hipStreamSynchronize(cs);
+    if (e == hipSuccess) e = es;
+  }
+  for (int i = 0; i < h->n_h2d; ++i) {
+    const hipError_t es = hipStreamSynchronize(h->h2d_s[i]);
+    if (e == hipSuccess) e = es;
+  }
+  if (cs) (void)hipStreamDestroy(cs);
+  (void)hipHostFree(scratch);
+  if (r) return r;
+  if (e != hipSuccess)
+    return fail((int)e, std::string("impala_stage_init (copy-path priming): ") + hipGetErrorString(e));
+  return 0;
+}
+
 int impala_stage_init(impala_learner* h, int nslots) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (nslots < 1 || nslots > impala_learner::kMaxStageSlots)
@@ -1435,6 +1501,12 @@ int impala_stage_init(impala_learner* h, int nslots) {
                          (const float*)(s.mem + o_mu)};
   }
   h->n_slots = nslots;
+  if (h->h2d_pull_wg == 0) {
+    if (int r = prime_copy_path(h)) {
+      free_ring(h);
+      return r;
+    }
+  }
   return 0;
 }
 

@@ -1174,6 +1174,17 @@ __global__ __launch_bounds__(1024) void h2d_pull_kernel(const PullArgs a) {
   }
 }
 
+// Stands in for a learner step while impala_stage_init primes the copy path: one lane waits
+// `ticks` of the 100 MHz real-time counter (bounded: at most 2^20 sleep rounds).
+__global__ __launch_bounds__(64) void stage_prime_spin_kernel(long long ticks) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < (1 << 20); ++i) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   const int i = blockIdx.x, f = blockIdx.y;
   if (i >= a.n || f >= a.nfields) return;

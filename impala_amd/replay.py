@@ -120,6 +120,8 @@ class DeviceReplayBuffer(ReplayBuffer):
         # page-locked ring for the sampled slot indices: their H2D is a true asynchronous copy
         # (from pageable memory it would wait behind the learner stream's queued work while
         # sample() holds the lock); a ring entry is reused after its copy has run
+        # page-locked index ring (_indices_to_device): starts at 4 entries, grows when the
+        # learner's stream runs further ahead than that
         self._idx_buf: List[Optional[torch.Tensor]] = [None] * 4
         self._idx_ev: List[Optional[torch.cuda.Event]] = [None] * 4
         self._idx_next = 0
@@ -163,12 +165,21 @@ class DeviceReplayBuffer(ReplayBuffer):
 
     def _indices_to_device(self, idx: np.ndarray, stream) -> torch.Tensor:
         """Slot indices -> a device int64 tensor, copied on `stream` from a page-locked ring
-        entry (asynchronous: nothing here waits for the stream's queued work)."""
+        entry (asynchronous: nothing here waits for the stream's queued work).  Called with
+        ``_cv`` held, so it never blocks on the device: when the next entry's previous copy is
+        still queued (the learner runs more than the ring's length ahead), the ring grows by a
+        fresh entry instead, up to ``_IDX_RING_MAX`` entries."""
         k = self._idx_next
-        self._idx_next = (k + 1) % len(self._idx_buf)
         ev = self._idx_ev[k]
-        if ev is not None:
-            ev.synchronize()  # the entry's previous copy (4 samples ago) has run
+        if ev is not None and not ev.query():
+            if len(self._idx_buf) < self._IDX_RING_MAX:
+                # the busy entry (the oldest) moves one place on and stays next in line
+                self._idx_buf.insert(k, None)
+                self._idx_ev.insert(k, None)
+                ev = None
+            else:  # bounded: only a learner thousands of steps ahead reaches this
+                ev.synchronize()
+        self._idx_next = (k + 1) % len(self._idx_buf)
         n = len(idx)
         buf = self._idx_buf[k]
         if buf is None or buf.numel() < n:
