@@ -407,7 +407,7 @@ def run_host_staged(eng, batch, args, dist, model, world):
 
     run(max(args.warmup, 2))
     torch.cuda.synchronize()
-    settled = settle(lambda: run(1), args.settle_ms)
+    settled = settle(lambda: run(1), args.settle_ms, dist, model.flat.device)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -784,7 +784,7 @@ def main():
     torch.cuda.synchronize()
     work = kernel_work(2 if args.dtype == "bf16" else 4)
     kernel_us, top = select_kernels(eng, step, work, args)
-    settled = settle(step, args.settle_ms)
+    settled = settle(step, args.settle_ms, dist, dev)
     clock = StepClock(args.steps)
     elapsed, _ = timed_steps(eng, step, [], args, dist, dev, clock)  # the headline: no kernel stamps
     steps_stat = step_stats(clock, dist, dev)
@@ -1006,20 +1006,28 @@ def timed_steps(eng, step, kernels, args, dist, dev, clock=None):
     return elapsed, k_times
 
 
-def settle(step, min_ms, max_steps=20000):
+def settle(step, min_ms, dist=None, dev=None, max_steps=20000):
     """Untimed steps until `min_ms` of wall time has passed (device synced): the GPU's clocks
-    and the runtime's lazily created queues settle before a short timed region.  Returns the
-    number of steps run."""
+    and the runtime's lazily created queues settle before a short timed region.  Data parallel:
+    every rank runs the same number of steps (each step holds collectives), rank 0's clock
+    deciding after every 10 (a broadcast of its flag).  Returns the number of steps run."""
     if min_ms <= 0:
         return 0
     n = 0
     t_end = time.perf_counter() + min_ms * 1e-3
+    flag = torch.zeros(1, dtype=torch.int32, device=dev) if dist is not None else None
     while n < max_steps:
         for _ in range(10):
             step()
         n += 10
-        torch.cuda.synchronize()
-        if time.perf_counter() >= t_end:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        done = time.perf_counter() >= t_end
+        if dist is not None:
+            flag.fill_(int(done))
+            dist.broadcast(flag, 0)
+            done = bool(flag.item())
+        if done:
             break
     return n
 
@@ -1087,7 +1095,7 @@ def alt_line(dtype, args, B, T, A, dev, dist, world, make_step, ppo):
     work = kernel_work(2 if dtype == "bf16" else 4)
     table, top = select_kernels(e, step, work, argparse.Namespace(steps=args.steps,
                                                                    roofline_kernel=None))
-    settled = settle(step, args.settle_ms)
+    settled = settle(step, args.settle_ms, dist, dev)
     clock = StepClock(args.steps)
     elapsed, _ = timed_steps(e, step, [], args, dist, dev, clock)
     st = step_stats(clock, dist, dev)

@@ -121,3 +121,48 @@ def test_replicas_bitwise_equal_over_gloo():
     for p in ps:
         p.join(60)
     assert res == [(0, True, False), (1, True, False)]
+
+
+def _settle_worker(rank, world, port, q):
+    import os
+    import time
+
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = [0]
+
+    def step():  # a collective per step, and rank-dependent step times
+        calls[0] += 1
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        time.sleep(0.001 * (1 + 3 * rank))
+
+    n = bench.settle(step, 60.0, dist, torch.device("cpu"))
+    t = torch.tensor([float(n)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # would hang if the ranks' step counts differed
+    q.put((rank, n, calls[0], int(t.item())))
+    dist.destroy_process_group()
+
+
+def test_settle_keeps_ranks_in_lockstep_over_gloo():
+    """bench.settle (the untimed clock-settling steps before each timed region) runs the same
+    number of steps on every rank when ranks run at different speeds: each step holds a
+    collective, so a per-rank time check would leave one rank in an all-reduce alone."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_settle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    (r0, n0, c0, m0), (r1, n1, c1, m1) = res
+    assert n0 == n1 == c0 == c1 == m0 == m1 and n0 >= 10 and n0 % 10 == 0
