@@ -296,6 +296,12 @@ template <typename T> struct C12FLds {
 
 // The kernel body on workgroup `wg` (frames wg*fpw ..) with the LDS passed in
 // (C12FLds<T>::ELEMS elements)
+// act1's store cache policy: bf16 streams it non-temporally (nt: it is re-read only by the
+// conv2 weight gradient two launches later), forward 22.8 -> 22.0 us, step 0.1035-0.1039 ->
+// 0.1027-0.1031 ms; fp32 unchanged within noise, so it keeps the default (tools/var_specs/ntst.py,
+// profiles/r05nt; nt on every activation store made the fp32 forward 60 -> 66 us)
+template <typename T> constexpr int kAct1Cpol = sizeof(T) == 2 ? 2 : 0;
+
 template <typename T>
 DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1,
                          const float* __restrict__ b1, const T* __restrict__ w2,
@@ -510,11 +516,11 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         store4(arow + oc, v);
         if constexpr (sizeof(T) == 2) {
           const i32x2 d = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(d, rs_act1, gofs + oc * 2, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(d, rs_act1, gofs + oc * 2, 0, kAct1Cpol<T>);
         } else {
           const i32x4 d = {(int)__float_as_uint(v[0]), (int)__float_as_uint(v[1]),
                            (int)__float_as_uint(v[2]), (int)__float_as_uint(v[3])};
-          __builtin_amdgcn_raw_buffer_store_b128(d, rs_act1, gofs + oc * 4, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(d, rs_act1, gofs + oc * 4, 0, kAct1Cpol<T>);
         }
       }
       bits = xor32_or(xor16_or(bits));
