@@ -4,6 +4,8 @@
 # variant in $V, then the bench for each variant
 set -o pipefail
 export TMPDIR=/tmp
+# the variants live in the A/B build only (python -m impala_amd.build --ab)
+export IMPALA_HIP_LIB=impala_amd/libimpala_hip_ab.so
 O=gpurun_out/fcsk
 V=${V:-2}
 mkdir -p $O
