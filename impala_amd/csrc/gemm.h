@@ -372,6 +372,12 @@ template <class Op> struct wg_direct<Op, decltype(void(Op::DIRECT))> {
 // LDS passed in (gemm_wg_smem elements).
 // bf16 rows are stored bit-2/3 swapped (wg_row) at a pitch of BR / BC + 16 (conflict-free
 // transposing fragment reads); fp32 rows in order at + 4.
+template <class Op, class = void> struct wg_ycur { static constexpr bool value = false; };
+template <class Op> struct wg_ycur<Op, decltype(void(Op::YCUR))> {
+  static constexpr bool value = Op::YCUR;
+};
+template <class Op, bool = wg_ycur<Op>::value> struct WgYCur { struct type { int n, p; }; };
+template <class Op> struct WgYCur<Op, true> { typedef typename Op::YCur type; };
 template <typename T> constexpr int wg_pad() { return sizeof(T) == 2 ? 16 : 4; }
 template <typename T, int BR, int BC, int BM, int G>
 constexpr int gemm_wg_smem() {
@@ -436,6 +442,19 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
 #pragma unroll
   for (int i = 0; i < NY; ++i) ycol[i] = op.y_coff(c0 + ((tid + i * 256) % YV) * VEC) * (int)sizeof(T);
   V rx[PD][NX], ry[PD][NY];
+  // YCUR ops: the Y rows this thread stages, as cursors advanced by one chunk (BM * G rows) per
+  // fetch -- fetch(d, it) is called with it = 0, 1, 2, ... in order -- instead of y_roff's
+  // divisions per load (which the compiler put behind a branch each: 4 of them per chunk)
+  constexpr bool YC = wg_ycur<Op>::value;
+  typename WgYCur<Op>::type ycur[YC ? NY : 1];
+  int ym[YC ? NY : 1];
+  if constexpr (YC) {
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      ym[i] = m_beg + grp * BM + min(tid + i * 256, NYV - 1) / YV;
+      ycur[i] = op.ycur(ym[i]);
+    }
+  }
   // chunk `it` of this group -> ring slot d.  Offsets are computed for a clamped row and
   // replaced by OOB with a select afterwards (unsigned: OOB + a column offset stays out of
   // range), so no load sits behind a branch.
@@ -450,8 +469,17 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
     }
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
-      const int m = m0 + min(tid + i * 256, NYV - 1) / YV;
-      const uint32_t yr = m < m_end ? (uint32_t)(op.y_roff(min(m, m_end - 1)) * (int)sizeof(T)) : (uint32_t)OOB;
+      uint32_t yr;
+      if constexpr (YC) {
+        // rows past the split's end read as zero (OOB), whatever the cursor's offset
+        const uint32_t o = (uint32_t)(op.ycur_off(ycur[i]) * (int)sizeof(T));
+        yr = ym[i] < m_end ? o : (uint32_t)OOB;
+        ym[i] += BM * G;
+        op.template ycur_adv<BM * G>(ycur[i]);
+      } else {
+        const int m = m0 + min(tid + i * 256, NYV - 1) / YV;
+        yr = m < m_end ? (uint32_t)(op.y_roff(min(m, m_end - 1)) * (int)sizeof(T)) : (uint32_t)OOB;
+      }
       ry[d][i] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs_y, (int)(yr + (uint32_t)ycol[i]), 0, 0));
     }
   };

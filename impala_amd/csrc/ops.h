@@ -453,6 +453,20 @@ template <typename T> struct Conv3Wgrad {  // m = (n, oy, ox) in N*16; c = (kh*3
   }
   DEV int y_bytes() const { return (M / P3) * (H2 * H2 * OC2) * (int)sizeof(T); }
   DEV const T* ybase() const { return in; }
+  // row cursor (gemm_wg_body YCUR): (frame, pixel) of row m, advanced by a chunk stride without
+  // the divisions of y_roff (which the compiler also put behind a branch per staging load)
+  static constexpr bool YCUR = true;
+  struct YCur { int n, p; };
+  DEV YCur ycur(int m) const { const int n = m / P3; return YCur{n, m - n * P3}; }
+  template <int D> DEV void ycur_adv(YCur& c) const {
+    c.p += D % P3;
+    c.n += D / P3;
+    if (c.p >= P3) { c.p -= P3; c.n += 1; }
+  }
+  DEV int ycur_off(const YCur& c) const {
+    const int oy = c.p / H3, ox = c.p - oy * H3;
+    return ((c.n * H2 + oy) * H2 + ox) * OC2;
+  }
 };
 template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4+kw)*32 + ci
   static constexpr int R = OC2, C = K2;
@@ -471,6 +485,18 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
   }
   DEV int y_bytes() const { return (M / P2) * (H1 * H1 * OC1) * (int)sizeof(T); }
   DEV const T* ybase() const { return in; }
+  static constexpr bool YCUR = true;  // see Conv3Wgrad
+  struct YCur { int n, p; };
+  DEV YCur ycur(int m) const { const int n = m / P2; return YCur{n, m - n * P2}; }
+  template <int D> DEV void ycur_adv(YCur& c) const {
+    c.p += D % P2;
+    c.n += D / P2;
+    if (c.p >= P2) { c.p -= P2; c.n += 1; }
+  }
+  DEV int ycur_off(const YCur& c) const {
+    const int oy = c.p / H2, ox = c.p - oy * H2;
+    return ((c.n * H1 + ST2 * oy) * H1 + ST2 * ox) * OC1;
+  }
 };
 
 // FC weight gradient and FC input gradient in ONE launch.  Both read only dz (with y / Wfc), so
