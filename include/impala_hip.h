@@ -225,7 +225,11 @@ int impala_gather_rows(const void* const* src, void* const* dst, const size_t* r
 /* Host staging ring (SURVEY.md §8(b) impala_stage; replaces the 5·B pageable `.to(device)`
  * copies of learning.py:121-123).  The handle owns `nslots` device batch slots of B*T frames
  * and a non-blocking H2D stream:
- *   impala_stage_init     allocate the ring (1..8 slots; re-init frees the old ring)
+ *   impala_stage_init     allocate the ring (1..8 slots; re-init frees the old ring) and, for the
+ *                         SDMA copy path, prime it: the staging loop runs 24 rounds on a scratch
+ *                         page-locked batch, so the runtime's one-time SDMA-queue creations
+ *                         (6-9 ms host stalls inside hipMemcpyAsync) fall here and not into the
+ *                         first steps; ~50 ms (IMPALA_STAGE_PRIME=<rounds>, 0 = off)
  *   impala_stage          enqueue the H2D copies of one host batch (page-locked memory makes
  *                         them asynchronous; discounts may be NULL on PPO handles) into `slot`,
  *                         ordered after the last impala_slot_release of that slot
