@@ -334,16 +334,8 @@ class StepClock:
     def summary(self, digits=4):
         """-> per-step statistics in ms (call after the region's final synchronize)."""
         n = self.i - 1
-        ms = np.array([self.ev[i].elapsed_time(self.ev[i + 1]) for i in range(n)])
-        med = float(np.median(ms))
-        out = {"ms_per_step_median": round(med, digits),
-               "ms_per_step_min": round(float(ms.min()), digits),
-               "ms_per_step_max": round(float(ms.max()), digits),
-               "ms_per_step_p90": round(float(np.percentile(ms, 90)), digits),
-               "slow_steps": [int(i) for i in np.nonzero(ms > 2 * med)[0]],
-               "events_sum_ms": round(float(ms.sum()), digits)}
-        if n <= 256:
-            out["step_ms"] = [round(float(x), digits) for x in ms]
+        ms = [self.ev[i].elapsed_time(self.ev[i + 1]) for i in range(n)]
+        out = step_time_stats(ms, digits)
         if self.host:
             h = np.array(self.host) * 1e3
             out["host_ms_per_iter_median"] = round(float(np.median(h)), digits)
@@ -351,6 +343,23 @@ class StepClock:
             if len(h) <= 256:
                 out["host_ms"] = [round(float(x), digits) for x in h]
         return out
+
+
+def step_time_stats(ms, digits=4):
+    """Per-step statistics of a timed region's step times `ms` (milliseconds): median, min,
+    max, p90, the indices of steps over twice the median, their sum, and (<= 256 steps) the
+    steps themselves."""
+    ms = np.asarray(ms, dtype=np.float64)
+    med = float(np.median(ms))
+    out = {"ms_per_step_median": round(med, digits),
+           "ms_per_step_min": round(float(ms.min()), digits),
+           "ms_per_step_max": round(float(ms.max()), digits),
+           "ms_per_step_p90": round(float(np.percentile(ms, 90)), digits),
+           "slow_steps": [int(i) for i in np.nonzero(ms > 2 * med)[0]],
+           "events_sum_ms": round(float(ms.sum()), digits)}
+    if len(ms) <= 256:
+        out["step_ms"] = [round(float(x), digits) for x in ms]
+    return out
 
 
 def step_stats(clock, dist, dev):
@@ -361,13 +370,8 @@ def step_stats(clock, dist, dev):
         return s
     t = torch.tensor(s["step_ms"], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ms = t.cpu().numpy()
-    med = float(np.median(ms))
-    s.update({"ms_per_step_median": round(med, 4), "ms_per_step_max": round(float(ms.max()), 4),
-              "ms_per_step_min": round(float(ms.min()), 4),
-              "ms_per_step_p90": round(float(np.percentile(ms, 90)), 4),
-              "slow_steps": [int(i) for i in np.nonzero(ms > 2 * med)[0]],
-              "step_ms": [round(float(x), 4) for x in ms], "over_ranks": "max per step"})
+    s.update(step_time_stats(t.cpu().numpy()))
+    s["over_ranks"] = "max per step"
     return s
 
 

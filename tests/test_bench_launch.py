@@ -166,3 +166,16 @@ def test_settle_keeps_ranks_in_lockstep_over_gloo():
         p.join(60)
     (r0, n0, c0, m0), (r1, n1, c1, m1) = res
     assert n0 == n1 == c0 == c1 == m0 == m1 and n0 >= 10 and n0 % 10 == 0
+
+
+def test_step_time_stats_finds_the_stall():
+    """The per-step statistics bench.py reports beside `value` (the median step):
+    one 7.3 ms step among 0.3 ms steps -- the host-staged stall of the r04 driver record --
+    is its max and its only slow step, and leaves the median alone."""
+    ms = [0.30] * 20
+    ms[2] = 7.3
+    s = bench.step_time_stats(ms)
+    assert s["ms_per_step_median"] == 0.3 and s["ms_per_step_max"] == 7.3
+    assert s["slow_steps"] == [2] and len(s["step_ms"]) == 20
+    assert abs(s["events_sum_ms"] - (19 * 0.3 + 7.3)) < 1e-9
+    assert "step_ms" not in bench.step_time_stats([1.0] * 300)
