@@ -408,7 +408,10 @@ DEV void gemm_wg_body(const Op& op, float* __restrict__ slab, float* __restrict_
   static_assert(TRW >= 1 && TCW >= 1 && BR % 16 == 0 && BC % 16 == 0, "tile");
   static_assert(BM % F::KSTEP == 0, "chunk");
   static_assert(PD >= 1, "prefetch depth");
-  static_assert((size_t)STAGE * 2 * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float),
+  // the LDS is reused for the fixed-order group reduction (G > 1) and the bias / sum-of-squares
+  // combines (256 floats)
+  static_assert((G == 1 || (size_t)STAGE * 2 * G * sizeof(T) >= (size_t)256 * (NACC + 1) * sizeof(float)) &&
+                    (size_t)STAGE * 2 * G * sizeof(T) >= 256 * sizeof(float),
                 "LDS reuse for the group reduction");
   static_assert(STAGE * 2 * G == gemm_wg_smem<T, BR, BC, BM, G>(), "LDS size");
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
