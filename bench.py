@@ -792,7 +792,9 @@ def main():
     clock = StepClock(args.steps)
     elapsed, _ = timed_steps(eng, step, [], args, dist, dev, clock)  # the headline: no kernel stamps
     steps_stat = step_stats(clock, dist, dev)
-    elapsed_nomark, _ = timed_steps(eng, step, [], args, dist, dev)
+    # the stamped run for the roofline kernels' live durations, after its own settle: the
+    # regions 5-10 ms after a settle ends run 5-7 % slow (tools/region_order.py, profiles/r05host)
+    settle(step, args.settle_ms, dist, dev)
     elapsed_st, k_times = timed_steps(eng, step, top, args, dist, dev)
     met = eng.metrics.cpu().numpy()
     if not np.all(np.isfinite(met)):
@@ -828,7 +830,8 @@ def main():
         "kernel_us": kernel_us,
         **steps_stat,
         "value_at_median": round(world * B * T / (steps_stat["ms_per_step_median"] * 1e-3), 1),
-        "ms_per_step_unmarked": round(elapsed_nomark * 1e3 / args.steps, 4),
+        "step_events": "a timing event before every step of the headline region (StepClock); "
+                       "they cost about 1.4 % against unmarked steps (tools/region_order.py)",
         "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
         "settle": {"min_ms": args.settle_ms, "steps": settled},
     }
@@ -1103,6 +1106,7 @@ def alt_line(dtype, args, B, T, A, dev, dist, world, make_step, ppo):
     clock = StepClock(args.steps)
     elapsed, _ = timed_steps(e, step, [], args, dist, dev, clock)
     st = step_stats(clock, dist, dev)
+    settle(step, args.settle_ms, dist, dev)
     elapsed_st, k_times = timed_steps(e, step, top[:1], args, dist, dev)
     value = world * B * T * args.steps / elapsed
     out = {"dtype": dtype, "value": round(value, 1), "unit": "env-frames/s",
