@@ -92,6 +92,10 @@ class ReplayBuffer:
 class DeviceReplayBuffer(ReplayBuffer):
     """HBM-resident circular rollout store with pinned-host staging (see module doc)."""
 
+    # the most entries the page-locked index ring grows to (_indices_to_device) before sample()
+    # waits for the oldest one's copy
+    _IDX_RING_MAX = 64
+
     def __init__(self, capacity: int = 1000, rollout_length: int = 20, num_actions: int = 15,
                  device="cuda", seed: Optional[int] = None, staging_slots: int = 64):
         super().__init__(capacity, seed)
@@ -119,9 +123,8 @@ class DeviceReplayBuffer(ReplayBuffer):
         self._last_read: Optional[torch.cuda.Event] = None
         # page-locked ring for the sampled slot indices: their H2D is a true asynchronous copy
         # (from pageable memory it would wait behind the learner stream's queued work while
-        # sample() holds the lock); a ring entry is reused after its copy has run
-        # page-locked index ring (_indices_to_device): starts at 4 entries, grows when the
-        # learner's stream runs further ahead than that
+        # sample() holds the lock); a ring entry is reused after its copy has run.  It starts
+        # at 4 entries and grows when the learner's stream runs further ahead than that
         self._idx_buf: List[Optional[torch.Tensor]] = [None] * 4
         self._idx_ev: List[Optional[torch.cuda.Event]] = [None] * 4
         self._idx_next = 0

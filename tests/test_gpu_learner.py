@@ -291,6 +291,35 @@ def test_device_replay_overwrite_waits_for_queued_gather():
         np.testing.assert_array_equal(batch[4][j].cpu().numpy(), old[k][4].numpy())
 
 
+def test_device_replay_index_ring_grows_instead_of_waiting():
+    """sample() holds the replay lock, so it must never wait on the device for its
+    page-locked index ring.  With the learner stream blocked behind queued work, ten samples in
+    a row find the 4-entry ring's next entry still queued: the ring grows (no host wait) and
+    every sample still gathers the rows its keys name."""
+    dev = _dev()
+    from impala_amd.replay import DeviceReplayBuffer
+    T, A = 4, 3
+    rb = DeviceReplayBuffer(capacity=8, rollout_length=T, num_actions=A, device=dev, seed=2)
+    for k in range(8):  # every field of trajectory k holds k
+        rb.append([torch.full((T, 3, 64, 64), k, dtype=torch.uint8), torch.full((T, 1), k),
+                   torch.full((T, 1), float(k)), torch.full((T, 1), float(k)),
+                   torch.full((T, A), float(k))])
+    torch.cuda.synchronize()
+    busy = torch.randn(4096, 4096, device=dev)
+    for _ in range(16):  # a few ms of queued work on the learner (current) stream
+        busy = busy @ busy
+        busy = busy / busy.norm()
+    out = [rb.sample(4) for _ in range(10)]
+    grown = len(rb._idx_buf)
+    torch.cuda.synchronize()
+    assert grown > 4, "the index ring did not grow while the stream was busy"
+    assert grown <= rb._IDX_RING_MAX
+    for keys, batch, _ in out:
+        for j, k in enumerate(keys.tolist()):
+            assert int(batch[0][j].float().mean().item()) == k
+            assert float(batch[4][j].mean().item()) == float(k)
+
+
 def test_device_replay_append_during_sample_threaded():
     """appends racing sample() from another thread never tear a trajectory.  Every
     field of trajectory k encodes k, a capacity-8 ring is overwritten continuously by a writer
