@@ -383,8 +383,12 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   // ---- dgrad chain on `st`; each weight-gradient branch forks onto the side stream as soon
   // as its inputs exist and joins before the slab reduction ----
   // gemm_wg: 32-row m-chunks, several 4-wave groups per workgroup on interleaved chunks (more
-  // chunk loads in flight per CU); fp32 (parity mode) keeps one group for its LDS budget
-  constexpr int WG4 = sizeof(T) == 2 ? 4 : 1, WG2 = sizeof(T) == 2 ? 2 : 1;
+  // chunk loads in flight per CU); fp32 keeps one group for its LDS budget.  The bf16 conv
+  // weight gradients run 2 groups (56 KB of LDS: two workgroups per CU) rather than 4 (112 KB:
+  // one, so the merged launch's 508 workgroups ran in two rounds): 17.1 -> 14.0 us, step 0.1029
+  // -> 0.1000 ms (tools/var_specs/bfg.py, profiles/r05bg).  The bf16 FC weight gradient keeps 2
+  // (one group: 8.2 -> 8.9 us).
+  constexpr int WG4 = sizeof(T) == 2 ? 2 : 1, WG2 = sizeof(T) == 2 ? 2 : 1;
   hipStream_t ss = h->use_side ? h->side : st;
   auto fork = [&](int i) -> int {
     if (!h->use_side) return 0;
