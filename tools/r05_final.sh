@@ -4,7 +4,7 @@
 # of the fp32 and bf16 steps (tools/profile.sh).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05final
+O=gpurun_out/${OTAG:-r05final}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
