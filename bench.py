@@ -311,31 +311,36 @@ def _cpu_baseline(ref_cpu, B, T, A, seconds, warmup):
 
 class StepClock:
     """Per-step device times of a timed region (SURVEY.md §8(d) defines the metric on the
-    median step): a timing event recorded on the launch stream before every step and one after
-    the last, read once the region has ended (no host sync inside it).  Step i's time is
-    event i -> event i+1, so the steps tile the region's device time with no gaps.  Optionally
-    the host's own per-iteration times (enqueue + any host wait inside the loop body)."""
+    median step), from the library's device step clock (Engine.step_clock_*): the first kernel
+    of every step stamps the device's 100 MHz clock as it starts, and one 1-thread kernel after
+    the last step closes the region, so the steps tile the region's device time with no gaps
+    and nothing is enqueued between them (a timing event per step cost the fp32 step ~1.4 %:
+    tools/region_order.py, profiles/r05host).  Optionally the host's own per-iteration times
+    (enqueue + any host wait inside the loop body)."""
 
-    def __init__(self, n, host=False):
-        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    def __init__(self, eng, n, host=False):
+        self.eng, self.n = eng, n
         self.host = [] if host else None
-        self.i = 0
         self._t = None
+        eng.step_clock_start(n)
 
     def mark(self):
-        self.ev[self.i].record()
-        self.i += 1
+        """Before every step and after the last (host times only)."""
         if self.host is not None:
             t = time.perf_counter()
             if self._t is not None:
                 self.host.append(t - self._t)
             self._t = t
 
+    def close(self):
+        """After the last step, inside the timed region: the closing stamp."""
+        self.eng.step_clock_end()
+
     def summary(self, digits=4):
         """-> per-step statistics in ms (call after the region's final synchronize)."""
-        n = self.i - 1
-        ms = [self.ev[i].elapsed_time(self.ev[i + 1]) for i in range(n)]
+        ms = self.eng.step_clock_read()
         out = step_time_stats(ms, digits)
+        out["step_clock"] = "device: the step's first kernel stamps s_memrealtime (100 MHz)"
         if self.host:
             h = np.array(self.host) * 1e3
             out["host_ms_per_iter_median"] = round(float(np.median(h)), digits)
@@ -356,7 +361,7 @@ def step_time_stats(ms, digits=4):
            "ms_per_step_max": round(float(ms.max()), digits),
            "ms_per_step_p90": round(float(np.percentile(ms, 90)), digits),
            "slow_steps": [int(i) for i in np.nonzero(ms > 2 * med)[0]],
-           "events_sum_ms": round(float(ms.sum()), digits)}
+           "steps_sum_ms": round(float(ms.sum()), digits)}
     if len(ms) <= 256:
         out["step_ms"] = [round(float(x), digits) for x in ms]
     return out
@@ -408,14 +413,15 @@ def run_host_staged(eng, batch, args, dist, model, world):
             eng.slot_release(s)
         if clock is not None:
             clock.mark()
+            clock.close()
 
     run(max(args.warmup, 2))
     torch.cuda.synchronize()
     settled = settle(lambda: run(1), args.settle_ms, dist, model.flat.device)
+    clock = StepClock(eng, args.steps, host=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    clock = StepClock(args.steps, host=True)
     t0 = time.perf_counter()
     run(args.steps, clock)
     torch.cuda.synchronize()
@@ -789,7 +795,7 @@ def main():
     work = kernel_work(2 if args.dtype == "bf16" else 4)
     kernel_us, top = select_kernels(eng, step, work, args)
     settled = settle(step, args.settle_ms, dist, dev)
-    clock = StepClock(args.steps)
+    clock = StepClock(eng, args.steps)
     elapsed, _ = timed_steps(eng, step, [], args, dist, dev, clock)  # the headline: no kernel stamps
     steps_stat = step_stats(clock, dist, dev)
     # the stamped run for the roofline kernels' live durations, after its own settle: the
@@ -830,8 +836,8 @@ def main():
         "kernel_us": kernel_us,
         **steps_stat,
         "value_at_median": round(world * B * T / (steps_stat["ms_per_step_median"] * 1e-3), 1),
-        "step_events": "a timing event before every step of the headline region (StepClock); "
-                       "they cost about 1.4 % against unmarked steps (tools/region_order.py)",
+        "step_times": "device step clock (StepClock): each step's first kernel stamps the "
+                      "device clock; no event or marker between the headline region's steps",
         "ms_per_step_stamped": round(elapsed_st * 1e3 / args.steps, 4),
         "settle": {"min_ms": args.settle_ms, "steps": settled},
     }
@@ -986,7 +992,7 @@ def select_kernels(eng, step, work, args):
 def timed_steps(eng, step, kernels, args, dist, dev, clock=None):
     """The timed region: --steps steps between barriers + device syncs; the given kernels' own
     durations are stamped live (hipExtLaunchKernel events on their launch stream).  With a
-    StepClock, a timing event is recorded before every step and after the last."""
+    StepClock (armed before the region), its closing stamp is enqueued after the last step."""
     for k in kernels:
         eng.timer_start(k, args.steps)
     if dist is not None:
@@ -1001,6 +1007,7 @@ def timed_steps(eng, step, kernels, args, dist, dev, clock=None):
             clock.mark()
             step()
         clock.mark()
+        clock.close()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -1103,7 +1110,7 @@ def alt_line(dtype, args, B, T, A, dev, dist, world, make_step, ppo):
     table, top = select_kernels(e, step, work, argparse.Namespace(steps=args.steps,
                                                                    roofline_kernel=None))
     settled = settle(step, args.settle_ms, dist, dev)
-    clock = StepClock(args.steps)
+    clock = StepClock(e, args.steps)
     elapsed, _ = timed_steps(e, step, [], args, dist, dev, clock)
     st = step_stats(clock, dist, dev)
     settle(step, args.settle_ms, dist, dev)

@@ -59,7 +59,7 @@ EXPORTS = (
     "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
     "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
     "impala_timer_read_kernel", "impala_dp_unique_id", "impala_dp_init", "impala_dp_train_step",
-    "impala_dp_nranks",
+    "impala_dp_nranks", "impala_step_clock", "impala_step_clock_end",
 )
 # every symbol declared in include/sac_hip.h
 SAC_EXPORTS = (
@@ -173,6 +173,8 @@ def _declare(lib):
     lib.impala_timer_start.argtypes = [_P, C.c_int, C.c_int]
     lib.impala_timer_read.argtypes = [_P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     lib.impala_timer_read_kernel.argtypes = [_P, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    lib.impala_step_clock.argtypes = [_P, _P, C.c_int]
+    lib.impala_step_clock_end.argtypes = [_P, _P, C.POINTER(C.c_int)]
     for name in EXPORTS:
         if name not in ("impala_last_error", "impala_param_count", "impala_kernel_name",
                         "impala_grad_bucket_offset", "impala_grad_bucket_offset_fc"):

@@ -755,8 +755,13 @@ template <typename T>
 __global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
     const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
     const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
-    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3) {
+    uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3,
+    unsigned long long* __restrict__ step_stamp) {
   __shared__ __attribute__((aligned(16))) T smem[C12FLds<T>::ELEMS];
+  // the device step clock (impala_step_clock): the learner step's first kernel stamps the
+  // constant 100 MHz clock as its first workgroup starts (one vector store; nullptr = off)
+  if (step_stamp != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    *step_stamp = __builtin_amdgcn_s_memrealtime();
   conv12_fwd_body<T>(x, w1, b1, w2, b2, act1, mask, act2, N, fpw, c3, (int)blockIdx.x, smem);
 }
 

@@ -180,6 +180,9 @@ struct impala_learner {
   };
   KTimer timers[K_COUNT];
   int timers_armed = 0, timer_last = -1;
+  // device step clock (impala_step_clock): stamps[clock_i] by the next step's first kernel
+  unsigned long long* clock_buf = nullptr;
+  int clock_n = 0, clock_i = 0;
   // hipGraph replay of whole steps: the launch sequence of a step is captured once per batch
   // address set (on a private capture stream) and replayed with one hipGraphLaunch
   struct GraphSlot {
@@ -253,6 +256,11 @@ int klaunch(impala_learner* h, int kid, const char* name, void (*kernel)(KArgs..
 
 namespace {
 
+// the device step clock's slot for the step being enqueued (nullptr: not armed / full)
+unsigned long long* step_stamp(impala_learner* h) {
+  return h->clock_buf && h->clock_i < h->clock_n ? h->clock_buf + h->clock_i++ : nullptr;
+}
+
 template <typename T>
 int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
                    bool with_heads) {
@@ -298,9 +306,13 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     if (int r = klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>,
                         dim3(cdiv(n, fpw)), dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1,
                         vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
-                        (T*)h->act2, n, fpw, c3))
+                        (T*)h->act2, n, fpw, c3, with_heads ? nullptr : step_stamp(h)))
       return r;
   } else {
+    if (!with_heads)  // the unfused forward (IMPALA_FWD_FUSED=0): the clock gets a stamp launch
+      if (unsigned long long* ss = step_stamp(h))
+        if (int r = klaunch(h, -1, "clock_stamp", clock_stamp_kernel, dim3(1), dim3(64), st, ss))
+          return r;
     if (int r = klaunch(h, K_CONV1_FWD, "conv1_fwd", conv1_fwd_s2d<T>, dim3(min(n, h->n_cu * 4)),
                         dim3(256), st, obs, sw + sh.w1, vv + Vecs::b1, (T*)h->act1, h->mask1, n))
       return r;
@@ -1180,7 +1192,7 @@ bool same_batch(const impala_batch& a, const impala_batch& b) {
 // (its events must be recorded per launch) or IMPALA_GRAPH=0 the launches go straight to `st`.
 template <class Body>
 int run_graphed(impala_learner* h, int kind, const impala_batch* b, hipStream_t st, Body&& body) {
-  if (!h->use_graph || h->timers_armed > 0) return body(st);
+  if (!h->use_graph || h->timers_armed > 0 || h->clock_buf) return body(st);
   const impala_batch key = b ? *b : impala_batch{};
   for (auto& g : h->graphs)
     if (g.exec && g.kind == kind && same_batch(g.key, key)) {
@@ -1661,6 +1673,29 @@ int impala_timer_read_kernel(impala_learner* h, int kernel_id, float* total_ms, 
   if (t.armed) h->timers_armed--;
   t.armed = false;
   t.n = 0;
+  return 0;
+}
+
+int impala_step_clock(impala_learner* h, unsigned long long* stamps, int n) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (n < 0 || (n > 0 && !stamps)) return fail(IMPALA_E_INVALID, "bad step clock buffer / count");
+  h->clock_buf = n > 0 ? stamps : nullptr;
+  h->clock_n = n;
+  h->clock_i = 0;
+  return 0;
+}
+
+int impala_step_clock_end(impala_learner* h, void* stream, int* steps) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (!h->clock_buf) return fail(IMPALA_E_STATE, "step clock not armed");
+  CK(hipSetDevice(h->device));
+  unsigned long long* out = h->clock_buf + h->clock_i;
+  if (steps) *steps = h->clock_i;
+  h->clock_buf = nullptr;
+  h->clock_n = h->clock_i = 0;
+  if (int r = klaunch(h, -1, "clock_stamp", clock_stamp_kernel, dim3(1), dim3(64),
+                      (hipStream_t)stream, out))
+    return r;
   return 0;
 }
 

@@ -1185,6 +1185,11 @@ __global__ __launch_bounds__(64) void stage_prime_spin_kernel(long long ticks) {
   }
 }
 
+// the device step clock's closing stamp (impala_step_clock_end): one thread, one vector store
+__global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* __restrict__ out) {
+  if (threadIdx.x == 0) *out = __builtin_amdgcn_s_memrealtime();
+}
+
 __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   const int i = blockIdx.x, f = blockIdx.y;
   if (i >= a.n || f >= a.nfields) return;

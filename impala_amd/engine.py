@@ -355,6 +355,28 @@ class Engine:
                   "impala_timer_read_kernel")
         return float(ms.value), int(n.value)
 
+    # ------------------------------------------------------------------ device step clock
+    def step_clock_start(self, n: int):
+        """Arm the device step clock for the next `n` steps: each step's first kernel stamps
+        the device's 100 MHz clock as it starts (impala_step_clock); nothing is enqueued
+        between the steps."""
+        self._clock = torch.zeros(int(n) + 1, dtype=torch.int64, device=self.device)
+        check(_lib.lib().impala_step_clock(self._h, ptr(self._clock), int(n)), "impala_step_clock")
+
+    def step_clock_end(self, stream=None):
+        """Enqueue the stamp that closes the last armed step (a 1-thread kernel on `stream`)
+        and disarm; no host sync."""
+        k = C.c_int()
+        check(_lib.lib().impala_step_clock_end(self._h, stream_ptr(stream), C.byref(k)),
+              "impala_step_clock_end")
+        self._clock_steps = k.value
+
+    def step_clock_read(self):
+        """-> the per-step device times in ms of the last clocked region (a host sync)."""
+        st = self._clock[: self._clock_steps + 1].cpu().tolist()
+        self._clock = None
+        return [(b - a) * 1e-5 for a, b in zip(st, st[1:])]  # 10 ns ticks -> ms
+
     def _updated(self):
         # the Adam kernel rewrote params AND this handle's kernel-layout weights
         self.model._version += 1

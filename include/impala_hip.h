@@ -263,6 +263,18 @@ int impala_timer_start(impala_learner* h, int kernel_id, int max_launches);
 int impala_timer_read(impala_learner* h, float* total_ms, int* launches);
 int impala_timer_read_kernel(impala_learner* h, int kernel_id, float* total_ms, int* launches);
 
+/* Device step clock (bench): the first kernel of each of the next `n` learner steps (train,
+ * data-parallel and PPO steps; not impala_act) stamps the device's constant 100 MHz clock
+ * (s_memrealtime) as its first workgroup starts, into stamps[0 .. n-1] (a device buffer of
+ * n + 1 uint64).  impala_step_clock_end enqueues one 1-thread kernel on `stream` that stamps
+ * the slot after the last stamped step (stamps[*steps], *steps = the steps stamped, <= n)
+ * once that step has finished, and disarms.  Step i took stamps[i+1] - stamps[i]
+ * ticks of 10 ns.  Unlike a timing event per step, nothing is enqueued between the steps (an
+ * event or marker per step costs the fp32 step ~1.4 %, tools/region_order.py).  Steps run
+ * without graph replay while the clock is armed.  n = 0 disarms without stamping. */
+int impala_step_clock(impala_learner* h, unsigned long long* stamps, int n);
+int impala_step_clock_end(impala_learner* h, void* stream, int* steps);
+
 /* Standalone batched V-trace, [B][L] row-major, L <= 64 (test / reuse entry point). */
 int impala_vtrace(const float* v_tm1, const float* v_t, const float* r_t, const float* discount_t,
                   const float* rho_tm1, int B, int L, float lambda_, float clip_rho_threshold,

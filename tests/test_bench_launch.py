@@ -177,5 +177,5 @@ def test_step_time_stats_finds_the_stall():
     s = bench.step_time_stats(ms)
     assert s["ms_per_step_median"] == 0.3 and s["ms_per_step_max"] == 7.3
     assert s["slow_steps"] == [2] and len(s["step_ms"]) == 20
-    assert abs(s["events_sum_ms"] - (19 * 0.3 + 7.3)) < 1e-9
+    assert abs(s["steps_sum_ms"] - (19 * 0.3 + 7.3)) < 1e-9
     assert "step_ms" not in bench.step_time_stats([1.0] * 300)

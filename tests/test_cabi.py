@@ -83,3 +83,6 @@ def test_kernel_entry_points_validate_before_launch():
     assert lib.impala_slot_batch(None, 0, None, None) == 1001
     assert lib.impala_slot_release(None, 0, None) == 1001
     assert lib.impala_act(None, None, 1, None, 0, 0, 0, None, None, None, None) == 1001
+    # device step clock: a null handle is refused before any HIP call
+    assert lib.impala_step_clock(None, None, 3) == 1001
+    assert lib.impala_step_clock_end(None, None, None) == 1001

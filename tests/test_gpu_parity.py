@@ -287,6 +287,38 @@ def test_train_step_deterministic(dtype):
     np.testing.assert_array_equal(flats[0][1], flats[1][1])
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_step_clock(dtype):
+    """The device step clock (impala_step_clock): clocked steps are bitwise the unclocked ones,
+    every step gets a positive interval, the intervals tile the region (their sum is within the
+    wall time of the synced region), and a full clock ignores extra steps."""
+    import time
+    dev = _dev()
+    batch = [_t(x, dev) for x in ref_cpu.synthetic_batch(8, 20, 15, seed=5)]
+    flats = []
+    for clocked in (False, True):
+        m = _model(dev, dtype, seed=0)
+        e = _engine(m, 8, 20)
+        e.train_step(*batch)
+        torch.cuda.synchronize()
+        if clocked:
+            e.step_clock_start(3)
+        t0 = time.perf_counter()
+        for _ in range(4):  # one step past the clock's capacity
+            e.train_step(*batch)
+        if clocked:
+            e.step_clock_end()
+        torch.cuda.synchronize()
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        if clocked:
+            ms = e.step_clock_read()
+            assert len(ms) == 3 and all(0 < x < wall_ms for x in ms), (ms, wall_ms)
+            assert sum(ms) < wall_ms
+        flats.append((m.flat.cpu().numpy().copy(), e.metrics.cpu().numpy().copy()))
+    np.testing.assert_array_equal(flats[0][0], flats[1][0])
+    np.testing.assert_array_equal(flats[0][1], flats[1][1])
+
+
 @pytest.mark.parametrize("var", ["IMPALA_FC_SPLITK", "IMPALA_FWD_CHAIN", "IMPALA_FUSED_UPDATE",
                                  "IMPALA_EARLY_RED"])
 def test_product_library_refuses_ab_variants(var, monkeypatch):

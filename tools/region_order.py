@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Short timed regions after bench.py's settle: are 20-step regions with a timing event per step
-faster than unmarked ones, or does the order (time since the settle) decide?  (r05final: the
-marked headline ran 0.2360 ms/step and the unmarked run right after it 0.2536.)  Settle 250 ms,
-then alternating marked / unmarked 20-step regions, each bracketed by device syncs.
+"""Short timed regions after bench.py's settle, three kinds in rotation: a timing event per step
+(the round-5 StepClock), the device step clock (each step's first kernel stamps the device
+clock; bench.py's StepClock now), and unmarked.  Which instrumentation costs step time, and
+does the order (time since the settle) decide?  (r05final: the event-marked headline ran
+0.2360 ms/step and the unmarked run right after it 0.2536.)  Settle 250 ms, then 9 regions of
+`steps` steps, each bracketed by device syncs.
 
 usage: python tools/region_order.py [fp32|bf16] [steps]"""
 import os
@@ -34,21 +36,27 @@ for _ in range(5):
 torch.cuda.synchronize()
 n = bench.settle(step, 250.0)
 print(f"[{dtype}] settle {n} steps", flush=True)
-for r in range(8):
-    marked = r % 2 == 0
-    clock = bench.StepClock(steps) if marked else None
+for r in range(9):
+    kind = ("events", "device", "none")[r % 3]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if kind == "events" else None
+    clock = bench.StepClock(e, steps) if kind == "device" else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        if clock:
-            clock.mark()
+    for i in range(steps):
+        if ev:
+            ev[i].record()
         step()
+    if ev:
+        ev[steps].record()
     if clock:
-        clock.mark()
+        clock.close()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / steps
     extra = ""
-    if clock:
-        s = clock.summary()
+    if ev:
+        s = bench.step_time_stats([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])
         extra = f" median {s['ms_per_step_median']} first {s['step_ms'][0]}"
-    print(f"  region {r} {'marked  ' if marked else 'unmarked'} {ms:.4f} ms/step{extra}", flush=True)
+    elif clock:
+        s = clock.summary()
+        extra = f" median {s['ms_per_step_median']} first {s['step_ms'][0]} sum {s['steps_sum_ms']}"
+    print(f"  region {r} {kind:7s} {ms:.4f} ms/step{extra}", flush=True)
