@@ -648,7 +648,9 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.inv_world = 1.f / (float)h->cfg.world_size;
   aa.sp = ShadowPtrs{h->shadow, h->vecs, h->A};
   aa.cn = h->cn; aa.sh = h->sh;
-  return klaunch(h, K_ADAM, "adam", adam_kernel<T>, dim3(cdiv((long)(h->cn.total + 3) / 4, 256)),
+  // HID blocks for the FC weight rows, then the other parameters (adam_kernel)
+  const long rest = (long)h->cn.total - (long)(h->cn.bfc - h->cn.wfc);
+  return klaunch(h, K_ADAM, "adam", adam_kernel<T>, dim3(net::HID + cdiv((rest + 3) / 4, 256)),
                  dim3(256), st, aa);
 }
 

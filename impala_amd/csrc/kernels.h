@@ -845,14 +845,28 @@ DEV void adam_elem(const AdamArgs& a, float gscale, float step_size, float bc2s,
 }
 
 // clip + Adam on 4 consecutive parameters per thread; re-emits the kernel-layout weights.
-// (A row-wise variant that re-emits the big matrices through an LDS permutation with 16-byte
-// stores measured no faster: the scattered 2-byte shadow stores are absorbed by L2.)
+// Blocks [0, HID) each own one row o of the FC weight (canonical [wfc + o*FLAT, +FLAT): 64% of
+// the parameters) and re-emit its kernel-layout row (jj = p*64 + c for canonical j = c*16 + p)
+// through LDS as one 16-byte (fp32) / 8-byte (bf16) store per thread: the per-element
+// scattered stores of write_shadow cost the step ~3 us (tools/var_specs/adamko.py,
+// profiles/r05tail).  Blocks [HID, ..) take the other parameters, 4 per thread in canonical
+// order with the FC rows skipped (the segment starts and ends on a multiple of 4).
+static_assert((OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT) % 4 == 0,
+              "adam_kernel: the FC weight rows start float4-aligned in the canonical buffer");
 template <typename T>
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   __shared__ float red[4];
+  __shared__ __attribute__((aligned(16))) T fcrow[FLAT];
   // this thread's 4 parameters, the step scalars and the norm partials are all loaded up
   // front (one memory round trip), then one barrier combines the norm
-  const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const bool fc = blockIdx.x < HID;
+  size_t i0;
+  if (fc) {
+    i0 = a.cn.wfc + (size_t)blockIdx.x * FLAT + threadIdx.x * 4;
+  } else {
+    const size_t e = ((size_t)(blockIdx.x - HID) * 256 + threadIdx.x) * 4;
+    i0 = e < a.cn.wfc ? e : e + (a.cn.bfc - a.cn.wfc);
+  }
   const int n = i0 < a.cn.total ? (int)min((size_t)4, a.cn.total - i0) : 0;
   float g[4], m[4], v[4], p[4];
   if (n == 4) {
@@ -892,7 +906,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     a.metrics[6] = norm;
     a.metrics[7] = (float)step;
   }
-  if (n == 0) return;
+  if (n == 0) return;  // (never an FC block: those are full)
   const float gscale = a.inv_world * coef;
 #pragma unroll
   for (int k = 0; k < 4; ++k) adam_elem(a, gscale, step_size, bc2s, g[k], m[k], v[k], p[k]);
@@ -906,7 +920,22 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
       a.grads[i0 + k] = g[k]; a.m[i0 + k] = m[k]; a.v[i0 + k] = v[k]; a.params[i0 + k] = p[k];
     }
   }
-  for (int k = 0; k < n; ++k) write_shadow<T>(a.sp, a.cn, a.sh, i0 + k, p[k]);
+  if (fc) {
+    // canonical j = 4 tid + k = c*16 + q  ->  kernel-layout jj = q*64 + c (write_shadow's RK_FC)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = 4 * (int)threadIdx.x + k;
+      fcrow[(j & 15) * OC3 + (j >> 4)] = (T)p[k];
+    }
+    __syncthreads();
+    T* w = reinterpret_cast<T*>(a.sp.base) + a.sh.wfc + (size_t)blockIdx.x * FLAT + 4 * threadIdx.x;
+    if constexpr (sizeof(T) == 4)
+      *reinterpret_cast<f32x4*>(w) = *reinterpret_cast<const f32x4*>(fcrow + 4 * threadIdx.x);
+    else
+      *reinterpret_cast<uint2*>(w) = *reinterpret_cast<const uint2*>(fcrow + 4 * threadIdx.x);
+  } else {
+    for (int k = 0; k < n; ++k) write_shadow<T>(a.sp, a.cn, a.sh, i0 + k, p[k]);
+  }
 }
 
 // =========================================================================================
