@@ -650,7 +650,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   aa.cn = h->cn; aa.sh = h->sh;
   // HID blocks for the FC weight rows, then the other parameters (adam_kernel)
   const long rest = (long)h->cn.total - (long)(h->cn.bfc - h->cn.wfc);
-  return klaunch(h, K_ADAM, "adam", adam_kernel<T>, dim3(net::HID + cdiv((rest + 3) / 4, 256)),
+  return klaunch(h, K_ADAM, "adam", adam_kernel<T>, dim3(net::HID + cdiv(rest, 256)),
                  dim3(256), st, aa);
 }
 

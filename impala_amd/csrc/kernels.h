@@ -849,8 +849,8 @@ DEV void adam_elem(const AdamArgs& a, float gscale, float step_size, float bc2s,
 // the parameters) and re-emit its kernel-layout row (jj = p*64 + c for canonical j = c*16 + p)
 // through LDS as one 16-byte (fp32) / 8-byte (bf16) store per thread: the per-element
 // scattered stores of write_shadow cost the step ~3 us (tools/var_specs/adamko.py,
-// profiles/r05tail).  Blocks [HID, ..) take the other parameters, 4 per thread in canonical
-// order with the FC rows skipped (the segment starts and ends on a multiple of 4).
+// profiles/r05tail).  Blocks [HID, ..) take the other parameters, one per thread in canonical
+// order with the FC rows skipped.
 static_assert((OC1 * K1 + OC1 + OC2 * K2 + OC2 + OC3 * K3 + OC3 + 2 * FLAT) % 4 == 0,
               "adam_kernel: the FC weight rows start float4-aligned in the canonical buffer");
 template <typename T>
@@ -863,11 +863,12 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   size_t i0;
   if (fc) {
     i0 = a.cn.wfc + (size_t)blockIdx.x * FLAT + threadIdx.x * 4;
-  } else {
-    const size_t e = ((size_t)(blockIdx.x - HID) * 256 + threadIdx.x) * 4;
+  } else {  // one parameter per thread: the scattered shadow stores of write_shadow (two per
+            // conv2 / conv3 weight in fp32) spread over 4x the waves (profiles/r05tail)
+    const size_t e = (size_t)(blockIdx.x - HID) * 256 + threadIdx.x;
     i0 = e < a.cn.wfc ? e : e + (a.cn.bfc - a.cn.wfc);
   }
-  const int n = i0 < a.cn.total ? (int)min((size_t)4, a.cn.total - i0) : 0;
+  const int n = i0 < a.cn.total ? (fc ? 4 : 1) : 0;
   float g[4], m[4], v[4], p[4];
   if (n == 4) {
     const f32x4 G = *reinterpret_cast<const f32x4*>(a.grads + i0);

@@ -282,3 +282,31 @@ def test_distributed_agent_train_returns_total_samples():
     assert ev.dict()["episode_length"]["mean"] == 200
     # without a controller: the frames the learner consumed
     assert DistributedAgent(None, _Learner(), w).train(5) == 5 * 160
+
+
+@pytest.mark.parametrize("A", [1, 2, 6, 9, 15])
+def test_adam_block_partition_covers_every_parameter_once(A):
+    """adam_kernel's block map (kernels.h: HID blocks of one FC weight row each, 4 parameters per
+    thread, then one parameter per thread over [0, wfc) ++ [bfc, total)) restated on the host:
+    every canonical parameter is updated by exactly one thread, the FC rows start float4-aligned,
+    and the grid impala.hip launches (HID + cdiv(rest, 256)) is exactly enough."""
+    specs = param_specs(A)
+    sizes = [int(np.prod(s)) for _, s in specs]
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    seg = {n: (int(offs[i]), int(offs[i + 1])) for i, (n, _) in enumerate(specs)}
+    total = int(offs[-1])
+    wfc, bfc = seg["model.projection.1.weight"]
+    HID, FLAT = 256, 1024
+    assert bfc - wfc == HID * FLAT
+    hits = np.zeros(total, np.int32)
+    for o in range(HID):  # FC rows: thread t takes 4 t .. 4 t + 3
+        c0 = wfc + o * FLAT
+        assert c0 % 4 == 0
+        for t in range(256):
+            hits[c0 + 4 * t:c0 + 4 * t + 4] += 1
+    rest = total - (bfc - wfc)
+    for e in range(-(-rest // 256) * 256):  # the generic blocks
+        i = e if e < wfc else e + (bfc - wfc)
+        if i < total:
+            hits[i] += 1
+    assert (hits == 1).all(), np.nonzero(hits != 1)[0][:10]
