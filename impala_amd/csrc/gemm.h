@@ -144,7 +144,14 @@ constexpr int gemm_tile_smem() {
 // KACC: accumulator chains per output fragment over alternating k-steps, their elements
 // interleaved (Frag::mma_e) so consecutive MFMAs never wait on each other's result (a lone
 // 16x16x4 fp32 chain issues every 40 cycles instead of 32); summed in chain order at the end.
-template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1>
+// KW (KACC == 1, 4 waves): the waves split each chunk's k-steps instead of the tile -- wave w
+// computes every fragment of the tile over k-steps w, w + 4, ... -- so a wave runs
+// (BR/16)*(BC/16) independent accumulator chains and reads each A / B fragment once for all of
+// them; the four partial tiles are summed in wave order through LDS at the end of the tile,
+// and fragment f's epilogue runs on wave f % 4.  Any BR, BC multiple of 16 (e.g. 32 x 48:
+// 216 tiles of the FC forward at N = 1280, one per CU, instead of 320 32 x 32 tiles).
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1,
+          bool KW = false>
 DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __restrict__ smem) {
   constexpr int NT = 64 * WR * WC;
   constexpr bool AK = Op::A_KMAJOR;
@@ -153,17 +160,23 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int KV = BK / VEC;            // 16-byte vectors per tile row per chunk
   constexpr int LD = BK + tile_pad<T>();  // padded row (elements)
-  constexpr int TRW = BR / 16 / WR, TCW = BC / 16 / WC;
+  // (KW: the per-wave split is unused, but the arrays sized by it must not be empty)
+  constexpr int TRW = BR / 16 / WR > 0 ? BR / 16 / WR : 1, TCW = BC / 16 / WC > 0 ? BC / 16 / WC : 1;
   constexpr int NA = BR * KV / NT, NB = BC * KV / NT;
   constexpr int RV = BR / VEC;            // (A_KMAJOR) 16-byte vectors per k row
   constexpr int LDA = AK ? BR + tile_pad_ak<T>() : LD;  // A tile row length (elements)
   constexpr int ASZ = AK ? BK * LDA : BR * LD;
   constexpr int NK = Op::K / BK;
-  static_assert((WR * WC == 4 || (WR * WC == 8 && !Op::TILE_EPI)) && TRW >= 1 && TCW >= 1, "tile");
+  static_assert((WR * WC == 4 || (WR * WC == 8 && !Op::TILE_EPI)) && (KW || (BR / 16 / WR >= 1 && BC / 16 / WC >= 1)),
+                "tile");
   static_assert(BR * KV % NT == 0 && BC * KV % NT == 0, "staging");
   static_assert(Op::K % BK == 0 && BK % F::KSTEP == 0, "K chunking");
   static_assert((PF == 1 || PF == 2) && (KACC == 1 || KACC == 2) && (BK / F::KSTEP) % KACC == 0, "PF / KACC");
   static_assert(PF == 1 || NK % 2 == 0, "two chunks ahead: an even chunk count per tile");
+  constexpr int FR = BR / 16, FC = BC / 16;  // KW: fragments of the tile, all on every wave
+  constexpr int NOWN = (FR * FC + 3) / 4;     // KW: fragments whose epilogue a wave runs
+  static_assert(!KW || (KACC == 1 && WR * WC == 4 && !Op::TILE_EPI && BR % 16 == 0 &&
+                        BC % 16 == 0 && (BK / F::KSTEP) % 4 == 0), "KW: 4 waves");
   constexpr int SMEM = 2 * (ASZ + BC * LD);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
@@ -229,7 +242,14 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
     const int cr0 = fr0, cc0 = fc0;  // coordinates of tile t (the fetch cursor is on it)
     // the epilogue's global reads, issued now so they land under the K loop
     [[maybe_unused]] typename EpiTypes<Op>::Epi ep[TRW][TCW];
-    if constexpr (!Op::TILE_EPI) {
+    [[maybe_unused]] typename EpiTypes<Op>::Epi epw[KW ? NOWN : 1];
+    if constexpr (KW) {
+#pragma unroll
+      for (int u = 0; u < NOWN; ++u) {
+        const int f = min(wave + 4 * u, FR * FC - 1), i = f / FC, j = f % FC;
+        epw[u] = op.epi(cr0 + i * 16 + 4 * (lane >> 4), min(cc0 + j * 16 + (lane & 15), op.C - 1));
+      }
+    } else if constexpr (!Op::TILE_EPI) {
 #pragma unroll
       for (int j = 0; j < TCW; ++j)
 #pragma unroll
@@ -238,6 +258,13 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
                             min(cc0 + (wc * TCW + j) * 16 + (lane & 15), op.C - 1));
     }
     f32x4 acc[TRW][TCW], acc2[KACC > 1 ? TRW : 1][KACC > 1 ? TCW : 1];
+    f32x4 accw[KW ? FR : 1][KW ? FC : 1];
+    if constexpr (KW) {
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int i = 0; i < TRW; ++i)
 #pragma unroll
@@ -276,7 +303,24 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
         for (int j = 0; j < TCW; ++j)
           b[j] = *reinterpret_cast<const V*>(Bs + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
       };
-      if constexpr (KACC == 1) {
+      if constexpr (KW) {
+#pragma unroll
+        for (int kk = wave * F::KSTEP; kk < BK; kk += 4 * F::KSTEP) {
+          V a[FR], b[FC];
+#pragma unroll
+          for (int i = 0; i < FR; ++i)
+            a[i] = *reinterpret_cast<const V*>(As + (i * 16 + (lane & 15)) * LD + kk + kl);
+#pragma unroll
+          for (int j = 0; j < FC; ++j)
+            b[j] = *reinterpret_cast<const V*>(Bs + (j * 16 + (lane & 15)) * LD + kk + kl);
+#pragma unroll
+          for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+              for (int j = 0; j < FC; ++j) accw[i][j] = F::mma_e(e, a[i], b[j], accw[i][j]);
+        }
+      } else if constexpr (KACC == 1) {
 #pragma unroll
         for (int kk = 0; kk < BK; kk += F::KSTEP) {
           V a[TRW], b[TCW];
@@ -310,6 +354,33 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 #pragma unroll
         for (int j = 0; j < TCW; ++j) acc[i][j] += acc2[i][j];
     }
+    if constexpr (KW) {
+      // the four waves' partial tiles through LDS: [wave][fragment][lane] f32x4, summed in wave
+      // order into this wave's own fragment (wr, wc)
+      static_assert((size_t)4 * FR * FC * 64 * sizeof(f32x4) <= SMEM * sizeof(T), "KW partials");
+      f32x4* part = reinterpret_cast<f32x4*>(smem);
+      __syncthreads();  // every wave is done with the staging buffers
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int j = 0; j < FC; ++j) part[((wave * FR + i) * FC + j) * 64 + lane] = accw[i][j];
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < NOWN; ++u) {
+        const int f = wave + 4 * u;
+        if (f < FR * FC) {
+          f32x4 sum = part[f * 64 + lane];
+#pragma unroll
+          for (int w = 1; w < 4; ++w) sum += part[(w * FR * FC + f) * 64 + lane];
+          const int i = f / FC, j = f % FC, c = cc0 + j * 16 + (lane & 15);
+          if (c < op.C) {
+            float v[4] = {sum[0], sum[1], sum[2], sum[3]};
+            op.store(cr0 + i * 16 + 4 * (lane >> 4), c, v, epw[u]);
+          }
+        }
+      }
+      __syncthreads();  // the next tile's stash reuses the LDS
+    }
     if constexpr (Op::TILE_EPI) {
       // workgroup epilogue: fp32 tile [BC][BR+4] in (reused) LDS, then op.tile_epilogue
       static_assert((size_t)BC * (BR + 4) * sizeof(float) <= SMEM * sizeof(T), "epilogue tile");
@@ -326,7 +397,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
       __syncthreads();
       op.tile_epilogue(et, BR + 4, cr0, cc0, tid, econst);
       __syncthreads();  // the next tile's stash reuses the LDS
-    } else {
+    } else if constexpr (!KW) {
       if constexpr (NK % 2 == 1) __syncthreads();  // next tile reuses buffer 0 first
 #pragma unroll
       for (int j = 0; j < TCW; ++j) {
@@ -343,10 +414,11 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   }
 }
 
-template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1>
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1,
+          bool KW = false>
 __global__ __launch_bounds__(64 * WR * WC) void gemm_tile(const Op op, int n_rtiles) {
   __shared__ __attribute__((aligned(16))) T smem[gemm_tile_smem<T, BR, BC, BK, WR, WC, Op>()];
-  gemm_tile_body<T, BR, BC, BK, WR, WC, Op, PF, KACC>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
+  gemm_tile_body<T, BR, BC, BK, WR, WC, Op, PF, KACC, KW>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
 }
 
 // Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split

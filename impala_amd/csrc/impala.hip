@@ -79,6 +79,11 @@ constexpr int FCD_BR = 32, FCD_BC = 64, FCD_WR = 2, FCD_WC = 2, FCD_G = 4, FCD_P
 // PF / KACC 1 / 1: 13.97 us, 2 / 1: 13.40, 1 / 2: 14.20, 2 / 2: 13.67-13.69 (r04v2,
 // tools/var_specs/fcpf.py); 2 / 1 keeps the summation order, so the output bits are unchanged
 constexpr int FCF_PF = 2, FCF_KACC = 1;
+// fp32 FC forward: 32 (hidden) x FCF_BC (frames) tiles whose 4 waves split each chunk's
+// k-steps (gemm_tile_body KW).  32 x 48: 216 tiles at N = 1280, at most one per CU (the 32 x 32
+// tiles put two on 64 CUs, whose MFMA time bounds the kernel: profiles/r05kw)
+constexpr bool FCF_KW = true;
+constexpr int FCF_BR = 32, FCF_BC = 48;
 Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
   Split s;
   const long chunks = (M + chunk - 1) / chunk;
@@ -355,9 +360,11 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     // 32 x 32 tiles: 320 workgroups (5.9 vs 6.7 us for 64 x 32, tools/var_specs/fcfwd.py);
     // fp32: two K chunks in registers ahead of the MFMAs (FCF_PF / FCF_KACC)
     constexpr int PF = sizeof(T) == 4 ? FCF_PF : 1, KA = sizeof(T) == 4 ? FCF_KACC : 1;
-    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, 32, 32, BK(256), 2, 2, FcFwd<T>, PF, KA>,
-                        dim3(persist_grid(h, (long)cdiv(n, 32) * (HID / 32))), dim3(256), st, op,
-                        HID / 32))
+    constexpr bool KW = sizeof(T) == 4 && FCF_KW;
+    constexpr int BR = KW ? FCF_BR : 32, BC = KW ? FCF_BC : 32;
+    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, BR, BC, BK(256), 2, 2, FcFwd<T>, PF, KA, KW>,
+                        dim3(persist_grid(h, (long)cdiv(n, BC) * (HID / BR))), dim3(256), st, op,
+                        HID / BR))
       return r;
   }
   if (with_heads) {  // inference; in training the fused head kernel computes the heads
