@@ -505,10 +505,17 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
 // tiles for G = 1, 128 x 64 for G = 2).  The weight gradient's 96 workgroups leave most CUs
 // idle for its ~7 us; the dgrad tiles fill them instead of running after it.  Same per-tile
 // arithmetic as the two separate kernels (same tile shapes for the weight gradient).
+// dgrad tiles DR (flat) x DC (frames) on DWR x DWC waves.  fp32: 128 x 80 tiles, 128 of them
+// at N = 1280 beside the 128 weight-gradient workgroups -- 256 workgroups with about the same
+// MFMA work each, one round on 256 CUs (the 64 x 64 tiles made 320 tiles beside the 128, ~1.75
+// rounds at one workgroup per CU)
+constexpr int FCB_DR32 = 128, FCB_DC32 = 80, FCB_DWR32 = 4, FCB_DWC32 = 1;
 template <typename T, int G> struct FcBwdCfg {
-  static constexpr int DR = G == 2 ? 128 : 64, DWR = G == 2 ? 4 : 2, DBK = sizeof(T) == 2 ? 128 : 64;
+  static constexpr int DR = G == 2 ? 128 : FCB_DR32, DWR = G == 2 ? 4 : FCB_DWR32;
+  static constexpr int DC = G == 2 ? 64 : FCB_DC32, DWC = G == 2 ? 2 : FCB_DWC32;
+  static constexpr int DBK = sizeof(T) == 2 ? 128 : 64;
   static constexpr int SW = gemm_wg_smem<T, 64, 256, 32, G>();
-  static constexpr int SD = gemm_tile_smem<T, DR, 64, DBK, DWR, 2, FcDgrad<T>>();
+  static constexpr int SD = gemm_tile_smem<T, DR, DC, DBK, DWR, DWC, FcDgrad<T>>();
   static constexpr int SMEM = SW > SD ? SW : SD;
 };
 template <typename T, int G>
@@ -523,7 +530,7 @@ __global__ __launch_bounds__(256 * G) void fc_bwd_kernel(const FcWgrad<T> ow, fl
     gemm_wg_body<T, 64, 256, 1, 4, 32, G, FcWgrad<T>>(ow, slab, slab_bias, mps, (int)blockIdx.x,
                                                       gx, gy, gz, smem);
   else
-    gemm_tile_body<T, C::DR, 64, C::DBK, C::DWR, 2, FcDgrad<T>>(od, n_rtiles, (int)blockIdx.x - nw,
+    gemm_tile_body<T, C::DR, C::DC, C::DBK, C::DWR, C::DWC, FcDgrad<T>>(od, n_rtiles, (int)blockIdx.x - nw,
                                                                 (int)gridDim.x - nw, smem);
 }
 
