@@ -535,7 +535,7 @@ stage_b:
                           dim3(persist_grid(h, cdiv((long)N * P2, 128))), dim3(256), st, op, 1))
         return r;
     }
-    const int g3x = K3 / 64, g3z = h->sp3.S, g2x = K2 / 128, g2z = h->sp2.S;
+    const int g3x = K3 / 64, g3z = h->sp3.S, g2x = K2 / Wg2Tile<T>::BC, g2z = h->sp2.S;
 #if IMPALA_AB
     if (early) {
       // conv1 + b1 and LayerNorm (+ FC and heads unless part 2 reduced them) units ride along

@@ -1265,7 +1265,7 @@ __global__ __launch_bounds__(256 * G) void wgrad23r_kernel(
     gemm_wg_body<T, 64, 64, 2, 2, 32, G, Conv3Wgrad<T>>(o3, s_w3, s_b3, mps3, b, g3x, 1, g3z,
                                                         reinterpret_cast<T*>(lds));
   } else if (b < n3 + n2) {
-    gemm_wg_body<T, 64, 128, 1, 4, 32, G, Conv2Wgrad<T>>(o2, s_w2, s_b2, mps2, b - n3, g2x, 1, g2z,
+    gemm_wg_body<T, 64, Wg2Tile<T>::BC, Wg2Tile<T>::WR, Wg2Tile<T>::WC, 32, G, Conv2Wgrad<T>>(o2, s_w2, s_b2, mps2, b - n3, g2x, 1, g2z,
                                                          reinterpret_cast<T*>(lds));
   }
 }

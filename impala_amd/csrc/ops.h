@@ -538,8 +538,14 @@ __global__ __launch_bounds__(256 * G) void fc_bwd_kernel(const FcWgrad<T> ow, fl
 // outputs): blocks [0, n3) run the conv3 split weight-gradient body, the rest conv2's -- the
 // same tiles, splits and group order as the two separate launches (bitwise-equal slabs), with
 // one kernel boundary fewer and conv3's tail overlapping conv2's ramp.
+// conv2 weight-gradient tile of the merged launch: fp32 64 x 64 on 2 x 2 waves -- 512 workgroups
+// of conv3's size (64 splits as before, so the same slab and per-element sums), three per CU
+// beside conv3's 252, instead of 256 64 x 128 workgroups of twice conv3's MFMA work; bf16 64 x 128
+template <typename T> struct Wg2Tile {
+  static constexpr int BC = sizeof(T) == 4 ? 64 : 128, WR = sizeof(T) == 4 ? 2 : 1, WC = 4 / WR;
+};
 template <typename T, int G> struct Wg23Cfg {
-  static constexpr int S3 = gemm_wg_smem<T, 64, 64, 32, G>(), S2 = gemm_wg_smem<T, 64, 128, 32, G>();
+  static constexpr int S3 = gemm_wg_smem<T, 64, 64, 32, G>(), S2 = gemm_wg_smem<T, 64, Wg2Tile<T>::BC, 32, G>();
   static constexpr int SMEM = S3 > S2 ? S3 : S2;
 };
 template <typename T, int G>
@@ -553,8 +559,8 @@ __global__ __launch_bounds__(256 * G) void wgrad23_kernel(const Conv3Wgrad<T> o3
     gemm_wg_body<T, 64, 64, 2, 2, 32, G, Conv3Wgrad<T>>(o3, s_w3, s_b3, mps3, (int)blockIdx.x, g3x, 1,
                                                         g3z, smem);
   else
-    gemm_wg_body<T, 64, 128, 1, 4, 32, G, Conv2Wgrad<T>>(o2, s_w2, s_b2, mps2, (int)blockIdx.x - n3,
-                                                         g2x, 1, g2z, smem);
+    gemm_wg_body<T, 64, Wg2Tile<T>::BC, Wg2Tile<T>::WR, Wg2Tile<T>::WC, 32, G, Conv2Wgrad<T>>(
+        o2, s_w2, s_b2, mps2, (int)blockIdx.x - n3, g2x, 1, g2z, smem);
 }
 
 #if IMPALA_AB  // fwd_chain_kernel: measured slower, A/B builds only
