@@ -263,6 +263,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_s2d(const uint8_t* __restrict__
 // G 4-wave groups per workgroup take alternating frames of the workgroup's run.
 // ---------------------------------------------------------------------------------------
 template <typename T> constexpr int c12f_groups() { return sizeof(T) == 2 ? 2 : 1; }
+// waves per frame group: fp32 runs one frame at a time (its act1 tile and the frames' act2 fill
+// the LDS) on 8 waves, two per SIMD.  wq = wave & 3 takes the conv1 row phase and the conv2 /
+// conv3 output-channel tile, wh = wave >> 2 the conv1 output-channel tile.  conv2 and the conv3
+// GEMM run on waves 0..3 as before (split further, every wave would stream the W2 rows of its
+// tile: twice the weight traffic, 60 -> 68 us, profiles/r05fw8); waves 4..7 stash the next
+// image under waves 0..3's conv2.  Each output's k order is the 4-wave one (bitwise equal).
+template <typename T> constexpr int c12f_wpg() { return sizeof(T) == 2 ? 4 : 8; }
+template <typename T> constexpr int c12f_threads() { return 64 * c12f_wpg<T>() * c12f_groups<T>(); }
 
 // Optional conv3 + ReLU + LayerNorm tail of the fused forward (bf16): after its frames, the
 // workgroup stages W3 in LDS and computes conv3 for them from act2 kept in LDS, one wave per
@@ -331,7 +339,13 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   static_assert(G * GSZ + A2SZ == C12FLds<T>::ELEMS && GSZ == C12FLds<T>::GSZ, "LDS layout");
   T* a2s = smem + G * GSZ;
   const bool tail = c3.act3 != nullptr;
-  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  constexpr int WPG = c12f_wpg<T>(), NTG = 64 * WPG;
+  const int grp = (int)threadIdx.x / NTG, tid = (int)threadIdx.x % NTG, lane = tid & 63, wave = tid >> 6;
+  const int wq = wave & 3, wh = WPG == 8 ? wave >> 2 : 0;
+  constexpr int NI = WPG == 8 ? 1 : 2;  // conv1 output-channel tiles per wave
+  // the image loads / stash run on 256 threads: fp32 on waves 4..7, during waves 0..3's conv2
+  const bool ldr = WPG == 8 ? wh == 1 : tid < 256;
+  const int ltid = WPG == 8 ? tid - 256 : tid;
   // the image is bf16 in both modes: the bytes 0..255 are exact in bf16.  fp32 runs conv1 as
   // three exact bf16 MFMA passes (W1 split hi + mid + lo, below) over it.
   using FB = Frag<__bf16>;
@@ -344,18 +358,18 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = KPL * (lane >> 4);
   uint4 nv[3];
-  if (f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, tid, nv);
+  if (ldr && f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, ltid, nv);
   // biases: 16-byte loads issued with the frame, ahead of the weights (waiting for the weights
   // then covers them: loads retire in order)
   float bb1[2][4], bb2[4];
   // fp32: the conv2 bias of this lane's 4x4x1-block output channel (loaded in the frame loop, it
   // cost a wait for every load in flight there, the next frame's image included: 0.7-1.3k
   // clocks per frame, tools/var_specs/fwdstash32.py r04v4)
-  const float bb2q = b2[16 * wave + 4 * ((lane >> 2) & 3) + (lane >> 4)];
+  const float bb2q = b2[16 * wq + 4 * ((lane >> 2) & 3) + (lane >> 4)];
   {
     const f32x4 u0 = *reinterpret_cast<const f32x4*>(b1 + 4 * (lane >> 4));
     const f32x4 u1 = *reinterpret_cast<const f32x4*>(b1 + 16 + 4 * (lane >> 4));
-    const f32x4 u2 = *reinterpret_cast<const f32x4*>(b2 + 16 * wave + 4 * (lane >> 4));
+    const f32x4 u2 = *reinterpret_cast<const f32x4*>(b2 + 16 * wq + 4 * (lane >> 4));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       bb1[0][q] = u0[q];
@@ -370,8 +384,8 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // split exactly into three bf16 terms x = hi + mid + lo (fp32 mode: round-to-nearest 8-bit
   // pieces of a 24-bit significand; each product with an image byte is exact in the fp32
   // accumulator, so the three passes give the fp32 products)
-  VB wa1[2][NKB1][sizeof(T) == 4 ? 3 : 1];
-  const T* w2row = w2 + (size_t)(16 * wave + (lane & 15)) * K2 + kl;  // conv2: oc tile = wave
+  VB wa1[NI][NKB1][sizeof(T) == 4 ? 3 : 1];
+  const T* w2row = w2 + (size_t)(16 * wq + (lane & 15)) * K2 + kl;  // conv2: oc tile = wq
   // bf16: this wave's W2 rows in registers for the whole frame run (64 VGPRs).  fp32 reads its
   // fragments from L2 per k-step: holding all 128 VGPRs of them made the kernel 3.5 us slower
   // (78.9 -> 82.4 us, r03 q32 run)
@@ -416,16 +430,16 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
     // the fragments read from LDS
     static_assert(3 * OC1 * C1W_LD * 2 <= (int)sizeof(T) * G * GSZ, "W1 plane staging");
     __bf16* w1p = reinterpret_cast<__bf16*>(smem);
-    c1_stage_w1_f32(reinterpret_cast<const float*>(w1), w1p, (int)threadIdx.x);
+    if (threadIdx.x < 256) c1_stage_w1_f32(reinterpret_cast<const float*>(w1), w1p, (int)threadIdx.x);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int kb = 0; kb < NKB1; ++kb)
 #pragma unroll
         for (int tm = 0; tm < 3; ++tm)
-          wa1[i][kb][tm] = *reinterpret_cast<const VB*>(w1p + (tm * OC1 + 16 * i + (lane & 15)) * C1W_LD +
-                                                        kb * FB::KSTEP + klb);
+          wa1[i][kb][tm] = *reinterpret_cast<const VB*>(
+              w1p + (tm * OC1 + 16 * (NI == 1 ? wh : i) + (lane & 15)) * C1W_LD + kb * FB::KSTEP + klb);
     __syncthreads();  // the staging area becomes the frame tiles
   }
   // consume the bias loads here: waits for them placed inside the loop would (merged over the
@@ -442,7 +456,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // (scale, bias, ReLU, bf16 pack, mask bits, stores) runs on the VALU.
   int c1base[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) c1base[t] = (min(wave + 4 * t, 14) * c1::GRID + (lane & 15)) * ILDI;
+  for (int t = 0; t < 4; ++t) c1base[t] = (min(wq + 4 * t, 14) * c1::GRID + (lane & 15)) * ILDI;
   auto c1_off = [&](int kb) {  // bf16 fragment k-block kb: this lane's 8 k = 8 channels of one tap
     const int k = kb * FB::KSTEP + klb, tap = k / c1::CH, ch = k - tap * c1::CH;
     return ((tap >> 1) * c1::GRID + (tap & 1)) * ILDI + ch;
@@ -469,9 +483,11 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   const __amdgpu_buffer_rsrc_t rs_mask =
       __builtin_amdgcn_make_buffer_rsrc(mask, 0, N * c1::NPIX * 4, 0x00020000);
   constexpr int OOB = 0x7ffffff0;
-  auto c1_mma = [&](f32x4 (&acc)[2][2], int t0) {
+  auto c1_mma = [&](f32x4 (&acc)[2][NI], int t0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ii = 0; ii < NI; ++ii) acc[u][ii] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr int NT = sizeof(T) == 4 ? 3 : 1;  // W1 terms
     VB bq[2][2];
 #pragma unroll
@@ -486,27 +502,27 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
 #pragma unroll
       for (int tm = 0; tm < NT; ++tm)
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          acc[u][0] = FB::mma(wa1[0][kb][tm], bq[kb & 1][u], acc[u][0]);
-          acc[u][1] = FB::mma(wa1[1][kb][tm], bq[kb & 1][u], acc[u][1]);
-        }
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int ii = 0; ii < NI; ++ii) acc[u][ii] = FB::mma(wa1[ii][kb][tm], bq[kb & 1][u], acc[u][ii]);
     }
   };
-  auto c1_epi = [&](const f32x4 (&acc)[2][2], int t0, int f) {
+  auto c1_epi = [&](const f32x4 (&acc)[2][NI], int t0, int f) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int oy = wave + 4 * (t0 + u), ox = lane & 15;
+      const int oy = wq + 4 * (t0 + u), ox = lane & 15;
       const bool st = oy < H1 && ox < H1;
       const int pc = oy * H1 + ox;               // act1 / mask pixel (15 x 15)
       T* arow = a1s + (oy * A1P + ox) * LDA1;    // LDS act1 row (pad lanes: unused slots)
       const int gofs = st ? (int)((((size_t)f * c1::NPIX + pc) * OC1) * sizeof(T)) : OOB;
       uint32_t bits = 0;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int ii = 0; ii < NI; ++ii) {
+        const int i = NI == 1 ? wh : ii;  // output-channel tile
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float xv = acc[u][i][q] * (1.f / 255.f) + bb1[i][q];
+          const float xv = acc[u][ii][q] * (1.f / 255.f) + bb1[i][q];
           v[q] = fmaxf(xv, 0.f);
           // ReLU mask bit = (x > 0): the float's bits as a signed int are > 0 exactly then
           // (one v_med3_i32)
@@ -524,15 +540,21 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         }
       }
       bits = xor32_or(xor16_or(bits));
-      __builtin_amdgcn_raw_buffer_store_b32((int)bits, rs_mask,
-                                            st && lane < 16 ? (int)(((size_t)f * c1::NPIX + pc) * 4) : OOB,
-                                            0, 0);
+      if constexpr (NI == 2) {
+        __builtin_amdgcn_raw_buffer_store_b32((int)bits, rs_mask,
+                                              st && lane < 16 ? (int)(((size_t)f * c1::NPIX + pc) * 4) : OOB,
+                                              0, 0);
+      } else {  // this wave's 16 bits (oc tile wh) into its half of the pixel's mask word
+        __builtin_amdgcn_raw_buffer_store_b16((short)(bits >> (16 * wh)), rs_mask,
+                                              st && lane < 16 ? (int)(((size_t)f * c1::NPIX + pc) * 4 + 2 * wh) : OOB,
+                                              0, 0);
+      }
     }
   };
   // the group's first frame goes into the image now (the weight staging area is free), and the
   // second is fetched; every later frame is staged during the previous frame's conv2
-  if (f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, tid, nv);
-  if (f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, tid, nv);
+  if (ldr && f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
+  if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, ltid, nv);
   __syncthreads();
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
@@ -540,7 +562,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
     V ar0[3];  // fp32: conv2's first W2 fragments, loaded under this frame's conv1
     if (active) {
       // ---- conv1 -> act1 (HBM + LDS) and its ReLU bit mask ----
-      f32x4 accA[2][2], accB[2][2];
+      f32x4 accA[2][NI], accB[2][NI];
       // issued here, 4.6k clocks ahead of their use: loaded at the top of the conv2 loop, the
       // first MFMA of every frame waited a whole L2 round trip (forward 60.2 -> 58.8 us,
       // tools/var_specs/w2early.py r04v7)
@@ -559,8 +581,12 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                       f32x4{0.f, 0.f, 0.f, 0.f}};
       V bq[2][3];
+      constexpr int NPT = W2REG ? 3 : 2;  // 16-pixel tiles in slots 0 .. NPT-1
+      const bool c2w = WPG == 4 || wh == 0;  // fp32: conv2 on waves 0..3, the stash on 4..7
+      if (c2w) {
 #pragma unroll
-      for (int pt = 0; pt < 3; ++pt) bq[0][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + c2_off(0));
+      for (int pt = 0; pt < 3; ++pt)
+        if (pt < NPT || pt == 2) bq[0][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + c2_off(0));
       // fp32: the W2 fragments stream from L2 in a ring PD2 k-steps ahead of their MFMAs (the
       // order pinned by scheduling barriers; the compiler kept them one step ahead)
       constexpr int PD2 = W2REG ? 1 : 4;
@@ -578,7 +604,8 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         if (ks + 1 < NKS2) {
           const int off = c2_off(ks + 1);
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) bq[(ks + 1) & 1][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + off);
+          for (int pt = 0; pt < 3; ++pt)
+            if (pt < NPT || pt == 2) bq[(ks + 1) & 1][pt] = *reinterpret_cast<const V*>(a1s + c2row[pt] + off);
         }
         V a;
         if constexpr (W2REG) a = wa2[ks];
@@ -600,13 +627,14 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         }
         if constexpr (!W2REG) __builtin_amdgcn_sched_barrier(0);
       }
-      if (f + G < f1) c1_stash_frame_rot<__bf16, ILDI>(img, tid, nv);
-      if (f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, tid, nv);
-      if constexpr (!W2REG) {
+      }
+      if (ldr && f + G < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
+      if (ldr && f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, ltid, nv);
+      if (!W2REG && wh == 0) {
         // the 4x4x1 blocks: lane 16 g + 4 og + j holds act2[pixel 32 + j][oc 16 w + 4 og + reg]
         // over k-phase g; ((g0 + g1) + (g2 + g3)) of reg q lands on row q (rows_sum4), so lane
         // 16 q + 4 og + j stores one value
-        const int pc = 32 + (lane & 3), oc = 16 * wave + 4 * ((lane >> 2) & 3) + (lane >> 4);
+        const int pc = 32 + (lane & 3), oc = 16 * wq + 4 * ((lane >> 2) & 3) + (lane >> 4);
         const float v = fmaxf(rows_sum4(acc[2][0], acc[2][1], acc[2][2], acc[2][3]) + bb2q, 0.f);
         act2[((size_t)f * P2 + pc) * OC2 + oc] = (T)v;
         if (tail) {
@@ -615,16 +643,16 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
         }
       }
 #pragma unroll
-      for (int pt = 0; pt < (W2REG ? 3 : 2); ++pt) {
+      for (int pt = 0; pt < NPT; ++pt) {
         const int pc = pt * 16 + (lane & 15);
-        if (pc < P2) {
+        if (c2w && pc < P2) {
           float v[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = fmaxf(acc[pt][q] + bb2[q], 0.f);
-          store4(act2 + ((size_t)f * P2 + pc) * OC2 + 16 * wave + 4 * (lane >> 4), v);
+          store4(act2 + ((size_t)f * P2 + pc) * OC2 + 16 * wq + 4 * (lane >> 4), v);
           if (tail) {
             const int cy = pc / H2, cx = pc - cy * H2;
-            store4(a2s + ((f - f0) * A2F + cy * A2W + cx) * LDA2 + 16 * wave + 4 * (lane >> 4), v);
+            store4(a2s + ((f - f0) * A2F + cy * A2W + cx) * LDA2 + 16 * wq + 4 * (lane >> 4), v);
           }
         }
       }
@@ -700,59 +728,69 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       // issue itself (per-CU load bandwidth, ~17 B/clk) for ~7k cycles before the first MFMA
       // (r03 stamps)
       constexpr int PD3 = 8;
-      V w3a[NKS3];
-      const T* w3row = c3.w3 + (size_t)(16 * wave + (lane & 15)) * K3 + kl;
-#pragma unroll
-      for (int ks = 0; ks < PD3; ++ks) w3a[ks] = F::load(w3row + ks * KS);
       const int nF = f1 - f0;
       const LnLane lk = ln_lane_consts(lane, c3.b3, c3.gam, c3.bet);
-      const int p = lane & 15, oy = p >> 2, ox = p & 3;
-      const T* a2f = a2s + (oy * A2W + ox) * LDA2 + kl;
-      f32x4 acc3[FMAX];
+      float* ets = reinterpret_cast<float*>(smem);
+      if (wh == 0) {  // (8 waves: the first four run the conv3 GEMM, all eight the LayerNorm)
+        V w3a[NKS3];
+        const T* w3row = c3.w3 + (size_t)(16 * wq + (lane & 15)) * K3 + kl;
 #pragma unroll
-      for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // every frame slot runs (a slot past the run re-reads the last frame; its result is
-      // dropped), so the FMAX accumulators interleave (F::mma_e); the act2 window reads run one
-      // k-step ahead (k = ks*16 + kl: tap = k / 64, ci = k % 64)
-      auto bload = [&](int ks, V* b) {
-        const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
+        for (int ks = 0; ks < PD3; ++ks) w3a[ks] = F::load(w3row + ks * KS);
+        const int p = lane & 15, oy = p >> 2, ox = p & 3;
+        const T* a2f = a2s + (oy * A2W + ox) * LDA2 + kl;
+        f32x4 acc3[FMAX];
+#pragma unroll
+        for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // every frame slot runs (a slot past the run re-reads the last frame; its result is
+        // dropped), so the FMAX accumulators interleave (F::mma_e); the act2 window reads run one
+        // k-step ahead (k = ks*16 + kl: tap = k / 64, ci = k % 64)
+        auto bload = [&](int ks, V* b) {
+          const int k = ks * KS, tap = k >> 6, kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+          for (int fr = 0; fr < FMAX; ++fr)
+            b[fr] = *reinterpret_cast<const V*>(a2f + (min(fr, nF - 1) * A2F + kh * A2W + kw) * LDA2 + (k & 63));
+        };
+        V b[2][FMAX];
+        bload(0, b[0]);
+#pragma unroll
+        for (int ks = 0; ks < NKS3; ++ks) {
+          if (ks + PD3 < NKS3) w3a[ks + PD3] = F::load(w3row + (ks + PD3) * KS);
+          if (ks + 1 < NKS3) bload(ks + 1, b[(ks + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int e = 0; e < F::NE; ++e)
+#pragma unroll
+            for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = F::mma_e(e, w3a[ks], b[ks & 1][fr], acc3[fr]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int fr = 0; fr < FMAX; ++fr)
-          b[fr] = *reinterpret_cast<const V*>(a2f + (min(fr, nF - 1) * A2F + kh * A2W + kw) * LDA2 + (k & 63));
-      };
-      V b[2][FMAX];
-      bload(0, b[0]);
-#pragma unroll
-      for (int ks = 0; ks < NKS3; ++ks) {
-        if (ks + PD3 < NKS3) w3a[ks + PD3] = F::load(w3row + (ks + PD3) * KS);
-        if (ks + 1 < NKS3) bload(ks + 1, b[(ks + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int e = 0; e < F::NE; ++e)
-#pragma unroll
-          for (int fr = 0; fr < FMAX; ++fr) acc3[fr] = F::mma_e(e, w3a[ks], b[ks & 1][fr], acc3[fr]);
-        __builtin_amdgcn_sched_barrier(0);
+          if (fr < nF) *reinterpret_cast<f32x4*>(ets + (fr * P3 + p) * LDE + 16 * wq + 4 * (lane >> 4)) = acc3[fr];
       }
-      float* ets = reinterpret_cast<float*>(smem);
-#pragma unroll
-      for (int fr = 0; fr < FMAX; ++fr)
-        if (fr < nF) *reinterpret_cast<f32x4*>(ets + (fr * P3 + p) * LDE + 16 * wave + 4 * (lane >> 4)) = acc3[fr];
       __syncthreads();
-      // frames wave and wave + 4 (FMAX <= 8) in one interleaved pass
-      static_assert(FMAX <= 8, "two frames per wave");
-      if (wave + 4 < nF) {
-        const int fr2[2] = {f0 + wave, f0 + wave + 4};
-        ln_frames_epilogue<T, 2>(ets + wave * P3 * LDE, 4 * P3 * LDE, LDE, fr2, lane, lk, c3.act3, c3.y, c3.stats);
-      } else if (wave < nF) {
-        const int fr1[1] = {f0 + wave};
-        ln_frames_epilogue<T, 1>(ets + wave * P3 * LDE, 0, LDE, fr1, lane, lk, c3.act3, c3.y, c3.stats);
+      if constexpr (WPG == 8) {  // one frame per wave
+        static_assert(FMAX <= 8, "a wave per frame");
+        if (wave < nF) {
+          const int fr1[1] = {f0 + wave};
+          ln_frames_epilogue<T, 1>(ets + wave * P3 * LDE, 0, LDE, fr1, lane, lk, c3.act3, c3.y, c3.stats);
+        }
+      } else {
+        // frames wave and wave + 4 (FMAX <= 8) in one interleaved pass
+        static_assert(FMAX <= 8, "two frames per wave");
+        if (wave + 4 < nF) {
+          const int fr2[2] = {f0 + wave, f0 + wave + 4};
+          ln_frames_epilogue<T, 2>(ets + wave * P3 * LDE, 4 * P3 * LDE, LDE, fr2, lane, lk, c3.act3, c3.y, c3.stats);
+        } else if (wave < nF) {
+          const int fr1[1] = {f0 + wave};
+          ln_frames_epilogue<T, 1>(ets + wave * P3 * LDE, 0, LDE, fr1, lane, lk, c3.act3, c3.y, c3.stats);
+        }
       }
     }
   }
 }
 
 template <typename T>
-__global__ __launch_bounds__(256 * c12f_groups<T>()) void conv12_fwd_s2d(
+__global__ __launch_bounds__(c12f_threads<T>()) void conv12_fwd_s2d(
     const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
     const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
     uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3,

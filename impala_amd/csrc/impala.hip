@@ -309,7 +309,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     }
 #endif
     if (int r = klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>,
-                        dim3(cdiv(n, fpw)), dim3(256 * c12f_groups<T>()), st, obs, sw + sh.w1,
+                        dim3(cdiv(n, fpw)), dim3(c12f_threads<T>()), st, obs, sw + sh.w1,
                         vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
                         (T*)h->act2, n, fpw, c3, with_heads ? nullptr : step_stamp(h)))
       return r;
