@@ -458,7 +458,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     ow.M = N; ow.x = (const T*)h->dz; ow.y = (const T*)h->y;
     FcDgrad<T> od{N, sw + sh.wfc, (const T*)h->dz, h->dy};
     using C = FcBwdCfg<T, WG2>;
-    const int gx = FLAT / 256, gy = HID / 64, gz = h->spfc.S;
+    const int gx = FLAT / C::WBC, gy = HID / 64, gz = h->spfc.S;
     const int n_rt = FLAT / C::DR, n_dt = n_rt * cdiv(N, C::DC);
     if (int r = klaunch(h, K_FC_BWD, "fc_wgrad_fc_dgrad", fc_bwd_kernel<T, WG2>,
                         dim3(gx * gy * gz + n_dt), dim3(256 * WG2), st, ow, h->s_fc, h->s_bfc,

@@ -505,16 +505,20 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
 // tiles for G = 1, 128 x 64 for G = 2).  The weight gradient's 96 workgroups leave most CUs
 // idle for its ~7 us; the dgrad tiles fill them instead of running after it.  Same per-tile
 // arithmetic as the two separate kernels (same tile shapes for the weight gradient).
-// dgrad tiles DR (flat) x DC (frames) on DWR x DWC waves.  fp32: 128 x 80 tiles, 128 of them
-// at N = 1280 beside the 128 weight-gradient workgroups -- 256 workgroups with about the same
-// MFMA work each, one round on 256 CUs (the 64 x 64 tiles made 320 tiles beside the 128, ~1.75
-// rounds at one workgroup per CU)
-constexpr int FCB_DR32 = 128, FCB_DC32 = 80, FCB_DWR32 = 4, FCB_DWC32 = 1;
+// dgrad tiles DR (flat) x DC (frames) on DWR x DWC waves, weight-gradient tiles 64 x WBC.
+// fp32: 64 x 80 dgrad tiles (256 at N = 1280, 78 KB of LDS) beside 256 weight-gradient
+// workgroups of 64 x 128 (the same 8 splits, 51 KB): 512 workgroups of about the same MFMA
+// work, two per CU -- two waves per SIMD (profiles/r05kw: 64 x 64 dgrad tiles beside 64 x 256
+// weight-gradient tiles ran ~1.75 rounds at one workgroup per CU, 20.6 us; 128 x 80 one round
+// at one per CU, 19.7; this 16.7)
+constexpr int FCB_DR32 = 64, FCB_DC32 = 80, FCB_DWR32 = 4, FCB_DWC32 = 1;
+constexpr int FCB_WBC32 = 128;
 template <typename T, int G> struct FcBwdCfg {
   static constexpr int DR = G == 2 ? 128 : FCB_DR32, DWR = G == 2 ? 4 : FCB_DWR32;
   static constexpr int DC = G == 2 ? 64 : FCB_DC32, DWC = G == 2 ? 2 : FCB_DWC32;
   static constexpr int DBK = sizeof(T) == 2 ? 128 : 64;
-  static constexpr int SW = gemm_wg_smem<T, 64, 256, 32, G>();
+  static constexpr int WBC = G == 2 ? 256 : FCB_WBC32;
+  static constexpr int SW = gemm_wg_smem<T, 64, WBC, 32, G>();
   static constexpr int SD = gemm_tile_smem<T, DR, DC, DBK, DWR, DWC, FcDgrad<T>>();
   static constexpr int SMEM = SW > SD ? SW : SD;
 };
@@ -527,8 +531,8 @@ __global__ __launch_bounds__(256 * G) void fc_bwd_kernel(const FcWgrad<T> ow, fl
   __shared__ __attribute__((aligned(16))) T smem[C::SMEM];
   const int nw = gx * gy * gz;
   if ((int)blockIdx.x < nw)
-    gemm_wg_body<T, 64, 256, 1, 4, 32, G, FcWgrad<T>>(ow, slab, slab_bias, mps, (int)blockIdx.x,
-                                                      gx, gy, gz, smem);
+    gemm_wg_body<T, 64, C::WBC, 1, 4, 32, G, FcWgrad<T>>(ow, slab, slab_bias, mps, (int)blockIdx.x,
+                                                         gx, gy, gz, smem);
   else
     gemm_tile_body<T, C::DR, C::DC, C::DBK, C::DWR, C::DWC, FcDgrad<T>>(od, n_rtiles, (int)blockIdx.x - nw,
                                                                 (int)gridDim.x - nw, smem);
