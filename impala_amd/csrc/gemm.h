@@ -144,11 +144,11 @@ constexpr int gemm_tile_smem() {
 // KACC: accumulator chains per output fragment over alternating k-steps, their elements
 // interleaved (Frag::mma_e) so consecutive MFMAs never wait on each other's result (a lone
 // 16x16x4 fp32 chain issues every 40 cycles instead of 32); summed in chain order at the end.
-// KW (KACC == 1, 4 waves): the waves split each chunk's k-steps instead of the tile -- wave w
-// computes every fragment of the tile over k-steps w, w + 4, ... -- so a wave runs
+// KW (KACC == 1): the NW waves split each chunk's k-steps instead of the tile -- wave w
+// computes every fragment of the tile over k-steps w, w + NW, ... -- so a wave runs
 // (BR/16)*(BC/16) independent accumulator chains and reads each A / B fragment once for all of
-// them; the four partial tiles are summed in wave order through LDS at the end of the tile,
-// and fragment f's epilogue runs on wave f % 4.  Any BR, BC multiple of 16 (e.g. 32 x 48:
+// them; the NW partial tiles are summed in wave order through LDS at the end of the tile,
+// and fragment f's epilogue runs on wave f % NW.  Any BR, BC multiple of 16 (e.g. 32 x 48:
 // 216 tiles of the FC forward at N = 1280, one per CU, instead of 320 32 x 32 tiles).
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1,
           bool KW = false>
@@ -174,9 +174,10 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   static_assert((PF == 1 || PF == 2) && (KACC == 1 || KACC == 2) && (BK / F::KSTEP) % KACC == 0, "PF / KACC");
   static_assert(PF == 1 || NK % 2 == 0, "two chunks ahead: an even chunk count per tile");
   constexpr int FR = BR / 16, FC = BC / 16;  // KW: fragments of the tile, all on every wave
-  constexpr int NOWN = (FR * FC + 3) / 4;     // KW: fragments whose epilogue a wave runs
-  static_assert(!KW || (KACC == 1 && WR * WC == 4 && !Op::TILE_EPI && BR % 16 == 0 &&
-                        BC % 16 == 0 && (BK / F::KSTEP) % 4 == 0), "KW: 4 waves");
+  constexpr int NW = WR * WC;                   // waves (KW: each takes every NW-th k-step)
+  constexpr int NOWN = (FR * FC + NW - 1) / NW;  // KW: fragments whose epilogue a wave runs
+  static_assert(!KW || (KACC == 1 && !Op::TILE_EPI && BR % 16 == 0 && BC % 16 == 0 &&
+                        (BK / F::KSTEP) % NW == 0), "KW: whole k-steps per wave per chunk");
   constexpr int SMEM = 2 * (ASZ + BC * LD);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
@@ -246,7 +247,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
     if constexpr (KW) {
 #pragma unroll
       for (int u = 0; u < NOWN; ++u) {
-        const int f = min(wave + 4 * u, FR * FC - 1), i = f / FC, j = f % FC;
+        const int f = min(wave + NW * u, FR * FC - 1), i = f / FC, j = f % FC;
         epw[u] = op.epi(cr0 + i * 16 + 4 * (lane >> 4), min(cc0 + j * 16 + (lane & 15), op.C - 1));
       }
     } else if constexpr (!Op::TILE_EPI) {
@@ -305,7 +306,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
       };
       if constexpr (KW) {
 #pragma unroll
-        for (int kk = wave * F::KSTEP; kk < BK; kk += 4 * F::KSTEP) {
+        for (int kk = wave * F::KSTEP; kk < BK; kk += NW * F::KSTEP) {
           V a[FR], b[FC];
 #pragma unroll
           for (int i = 0; i < FR; ++i)
@@ -355,9 +356,9 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
         for (int j = 0; j < TCW; ++j) acc[i][j] += acc2[i][j];
     }
     if constexpr (KW) {
-      // the four waves' partial tiles through LDS: [wave][fragment][lane] f32x4, summed in wave
-      // order into this wave's own fragment (wr, wc)
-      static_assert((size_t)4 * FR * FC * 64 * sizeof(f32x4) <= SMEM * sizeof(T), "KW partials");
+      // the waves' partial tiles through LDS: [wave][fragment][lane] f32x4, summed in wave order;
+      // fragment f's epilogue on wave f % NW
+      static_assert((size_t)NW * FR * FC * 64 * sizeof(f32x4) <= SMEM * sizeof(T), "KW partials");
       f32x4* part = reinterpret_cast<f32x4*>(smem);
       __syncthreads();  // every wave is done with the staging buffers
 #pragma unroll
@@ -367,11 +368,11 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < NOWN; ++u) {
-        const int f = wave + 4 * u;
+        const int f = wave + NW * u;
         if (f < FR * FC) {
           f32x4 sum = part[f * 64 + lane];
 #pragma unroll
-          for (int w = 1; w < 4; ++w) sum += part[(w * FR * FC + f) * 64 + lane];
+          for (int w = 1; w < NW; ++w) sum += part[(w * FR * FC + f) * 64 + lane];
           const int i = f / FC, j = f % FC, c = cc0 + j * 16 + (lane & 15);
           if (c < op.C) {
             float v[4] = {sum[0], sum[1], sum[2], sum[3]};

@@ -84,6 +84,7 @@ constexpr int FCF_PF = 2, FCF_KACC = 1;
 // tiles put two on 64 CUs, whose MFMA time bounds the kernel: profiles/r05kw)
 constexpr bool FCF_KW = true;
 constexpr int FCF_BR = 32, FCF_BC = 48;
+constexpr int FCF_NW = 8;
 Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
   Split s;
   const long chunks = (M + chunk - 1) / chunk;
@@ -362,8 +363,10 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     constexpr int PF = sizeof(T) == 4 ? FCF_PF : 1, KA = sizeof(T) == 4 ? FCF_KACC : 1;
     constexpr bool KW = sizeof(T) == 4 && FCF_KW;
     constexpr int BR = KW ? FCF_BR : 32, BC = KW ? FCF_BC : 32;
-    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, BR, BC, BK(256), 2, 2, FcFwd<T>, PF, KA, KW>,
-                        dim3(persist_grid(h, (long)cdiv(n, BC) * (HID / BR))), dim3(256), st, op,
+    // KW on FCF_NW waves (8: two per SIMD, K chunk 128 = one k-step per wave per chunk)
+    constexpr int NWF = KW ? FCF_NW : 4, FBK = KW && FCF_NW == 8 ? 128 : BK(256);
+    if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, BR, BC, FBK, 2, NWF / 2, FcFwd<T>, PF, KA, KW>,
+                        dim3(persist_grid(h, (long)cdiv(n, BC) * (HID / BR))), dim3(64 * NWF), st, op,
                         HID / BR))
       return r;
   }
