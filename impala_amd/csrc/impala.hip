@@ -364,7 +364,7 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
     constexpr bool KW = sizeof(T) == 4 && FCF_KW;
     constexpr int BR = KW ? FCF_BR : 32, BC = KW ? FCF_BC : 32;
     // KW on FCF_NW waves (8: two per SIMD, K chunk 128 = one k-step per wave per chunk)
-    constexpr int NWF = KW ? FCF_NW : 4, FBK = KW && FCF_NW == 8 ? 128 : BK(256);
+    constexpr int NWF = KW ? FCF_NW : 4, FBK = KW && FCF_NW == 8 ? (sizeof(T) == 4 ? 128 : 256) : BK(256);
     if (int r = klaunch(h, K_FC_FWD, "fc_fwd", gemm_tile<T, BR, BC, FBK, 2, NWF / 2, FcFwd<T>, PF, KA, KW>,
                         dim3(persist_grid(h, (long)cdiv(n, BC) * (HID / BR))), dim3(64 * NWF), st, op,
                         HID / BR))
