@@ -79,11 +79,12 @@ constexpr int FCD_BR = 32, FCD_BC = 64, FCD_WR = 2, FCD_WC = 2, FCD_G = 4, FCD_P
 // PF / KACC 1 / 1: 13.97 us, 2 / 1: 13.40, 1 / 2: 14.20, 2 / 2: 13.67-13.69 (r04v2,
 // tools/var_specs/fcpf.py); 2 / 1 keeps the summation order, so the output bits are unchanged
 constexpr int FCF_PF = 2, FCF_KACC = 1;
-// fp32 FC forward: 32 (hidden) x FCF_BC (frames) tiles whose 4 waves split each chunk's
-// k-steps (gemm_tile_body KW).  32 x 48: 216 tiles at N = 1280, at most one per CU (the 32 x 32
-// tiles put two on 64 CUs, whose MFMA time bounds the kernel: profiles/r05kw)
+// fp32 FC forward: FCF_BR (hidden) x FCF_BC (frames) tiles whose FCF_NW waves split each
+// chunk's k-steps (gemm_tile_body KW).  16 x 80 on 8 waves: 256 tiles at N = 1280, one per CU,
+// two waves per SIMD (the 32 x 32 tiles put two on 64 CUs, whose MFMA time bounds the kernel;
+// 32 x 48 on 4 / 8 waves: 12.3 / 11.7 us, 16 x 80 on 8: 11.4 us; profiles/r05kw)
 constexpr bool FCF_KW = true;
-constexpr int FCF_BR = 32, FCF_BC = 48;
+constexpr int FCF_BR = 16, FCF_BC = 80;
 constexpr int FCF_NW = 8;
 Split plan_split(long M, int tiles, int target_wgs, int chunk = 64) {
   Split s;
