@@ -511,13 +511,15 @@ template <typename T> struct Conv2Wgrad {  // m = (n, oy, ox) in N*36; c = (kh*4
 // work, two per CU -- two waves per SIMD (profiles/r05kw: 64 x 64 dgrad tiles beside 64 x 256
 // weight-gradient tiles ran ~1.75 rounds at one workgroup per CU, 20.6 us; 128 x 80 one round
 // at one per CU, 19.7; this 16.7)
+// bf16 (G = 2, 8 waves): 64 x 64 dgrad tiles on 2 x 4 waves (320) beside 64 x 128 weight-gradient
+// workgroups (192 at the same 6 splits), 78 KB: 512 workgroups, two per CU (8.4 -> 6.8 us)
 constexpr int FCB_DR32 = 64, FCB_DC32 = 80, FCB_DWR32 = 4, FCB_DWC32 = 1;
 constexpr int FCB_WBC32 = 128;
 template <typename T, int G> struct FcBwdCfg {
-  static constexpr int DR = G == 2 ? 128 : FCB_DR32, DWR = G == 2 ? 4 : FCB_DWR32;
-  static constexpr int DC = G == 2 ? 64 : FCB_DC32, DWC = G == 2 ? 2 : FCB_DWC32;
+  static constexpr int DR = G == 2 ? 64 : FCB_DR32, DWR = G == 2 ? 2 : FCB_DWR32;
+  static constexpr int DC = G == 2 ? 64 : FCB_DC32, DWC = G == 2 ? 4 : FCB_DWC32;
   static constexpr int DBK = sizeof(T) == 2 ? 128 : 64;
-  static constexpr int WBC = G == 2 ? 256 : FCB_WBC32;
+  static constexpr int WBC = G == 2 ? 128 : FCB_WBC32;
   static constexpr int SW = gemm_wg_smem<T, 64, WBC, 32, G>();
   static constexpr int SD = gemm_tile_smem<T, DR, DC, DBK, DWR, DWC, FcDgrad<T>>();
   static constexpr int SMEM = SW > SD ? SW : SD;
