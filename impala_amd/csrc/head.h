@@ -54,15 +54,21 @@ struct HeadArgs {
                         // V-trace inputs / outputs (impala_set_debug_vtrace)
 };
 
-constexpr int HEAD_SPLIT = 4;              // workgroups per trajectory group (hidden-column slices)
-constexpr int HEAD_JC = HID / HEAD_SPLIT;  // 64 hidden columns per workgroup in phases 3/4
+// workgroups per trajectory group (hidden-column slices).  fp32 8: 32 columns each, so the
+// kernel fills the 256 CUs at B = 64 (32 groups), and phases 3 / 4 run half the columns per
+// workgroup (the waves split the frame tiles / the frame range instead): 7.9 -> 7.35 us.  bf16
+// 4 (64 columns, one tile per wave): 8 measured 5.7 -> 6.0 us (profiles/r05hs8)
+template <typename T> constexpr int head_split() { return sizeof(T) == 4 ? 8 : 4; }
 
-// grid (groups, HEAD_SPLIT): all HEAD_SPLIT workgroups of a group redo phases 1-2 (cheap: h is an
+// grid (groups, head_split): all head_split workgroups of a group redo phases 1-2 (cheap: h is an
 // L2 hit and the loss is one wavefront), then each takes a 64-column slice of dz / dWh.
 // PPO = true: the PPO clipped-surrogate loss (kernels.h::ppo_frame) on flat transitions (T = 1,
 // one lane per transition, targets in `rew`, `disc` unused) instead of V-trace.
 template <typename T, bool PPO = false>
 __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
+  constexpr int HEAD_JC = HID / head_split<T>();  // hidden columns per workgroup in phases 3/4
+  static_assert(HEAD_JC == 64 || HEAD_JC == 32, "phase 3 / 4 wave map");
+  constexpr int HEAD_CW = HEAD_JC / 16;           // column tiles per workgroup (4 or 2)
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int VEC = 16 / (int)sizeof(T);
@@ -78,6 +84,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   __shared__ __attribute__((aligned(16))) T whs[HEADS * LDH];
   __shared__ f32x4 fst[64];    // per frame: H, KL, log pi(a), rho (phase 2a -> 2b)
   __shared__ float kd[64][2];  // per frame: d loss / d log pi(a), d loss / d value (2b -> 2c)
+  __shared__ f32x4 p4[HEAD_CW == 2 ? 2 : 1][64];  // phase 4 (2 column tiles): the second frame half's partials
   // the wave index as a scalar: `wave == 0` branches are uniform (no exec-mask joins)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T_ = a.T, S = a.S;
@@ -138,7 +145,7 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
     for (int i = 0; i < NWV; ++i) whv[i] = F::load(wh + (size_t)(tid + i * 256) * VEC);
 #pragma unroll
     for (int ks = 0; ks < NKT; ++ks)
-      wtf[ks] = F::load(wht + (jw + wave * 16 + (lane & 15)) * HPAD + ks * F::KSTEP + kl);
+      wtf[ks] = F::load(wht + (jw + (wave % HEAD_CW) * 16 + (lane & 15)) * HPAD + ks * F::KSTEP + kl);
   }
   float bhv[4];
 #pragma unroll
@@ -323,9 +330,10 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   {
     T* dz = reinterpret_cast<T*>(a.dz);
     {
-      const int j0 = jw + wave * 16;
+      // wave: column tile wave % HEAD_CW, frame tiles wave / HEAD_CW, + 4 / HEAD_CW, ...
+      const int j0 = jw + (wave % HEAD_CW) * 16;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = wave / HEAD_CW; ct < 4; ct += 4 / HEAD_CW) {
         if (ct * 16 >= nf) break;  // frame tiles past the group's frames (uniform)
         const int f = ct * 16 + (lane & 15);
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -345,15 +353,27 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   }
   // ---- phase 4: dWh partial = dH^T . h over this group's frames (k = frame) ----
   {
+    // wave: column tile wave % HEAD_CW over frames [k0, k0 + KR): all 64 (4 tiles), or the
+    // half wave / HEAD_CW (2 tiles: the halves summed in order through LDS)
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int c0 = jw + wave * 16;
+    const int c0 = jw + (wave % HEAD_CW) * 16;
+    constexpr int KR = 64 * HEAD_CW / 4;
+    const int k0 = (wave / HEAD_CW) * KR;
 #pragma unroll
-    for (int kk = 0; kk < 64; kk += F::KSTEP)  // k-steps past the group's frames: dH rows 0
-      if (kk < nf)
-        acc = F::mma(lds_frag_k(dHs + kk * LDD, LDD, lane), lds_frag_k(hs + kk * LDH + c0, LDH, lane), acc);
+    for (int kk = 0; kk < KR; kk += F::KSTEP)  // k-steps past the group's frames: dH rows 0
+      if (k0 + kk < nf)
+        acc = F::mma(lds_frag_k(dHs + (k0 + kk) * LDD, LDD, lane),
+                     lds_frag_k(hs + (k0 + kk) * LDH + c0, LDH, lane), acc);
+    if constexpr (HEAD_CW == 2) {
+      if (wave >= 2) p4[wave - 2][lane] = acc;
+      __syncthreads();
+      if (wave < 2) acc += p4[wave][lane];
+    }
     float* sl = a.slab_h + (size_t)blockIdx.x * HEADS * HID;
+    if (wave < HEAD_CW) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sl[(4 * (lane >> 4) + q) * HID + c0 + (lane & 15)] = acc[q];
+      for (int q = 0; q < 4; ++q) sl[(4 * (lane >> 4) + q) * HID + c0 + (lane & 15)] = acc[q];
+    }
     if (lead) {
     {  // bias = sum over frames of dH: 16 frame groups x 16 heads, fixed-order tree
       const int o = tid & 15, fg = tid >> 4;

@@ -450,7 +450,7 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     // torch.clamp(ratio, 1 - clip, 1 + clip): the bounds are python floats cast to fp32
     ha.clip_lo = (float)(1.0 - (double)h->cfg.ppo_clip);
     ha.clip_hi = (float)(1.0 + (double)h->cfg.ppo_clip);
-    const dim3 hg(h->n_loss_wg, HEAD_SPLIT);
+    const dim3 hg(h->n_loss_wg, head_split<T>());
     if (int r = h->cfg.algo == IMPALA_ALGO_PPO
                     ? klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, true>, hg, dim3(256), st, ha)
                     : klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, false>, hg, dim3(256), st, ha))
