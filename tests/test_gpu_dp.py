@@ -10,15 +10,13 @@ overlapped all-reduce.
   batch gradient, up to fp32 summation order amplified by Adam's normalised step).
 """
 import os
-import socket
-import subprocess
-import sys
 
 import numpy as np
 import pytest
 import torch
 
 from oracle import ref_cpu
+from torchrun_util import torchrun
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -82,14 +80,6 @@ def test_grad_parts_match_whole_backward(dtype):
     np.testing.assert_array_equal(e4.metrics.cpu().numpy(), met_whole)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 WORKER = r"""
 import os, sys, numpy as np, torch
 sys.path.insert(0, os.environ["IMPALA_ROOT"])
@@ -127,9 +117,7 @@ def test_two_replicas_bucketed_allreduce_match_full_batch(tmp_path, buckets):
     wf = tmp_path / "worker.py"
     wf.write_text(WORKER)
     env = dict(os.environ, IMPALA_ROOT=ROOT, OUT=str(tmp_path), IMPALA_DP_BUCKETS=buckets)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(wf)]
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    r = torchrun(wf, 2, env, ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
     np.testing.assert_array_equal(p0, p1)  # replicas stay bit-identical

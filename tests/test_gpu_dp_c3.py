@@ -14,15 +14,13 @@
 """
 import json
 import os
-import socket
-import subprocess
-import sys
 
 import numpy as np
 import pytest
 import torch
 
 from oracle import ref_cpu
+from torchrun_util import torchrun
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,23 +32,12 @@ def _dev():
     return torch.device("cuda:0")
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _launch(tmp_path, src, nproc, extra_env=None, timeout=300):
     wf = tmp_path / "worker.py"
     wf.write_text(src)
     env = dict(os.environ, IMPALA_ROOT=ROOT, OUT=str(tmp_path), **(extra_env or {}))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
-           f"--master-port={_free_port()}", str(wf)]
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    r = torchrun(wf, nproc, env, ROOT, timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return r
 
