@@ -152,6 +152,7 @@ enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROW_MIRROR = 0x140,
 // with two read-write operands keeps the two copies in distinct registers: the builtin lets the
 // compiler tie both operands to one register, which swaps a register with itself.  The s_nop
 // covers the VALU-write -> permlane-read hazard the compiler cannot see through inline asm.
+// (Operand semantics checked on gfx950 by tools/probe/permswap.hip.)
 DEV void swap16(uint32_t& a, uint32_t& b) { asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
 DEV void swap32(uint32_t& a, uint32_t& b) { asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
 DEV float xor16_sum(float v) {  // v[lane & ~16] + v[lane | 16] on every lane
