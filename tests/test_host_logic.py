@@ -310,3 +310,25 @@ def test_adam_block_partition_covers_every_parameter_once(A):
         if i < total:
             hits[i] += 1
     assert (hits == 1).all(), np.nonzero(hits != 1)[0][:10]
+
+
+def test_torchrun_relaunches_only_on_a_rendezvous_port_race(monkeypatch):
+    """tests/torchrun_util.py launches again only when the launcher's store lost its port
+    (EADDRINUSE at rendezvous, before any worker starts); any other failure is returned."""
+    import subprocess
+    import torchrun_util
+
+    race = subprocess.CompletedProcess([], 1, "", "next_rendezvous ... EADDRINUSE, address already in use")
+    crash = subprocess.CompletedProcess([], 1, "", "worker raised RuntimeError")
+    ok = subprocess.CompletedProcess([], 0, "", "")
+    for seq, want_calls, want_rc in (([race, ok], 2, 0), ([crash, ok], 1, 1), ([race] * 3, 3, 1)):
+        calls = []
+
+        def run(cmd, seq=seq, calls=calls, **kw):
+            calls.append(cmd)
+            return seq[len(calls) - 1]
+
+        monkeypatch.setattr(torchrun_util.subprocess, "run", run)
+        r = torchrun_util.torchrun("w.py", 2, {}, ".")
+        assert (len(calls), r.returncode) == (want_calls, want_rc)
+        assert all("--master-addr=127.0.0.1" in c for c in calls)
