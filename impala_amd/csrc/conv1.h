@@ -299,7 +299,9 @@ template <typename T> struct C12FLds {
   // act2 tile rows: bf16 6 x 7 cells (one pad column), fp32 6 x 6 (the LDS budget)
   static constexpr int A2W = sizeof(T) == 2 ? H2 + 1 : H2;
   static constexpr int A2SZ = c3t_fmax<T>() * H2 * A2W * LDA2;
-  static constexpr int ELEMS = c12f_groups<T>() * GSZ + A2SZ;
+  // bf16: the W2 staging rows from group 1's act1 tile on (W1 in group 0's), past the act2 tiles
+  static constexpr int WSTG = sizeof(T) == 2 ? GSZ + IMGSZ + OC2 * (K2 + 2 * VEC) : 0;
+  static constexpr int ELEMS = c12f_groups<T>() * GSZ + A2SZ > WSTG ? c12f_groups<T>() * GSZ + A2SZ : WSTG;
 };
 
 // The kernel body on workgroup `wg` (frames wg*fpw ..) with the LDS passed in
@@ -336,7 +338,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // instead of 1.67x (tools/ldsbank.py)
   constexpr int LDA2 = OC2 + VEC, A2W = C12FLds<T>::A2W, A2F = H2 * A2W;
   constexpr int A2SZ = c3t_fmax<T>() * A2F * LDA2;
-  static_assert(G * GSZ + A2SZ == C12FLds<T>::ELEMS && GSZ == C12FLds<T>::GSZ, "LDS layout");
+  static_assert(G * GSZ + A2SZ <= C12FLds<T>::ELEMS && GSZ == C12FLds<T>::GSZ, "LDS layout");
   T* a2s = smem + G * GSZ;
   const bool tail = c3.act3 != nullptr;
   constexpr int WPG = c12f_wpg<T>(), NTG = 64 * WPG;
@@ -391,12 +393,15 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // (78.9 -> 82.4 us, r03 q32 run)
   V wa2[W2REG ? NKS2 : 1];
   if constexpr (W2REG) {
-    // rows padded by 16 (row step 8 mod 32 dwords): conflict-free b128 fragment reads
+    // rows padded by 16 (row step 8 mod 32 dwords): conflict-free b128 fragment reads.  The rows
+    // sit in the act1 tiles (and past the act2 tiles), not over the images, so each group takes
+    // its first frame into its image while the weights load
     constexpr int LW1 = K1 + 2 * VEC, LW2 = K2 + 2 * VEC, NT = 256 * G;
     constexpr int NV1 = OC1 * K1 / VEC, NV2 = OC2 * K2 / VEC;
-    static_assert(OC1 * LW1 + OC2 * LW2 <= G * GSZ, "weight staging");
-    T* w1s = smem;
-    T* w2s = smem + OC1 * LW1;
+    static_assert(G == 2 && OC1 * LW1 <= GSZ - IMGSZ && GSZ + IMGSZ + OC2 * LW2 <= C12FLds<T>::ELEMS,
+                  "weight staging beside the images");
+    T* w1s = smem + IMGSZ;
+    T* w2s = smem + GSZ + IMGSZ;
     constexpr int NPT = (NV1 + NV2 + NT - 1) / NT;
     V wv[NPT];
 #pragma unroll
@@ -405,6 +410,9 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       if (e < NV1) wv[i] = *reinterpret_cast<const V*>(w1 + (size_t)e * VEC);
       else if (e < NV1 + NV2) wv[i] = *reinterpret_cast<const V*>(w2 + (size_t)(e - NV1) * VEC);
     }
+    // the frame was loaded first: waiting for it leaves the weight loads in flight
+    if (ldr && f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
+    if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, ltid, nv);
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int e = (int)threadIdx.x + i * NT;
@@ -551,11 +559,14 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       }
     }
   };
-  // the group's first frame goes into the image now (the weight staging area is free), and the
-  // second is fetched; every later frame is staged during the previous frame's conv2
-  if (ldr && f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
-  if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, ltid, nv);
-  __syncthreads();
+  // fp32: the group's first frame goes into the image now (the weight staging area is free), and
+  // the second is fetched (bf16 did both during its weight staging); every later frame is staged
+  // during the previous frame's conv2
+  if constexpr (!W2REG) {
+    if (ldr && f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
+    if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, ltid, nv);
+    __syncthreads();
+  }
   for (int it = 0; it < n_it; ++it) {
     const int f = f0 + G * it + grp;
     const bool active = f < f1;
