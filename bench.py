@@ -146,13 +146,7 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA, MI355X_MICROARCH.md
 def synthetic_batch(B, T, A, seed, device):
     """BASELINE.md §3: obs u8 uniform; a ~ U[0,A); r ~ N(0,1) clipped; g = 0.99*(u>0.05);
     mu ~ N(0,1).  Built on the host once, copied to HBM before timing."""
-    rng = np.random.default_rng(seed)
-    obs = rng.integers(0, 256, size=(B, T, 3, 64, 64), dtype=np.uint8)
-    act = rng.integers(0, A, size=(B, T), dtype=np.int64)
-    rew = np.clip(rng.standard_normal((B, T)), -10, 10).astype(np.float32)
-    disc = (0.99 * (rng.random((B, T)) > 0.05)).astype(np.float32)
-    mu = rng.standard_normal((B, T, A)).astype(np.float32)
-    return [torch.from_numpy(x).to(device) for x in (obs, act, rew, disc, mu)]
+    return [torch.from_numpy(x).to(device) for x in _synthetic_np(B, T, A, seed)]
 
 
 def synthetic_ppo_batch(N, A, seed, device):
@@ -244,18 +238,12 @@ def host_cpu_info():
             "budget_rule": "cgroup CPU quota if set, else all physical cores of the affinity set"}
 
 
-def free_port():
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def launch_cmd(nproc, argv, port):
+def launch_cmd(nproc, argv):
     """The torch.distributed.run command `bench.py --gpus N` (N > 1, no WORLD_SIZE) runs as its
-    child: one rank per GPU of this node, rendezvous on 127.0.0.1."""
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-            f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+    child: one rank per GPU of this node; the launcher's c10d store binds a port itself on
+    127.0.0.1 (--standalone), so no port is chosen before the socket that uses it exists."""
+    return [sys.executable, "-m", "torch.distributed.run", "--standalone",
+            "--local-addr=127.0.0.1", f"--nproc-per-node={nproc}",
             os.path.abspath(__file__)] + list(argv)
 
 
@@ -271,7 +259,7 @@ def maybe_launch_ranks(args, argv):
     if args.gpus <= 1:
         return None
     import subprocess
-    cmd = launch_cmd(args.gpus, argv, free_port())
+    cmd = launch_cmd(args.gpus, argv)
     print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
     return subprocess.run(cmd).returncode
 
@@ -337,8 +325,9 @@ class StepClock:
         self.eng.step_clock_end()
 
     def summary(self, digits=4):
-        """-> per-step statistics in ms (call after the region's final synchronize)."""
-        ms = self.eng.step_clock_read()
+        """-> per-step statistics in ms (call after the region's final synchronize); the raw
+        per-step times stay in ``self.ms``."""
+        ms = self.ms = self.eng.step_clock_read()
         out = step_time_stats(ms, digits)
         out["step_clock"] = "device: the step's first kernel stamps s_memrealtime (100 MHz)"
         if self.host:
@@ -368,12 +357,16 @@ def step_time_stats(ms, digits=4):
 
 
 def step_stats(clock, dist, dev):
-    """StepClock.summary(), with the per-step arrays taken as the element-wise max over ranks
-    (the slowest rank sets every step) when data parallel."""
+    """StepClock.summary(), with the per-step times taken as the element-wise max over ranks
+    (the slowest rank sets every step) when data parallel, however many steps there are."""
     s = clock.summary()
-    if dist is None or "step_ms" not in s:
+    if dist is None:
         return s
-    t = torch.tensor(s["step_ms"], device=dev, dtype=torch.float64)
+    t = torch.tensor(clock.ms, device=dev, dtype=torch.float64)
+    n = torch.tensor([t.numel(), -t.numel()], device=dev, dtype=torch.int64)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX)  # every rank sees the same max and min
+    if int(n[0].item()) != -int(n[1].item()):
+        raise RuntimeError("step clock: the ranks stamped different step counts")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     s.update(step_time_stats(t.cpu().numpy()))
     s["over_ranks"] = "max per step"
@@ -446,6 +439,97 @@ def run_host_staged(eng, batch, args, dist, model, world):
                     "it); not `value`"}
 
 
+def synthetic_trajectories(n, T, A, seed):
+    """n trajectories in the reference's replay format ([s u8 (T,3,64,64), a i64 (T,1),
+    r (T,1), g (T,1), mu (T,A)], agents/impala/learning.py:77-80) on the host, with the
+    synthetic distributions of synthetic_batch."""
+    obs, act, rew, disc, mu = (torch.from_numpy(x) for x in _synthetic_np(n, T, A, seed))
+    return [[obs[i], act[i].view(T, 1), rew[i].view(T, 1), disc[i].view(T, 1), mu[i]]
+            for i in range(n)]
+
+
+def _synthetic_np(B, T, A, seed):
+    rng = np.random.default_rng(seed)
+    obs = rng.integers(0, 256, size=(B, T, 3, 64, 64), dtype=np.uint8)
+    act = rng.integers(0, A, size=(B, T), dtype=np.int64)
+    rew = np.clip(rng.standard_normal((B, T)), -10, 10).astype(np.float32)
+    disc = (0.99 * (rng.random((B, T)) > 0.05)).astype(np.float32)
+    mu = rng.standard_normal((B, T, A)).astype(np.float32)
+    return obs, act, rew, disc, mu
+
+
+LOOP_REPLAYS = ("device_replay", "pinned_replay", "host_list_replay")
+
+
+def run_learner_loop(args, dev, headline_ms):
+    """the loop the reference's caller runs, timed end to end --
+    DistributedAgent.train (agents/distributed_agent.py:26-41: prepare, then train_step x K,
+    float(v) of every metric) -> ImpalaLearner.train_step (learning.py:119-138: replay.sample(B),
+    stage, _train_step, push every 4 steps, debug timings) -> a replay of 1000 trajectories
+    (builder.py:30-36), for each replay the learner can be given:
+    * device_replay     DeviceReplayBuffer: HBM ring, device-side gather of the sampled slots;
+    * pinned_replay     PinnedReplayBuffer: page-locked host arena, the sampled rows copied
+                        in place by impala_stage_rows (SDMA, one copy per trajectory);
+    * host_list_replay  ReplayBuffer: the reference's list of pageable CPU tensors, collated
+                        by one torch.stack per field into a page-locked slot, then staged.
+    Each with sync_every 1 (the reference: the metrics read every step) and 100.  Per-step
+    device times from the step clock (each step's first learner kernel stamps it)."""
+    from impala_amd.agent import DistributedAgent
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    from impala_amd.replay import DeviceReplayBuffer, PinnedReplayBuffer, ReplayBuffer
+    B, T, A, cap = args.batch, args.rollout, args.actions, args.loop_capacity
+    trajs = synthetic_trajectories(cap, T, A, 4242)
+    makers = {"device_replay": lambda: DeviceReplayBuffer(cap, T, A, device=dev, seed=5),
+              "pinned_replay": lambda: PinnedReplayBuffer(cap, T, A, seed=5),
+              "host_list_replay": lambda: ReplayBuffer(cap, seed=5)}
+    out = {"steps": args.loop_steps, "capacity": cap, "headline_ms_per_step": headline_ms,
+           "note": "DistributedAgent.train -> ImpalaLearner.train_step -> replay.sample(B) on a "
+                   "replay pre-filled with the capacity's synthetic trajectories; fp32 step; "
+                   "wall ms per train_step (host sync on both sides of the loop), device step "
+                   "clock per step"}
+    for name in LOOP_REPLAYS:
+        rb = makers[name]()
+        for t in trajs:
+            rb.append(t)
+        torch.cuda.synchronize()
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=args.dtype, seed=0)
+        ln = ImpalaLearner(m, rb, batch_size=B, rollout_length=T, learning_starts=cap)
+        rec = {}
+        for sync in (1, 100):
+            ag = DistributedAgent(None, ln, sync_every=sync)
+            ag.train(max(args.warmup, 5))
+            torch.cuda.synchronize()
+            clock = StepClock(ln.engine, args.loop_steps, host=True)
+            step = ln.train_step
+
+            def marked(step=step, clock=clock):
+                clock.mark()
+                return step()
+
+            ln.train_step = marked
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ag.train(args.loop_steps)
+            clock.mark()
+            clock.close()
+            torch.cuda.synchronize()
+            elapsed = time.perf_counter() - t0
+            ln.train_step = step
+            st = clock.summary()
+            st.pop("step_ms", None)
+            st.pop("host_ms", None)
+            ms = elapsed * 1e3 / args.loop_steps
+            rec[f"sync_every_{sync}"] = {
+                "ms_per_step": round(ms, 4), "value": round(B * T / (ms * 1e-3), 1),
+                "ratio_to_headline": round(ms / headline_ms, 3), **st}
+        out[name] = rec
+        ln.engine.close()
+        del ln, m, rb
+        torch.cuda.synchronize()
+    return out
+
+
 PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
                  "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "head_step": "head_step",
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
@@ -460,10 +544,10 @@ PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "c
 SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_loss_chain"}
 
 
-def profiled_traffic(kernel, dtype, names=None, algo="impala"):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
-    same algorithm and dtype (profiles/<tag>/summary.json: "algo" defaults to impala; FETCH_SIZE
-    x2 gfx950 correction + WRITE_SIZE), or None."""
+def profiled_kernel(kernel, dtype, names=None, algo="impala"):
+    """The newest committed rocprofv3 summary record of `kernel` for the same algorithm and
+    dtype (profiles/<tag>/summary.json, "algo" defaulting to impala) that carries PMC HBM bytes
+    -> (record, tag), or (None, None).  Tags sort by round and letter (r05r6 < r06a)."""
     root = os.path.join(HERE, "profiles")
     if not os.path.isdir(root):
         return None, None
@@ -480,8 +564,15 @@ def profiled_traffic(kernel, dtype, names=None, algo="impala"):
             continue
         for k in js.get("kernels", []):
             if k.get("kernel") == (names or PROFILE_NAMES).get(kernel) and k.get("hbm_bytes"):
-                best = (float(k["hbm_bytes"]), tag)
+                best = (k, tag)
     return best if best else (None, None)
+
+
+def profiled_traffic(kernel, dtype, names=None, algo="impala"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+    rec, tag = profiled_kernel(kernel, dtype, names, algo)
+    return (float(rec["hbm_bytes"]), tag) if rec else (None, None)
 
 
 # ----------------------------------------------------------------------------- SAC
@@ -717,6 +808,16 @@ def main():
                     help="N > 1: skip timing / cross-checking every all-reduce arrangement")
     ap.add_argument("--no-host-staged", action="store_true",
                     help="skip the PCIe-inclusive pass (host batches through impala_stage)")
+    ap.add_argument("--no-step-clock", action="store_true",
+                    help="time the headline region without the device step clock (per-step "
+                         "times then unreported): the graph-replay A/B (IMPALA_GRAPH=1)")
+    ap.add_argument("--no-learner-loop", action="store_true",
+                    help="skip the drop-in loop sub-record (DistributedAgent -> ImpalaLearner "
+                         "-> replay, N=1 IMPALA only)")
+    ap.add_argument("--loop-steps", type=int, default=100,
+                    help="train_steps per learner_loop record")
+    ap.add_argument("--loop-capacity", type=int, default=1000,
+                    help="replay capacity of the learner_loop records (builder.py:30-36)")
     ap.add_argument("--algo", default="impala", choices=["impala", "ppo", "sac"],
                     help="ppo: PPO learner step (BASELINE config 4) on --batch transitions "
                          "(default 256, conf/agent/ppo.yaml); sac: SAC learner step (config 5, "
@@ -795,9 +896,12 @@ def main():
     work = kernel_work(2 if args.dtype == "bf16" else 4)
     kernel_us, top = select_kernels(eng, step, work, args)
     settled = settle(step, args.settle_ms, dist, dev)
-    clock = StepClock(eng, args.steps)
+    # --no-step-clock: the headline region without the device step clock, so that
+    # IMPALA_GRAPH=1 runs it as graph replays (an armed clock makes steps launch directly)
+    clock = None if args.no_step_clock else StepClock(eng, args.steps)
     elapsed, _ = timed_steps(eng, step, [], args, dist, dev, clock)  # the headline: no kernel stamps
-    steps_stat = step_stats(clock, dist, dev)
+    steps_stat = step_stats(clock, dist, dev) if clock is not None else {
+        "ms_per_step_median": elapsed * 1e3 / args.steps, "step_clock": "off (--no-step-clock)"}
     # the stamped run for the roofline kernels' live durations, after its own settle: the
     # regions 5-10 ms after a settle ends run 5-7 % slow (tools/region_order.py, profiles/r05host)
     settle(step, args.settle_ms, dist, dev)
@@ -856,6 +960,8 @@ def main():
             out["dp_variants"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     if not args.no_host_staged:
         out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
+    if world == 1 and dist is None and not ppo and not args.no_learner_loop:
+        out["learner_loop"] = run_learner_loop(args, dev, round(ms_step, 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if ppo:
             out["cpu_baseline"] = cpu_baseline_ppo(B, A, args.cpu_seconds,
@@ -1058,9 +1164,19 @@ def kernel_roofline(k, timing, work, frames, dtype, algo):
         bound, unit, achieved, peak = "mfma", "TFLOP/s", flops / t_s / 1e12, PEAK_TFLOPS[dtype]
     else:
         bound, unit, achieved, peak = "hbm", "GB/s", nbytes / t_s / 1e9, PEAK_HBM_GBS
-    traffic, tsrc = profiled_traffic(k, dtype, algo=algo)
+    rec, tsrc = profiled_kernel(k, dtype, algo=algo)
+    traffic = float(rec["hbm_bytes"]) if rec else None
     mix = kernel_mix(k, work, dtype)
     floor = mix_floor_s(mix, frames)
+    # the same fraction from the committed rocprofv3 kernel-trace average (a reader can
+    # reproduce it from profiles/<tag>/summary.json; the profiler's runs clock each launch a
+    # few % longer than the live stamps of an unprofiled run)
+    prof = None
+    if rec and rec.get("avg_us"):
+        pt = float(rec["avg_us"]) * 1e-6
+        ach = (flops / pt / 1e12) if bound == "mfma" else (nbytes / pt / 1e9)
+        prof = {"avg_us": round(float(rec["avg_us"]), 2), "frac": round(ach / peak, 4),
+                "source": f"profiles/{tsrc}/summary.json (rocprofv3 --kernel-trace --stats avg)"}
     return {"bound": bound, "kernel": k, "achieved": round(achieved, 2), "peak": peak,
             "unit": unit, "frac": round(achieved / peak, 4),
             # against the instruction mix the kernel executes (kernel_mix): the time its MFMAs
@@ -1073,6 +1189,7 @@ def kernel_roofline(k, timing, work, frames, dtype, algo):
                                "WRITE_SIZE, bytes per launch)") if tsrc else None,
             "algorithmic": {"flops": flops, "bytes": nbytes},
             "avg_launch_us": round(k_avg_ms * 1e3, 2), "launches": n,
+            "rocprof": prof,
             "timing": "hipExtLaunchKernel start/stop events (kernel begin/end stamps) over the "
                       "timed steps"}
 

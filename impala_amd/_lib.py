@@ -51,12 +51,14 @@ PPO_METRIC_SLOTS = (("train/loss", 0), ("train/entropy", 1), ("train/td", 2), ("
 EXPORTS = (
     "impala_abi_version", "impala_last_error", "impala_config_default", "impala_param_count",
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
-    "impala_set_step", "impala_forward", "impala_train_step", "impala_compute_grads",
+    "impala_set_step", "impala_set_metrics", "impala_forward", "impala_train_step", "impala_compute_grads",
     "impala_apply_update", "impala_compute_grads_part", "impala_grad_bucket_offset",
     "impala_grad_bucket_offset_fc",
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
-    "impala_stage_init", "impala_stage", "impala_stage_wait", "impala_slot_batch",
+    "impala_gather_rows_hidx",
+    "impala_stage_init", "impala_stage", "impala_stage_rows", "impala_stage_wait",
+    "impala_slot_batch",
     "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
     "impala_timer_read_kernel", "impala_dp_unique_id", "impala_dp_init", "impala_dp_train_step",
     "impala_dp_nranks", "impala_step_clock", "impala_step_clock_end",
@@ -90,6 +92,12 @@ class ImpalaConfig(C.Structure):
 
 
 class ImpalaBatch(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("actions", C.c_void_p), ("rewards", C.c_void_p),
+                ("discounts", C.c_void_p), ("behaviour_logits", C.c_void_p)]
+
+
+class ImpalaRows(C.Structure):
+    """impala_rows: per field, the address of an array of B row pointers (host memory)."""
     _fields_ = [("obs", C.c_void_p), ("actions", C.c_void_p), ("rewards", C.c_void_p),
                 ("discounts", C.c_void_p), ("behaviour_logits", C.c_void_p)]
 
@@ -138,6 +146,7 @@ def _declare(lib):
     lib.impala_refresh_weights.argtypes = [_P, _P]
     lib.impala_set_step.argtypes = [_P, C.c_int64, _P]
     lib.impala_set_debug_vtrace.argtypes = [_P, _P]
+    lib.impala_set_metrics.argtypes = [_P, _P]
     lib.impala_forward.argtypes = [_P, _P, C.c_int, _P, _P, _P]
     lib.impala_act.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_uint64, C.c_uint64, _P, _P, _P,
                                _P]
@@ -163,8 +172,11 @@ def _declare(lib):
                                      _P, _P, _P, _P, _P, _P]
     lib.impala_gather_rows.argtypes = [C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_size_t),
                                        C.c_int, _P, C.c_int, _P]
+    lib.impala_gather_rows_hidx.argtypes = [C.POINTER(_P), C.POINTER(_P),
+                                            C.POINTER(C.c_size_t), C.c_int, _P, C.c_int, _P]
     lib.impala_stage_init.argtypes = [_P, C.c_int]
     lib.impala_stage.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int]
+    lib.impala_stage_rows.argtypes = [_P, C.POINTER(ImpalaRows), C.c_int, C.c_int]
     lib.impala_stage_wait.argtypes = [_P, C.c_int]
     lib.impala_slot_batch.argtypes = [_P, C.c_int, _P, C.POINTER(ImpalaBatch)]
     lib.impala_slot_release.argtypes = [_P, C.c_int, _P]

@@ -5,9 +5,9 @@
 call every 100 steps; afterwards the controller's TRAIN episode statistics give
 ``total_samples`` (mean episode length x episode count), logged with
 ``debug/samples_per_second`` and the ``train_envs/*`` means, and returned -- as the reference.
-``eval`` runs the reference's controller protocol.  One optional change: ``sync_every`` > 1
-converts the device metrics to floats only every k steps (the reference's ``float(v)`` per step
-is a host-device sync per step).  The rlmeta controller itself is out of scope: any object with
+``eval`` runs the reference's controller protocol.  The device metrics of a step reach the host
+in one copy (the reference's ``float(v)`` per value is one synchronising copy each), and the
+optional ``sync_every`` > 1 converts them only every k steps, all k in one copy.  The rlmeta controller itself is out of scope: any object with
 its interface (set_phase, reset_phase, count, stats, connect) may be passed in.
 """
 from __future__ import annotations
@@ -15,7 +15,9 @@ from __future__ import annotations
 import enum
 import time
 from collections import defaultdict
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, List, Optional
+
+import torch
 
 from impala_amd.core import Agent, Learner
 
@@ -46,6 +48,41 @@ class StatsDict:
     def dict(self):
         return {k: {"mean": s["sum"] / max(s["count"], 1), "count": s["count"], "min": s["min"],
                     "max": s["max"]} for k, s in self._d.items()}
+
+
+def _host_floats(pending: List[Dict]) -> List[Dict[str, float]]:
+    """``{k: float(v)}`` for every metrics dict of ``pending`` (distributed_agent.py:31), with
+    one device-to-host copy for all of them: device scalars that are views of one metrics
+    vector (ImpalaLearner._train_step) are read from a single stacked copy of those vectors,
+    instead of one synchronising copy per value.  Anything else goes through float(v)."""
+    bases = {}
+    for m in pending:
+        for v in m.values():
+            if isinstance(v, torch.Tensor) and v.dim() == 0 and v._base is not None \
+                    and v.device.type != "cpu":
+                b = v._base
+                if b.dim() == 1 and b.is_contiguous():
+                    bases.setdefault(id(b), b)
+    host = {}
+    if bases:
+        bl = list(bases.values())
+        if len({(b.numel(), b.dtype, b.device) for b in bl}) == 1:
+            rows = torch.stack(bl).cpu().tolist()
+        else:
+            rows = [b.cpu().tolist() for b in bl]
+        host = {id(b): (b, r) for b, r in zip(bl, rows)}
+    out = []
+    for m in pending:
+        d = {}
+        for k, v in m.items():
+            hb = host.get(id(v._base)) if isinstance(v, torch.Tensor) and v._base is not None else None
+            if hb is not None:
+                b, r = hb
+                d[k] = float(r[v.storage_offset() - b.storage_offset()])
+            else:
+                d[k] = float(v)
+        out.append(d)
+    return out
 
 
 class DistributedAgent(Agent):
@@ -82,11 +119,11 @@ class DistributedAgent(Agent):
             metrics = self._learner.train_step()
             pending.append(metrics)
             if len(pending) >= self._sync_every or local_steps == num_steps - 1:
-                for m in pending:
-                    self._stats_dict.extend({k: float(v) for k, v in m.items()})
+                for d in _host_floats(pending):
+                    self._stats_dict.extend(d)
                 pending = []
             if local_steps % 100 == 0:
-                self._log({k: float(v) for k, v in metrics.items()})
+                self._log(_host_floats([metrics])[0])
         if self._controller is None:
             # no actor side to ask: the frames this learner consumed
             total_samples = float(num_steps * getattr(self._learner, "samples_per_step", 0))

@@ -15,7 +15,7 @@ import torch
 from impala_amd.core import Actor, Builder
 from impala_amd.learner import ImpalaAdam, ImpalaLearner
 from impala_amd.model import AtariPPOModel
-from impala_amd.replay import DeviceReplayBuffer, ReplayBuffer
+from impala_amd.replay import DeviceReplayBuffer, PinnedReplayBuffer, ReplayBuffer
 
 
 class ImpalaActor(Actor):
@@ -98,10 +98,13 @@ class ImpalaBuilder(Builder):
     def make_replay(self):  # builder.py:30-36
         cap = self.cfg.agent.replay_buffer_size
         seed = self.cfg.training.seed
-        if self._learner_cfg("replay", "device") == "device" and torch.cuda.is_available():
+        kind = self._learner_cfg("replay", "device")
+        A = self._learner_model.action_dim if self._learner_model is not None else 15
+        if kind == "device" and torch.cuda.is_available():
             dev = self.cfg.distributed.train_device
-            A = self._learner_model.action_dim if self._learner_model is not None else 15
             return DeviceReplayBuffer(cap, self.cfg.agent.rollout_length, A, device=dev, seed=seed)
+        if kind == "pinned":
+            return PinnedReplayBuffer(cap, self.cfg.agent.rollout_length, A, seed=seed)
         return ReplayBuffer(cap, seed=seed)
 
     def make_actor(self, model, rb=None, deterministic: bool = False):  # builder.py:38-40

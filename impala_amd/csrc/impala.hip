@@ -20,6 +20,7 @@
 
 #include "../../include/impala_hip.h"
 #include "head.h"
+#include "hostpool.h"
 #include "kernels.h"
 #include "lnc3.h"
 #include "ops.h"
@@ -209,6 +210,9 @@ struct impala_learner {
     char* mem = nullptr;
     impala_batch dev{};
     hipEvent_t ready = nullptr, done = nullptr;
+    // impala_stage_rows: the slot's page-locked host block (obs, then the four small fields,
+    // impala_stage's layout), allocated at the first row-staging into the slot
+    char* host_blk = nullptr;
   };
   static constexpr int kMaxStageSlots = 8;
   StageSlot ring[kMaxStageSlots];
@@ -223,6 +227,12 @@ struct impala_learner {
   int h2d_pull_threads = 256; // threads per pull workgroup (IMPALA_H2D_THREADS)
   bool h2d_small_pull = true; // SDMA obs: the four small fields in one 1-workgroup pull launch
   hipStream_t h2d = nullptr;  // = h2d_s[0]
+  // impala_stage_rows: 0 = collate the rows into the slot's host block with the thread pool,
+  // then impala_stage's copies; 1 = one SDMA copy per obs row straight from its memory
+  // (IMPALA_STAGE_ROWS=collate|rows; IMPALA_STAGE_THREADS = pool threads).  (The batched copy
+  // API, hipMemcpyBatchAsync, is newer than the HIP runtime torch loads.)
+  int stage_rows_mode = 0;
+  impala_host::HostPool* pool = nullptr;
   // native data-parallel step (impala_dp_*): the library's own RCCL communicator, so the
   // gradient all-reduces are enqueued with no host round trip and no c10d bookkeeping; the FC +
   // heads bucket is all-reduced on dp_stream while the per-frame backward runs
@@ -706,6 +716,7 @@ void free_ring(impala_learner* h) {
     if (s.ready) (void)hipEventDestroy(s.ready);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.mem) (void)hipFree(s.mem);
+    if (s.host_blk) (void)hipHostFree(s.host_blk);
     s = impala_learner::StageSlot{};
   }
   h->n_slots = 0;
@@ -1096,6 +1107,7 @@ int impala_destroy(impala_learner* h) {
     (void)hipStreamDestroy(h->side);
   }
   dp_release(h);
+  delete h->pool;
   if (h->ws) (void)hipFree(h->ws);
   delete h;
   return 0;
@@ -1111,6 +1123,17 @@ int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp
   h->red.grads = grads;
   h->red.metrics = metrics;
   return impala_refresh_weights(h, stream);
+}
+
+int impala_set_metrics(impala_learner* h, float* metrics) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (!metrics) return fail(IMPALA_E_INVALID, "null metrics pointer");
+  if (h->metrics != metrics) {
+    h->metrics = metrics;
+    h->red.metrics = metrics;
+    if (h->use_graph) drop_graphs(h);  // captured launches hold the previous pointer
+  }
+  return 0;
 }
 
 int impala_set_debug_vtrace(impala_learner* h, float* out) {
@@ -1388,24 +1411,59 @@ int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
   });
 }
 
-int impala_gather_rows(const void* const* src, void* const* dst, const size_t* row_bytes,
-                       int nfields, const int64_t* idx, int n, void* stream) {
-  if (nfields < 1 || nfields > 8 || n < 0 || !src || !dst || !row_bytes || (n > 0 && !idx))
+namespace {
+int gather_launch(const void* const* src, void* const* dst, const size_t* row_bytes, int nfields,
+                  const int64_t* idx, const int64_t* host_idx, int n, void* stream) {
+  if (nfields < 1 || nfields > 8 || n < 0 || !src || !dst || !row_bytes ||
+      (n > 0 && !idx && !host_idx))
     return fail(IMPALA_E_INVALID, "bad gather arguments");
   if (n == 0) return 0;
   GatherArgs ga{};
+  int units = 0;
   for (int f = 0; f < nfields; ++f) {
-    if (!src[f] || !dst[f] || row_bytes[f] % 4 != 0)
-      return fail(IMPALA_E_INVALID, "gather: null field or row size not a multiple of 4");
+    if (!src[f] || !dst[f] || row_bytes[f] % 4 != 0 || row_bytes[f] == 0)
+      return fail(IMPALA_E_INVALID, "gather: null field or row size not a positive multiple of 4");
     ga.src[f] = (const char*)src[f];
     ga.dst[f] = (char*)dst[f];
     ga.row_bytes[f] = (long long)row_bytes[f];
+    ga.pieces[f] = (int)((row_bytes[f] + GATHER_PIECE - 1) / GATHER_PIECE);
+    ga.unit0[f] = units;
+    units += ga.pieces[f] * n;
   }
+  ga.unit0[nfields] = units;
   ga.nfields = nfields;
   ga.idx = idx;
   ga.n = n;
-  gather_rows_kernel<<<dim3(n, nfields), 256, 0, (hipStream_t)stream>>>(ga);
+  if (!idx)
+    for (int i = 0; i < n; ++i) ga.hidx[i] = (int)host_idx[i];
+  gather_rows_kernel<<<dim3(units), 256, 0, (hipStream_t)stream>>>(ga);
   CK_LAUNCH("gather_rows");
+  return 0;
+}
+}  // namespace
+
+int impala_gather_rows(const void* const* src, void* const* dst, const size_t* row_bytes,
+                       int nfields, const int64_t* idx, int n, void* stream) {
+  if (n > 0 && !idx) return fail(IMPALA_E_INVALID, "bad gather arguments");
+  return gather_launch(src, dst, row_bytes, nfields, idx, nullptr, n, stream);
+}
+
+int impala_gather_rows_hidx(const void* const* src, void* const* dst, const size_t* row_bytes,
+                            int nfields, const int64_t* host_idx, int n, void* stream) {
+  if (n > 0 && !host_idx) return fail(IMPALA_E_INVALID, "bad gather arguments");
+  for (int i = 0; i < n; ++i)
+    if (host_idx[i] < 0 || host_idx[i] > INT32_MAX)
+      return fail(IMPALA_E_INVALID, "gather: host index out of range");
+  // GATHER_HIDX rows per launch, their indices in the launch's arguments
+  for (int i0 = 0; i0 < n; i0 += GATHER_HIDX) {
+    const int m = std::min(GATHER_HIDX, n - i0);
+    void* d[8];
+    for (int f = 0; f < nfields && f < 8; ++f)
+      d[f] = dst && dst[f] ? (char*)dst[f] + (size_t)i0 * row_bytes[f] : nullptr;
+    if (int r = gather_launch(src, dst ? d : nullptr, row_bytes, nfields, nullptr, host_idx + i0, m,
+                              stream))
+      return r;
+  }
   return 0;
 }
 
@@ -1464,6 +1522,13 @@ int prime_copy_path(impala_learner* h) {
     const hipError_t es = hipStreamSynchronize(h->h2d_s[i]);
     if (e == hipSuccess) e = es;
   }
+  // leave the ring as stage_init's allocation loop does: both events recorded (complete) on
+  // h2d, none referring to work of the private stream about to be destroyed
+  for (int i = 0; i < h->n_slots && e == hipSuccess; ++i) {
+    e = hipEventRecord(h->ring[i].ready, h->h2d);
+    if (e == hipSuccess) e = hipEventRecord(h->ring[i].done, h->h2d);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(h->h2d);
   if (cs) (void)hipStreamDestroy(cs);
   (void)hipHostFree(scratch);
   if (r) return r;
@@ -1480,7 +1545,7 @@ int impala_stage_init(impala_learner* h, int nslots) {
   free_ring(h);
   if (!h->n_h2d) {
     // Default: hipMemcpyAsync (SDMA) of obs split over 2 streams, the four small fields in one
-    // small pull launch.  Beside the fp32 step (tools/h2d_bw.py, r04hs / r04hs2) SDMA on
+    // small pull launch.  Beside the fp32 step (profiles/r04hs: H2D bandwidth A/B) SDMA on
     // 1 / 2 / 4 streams kept 41-43 / 46.4 / 43.9 GB/s, while the pull kernel (8 x 256 threads,
     // 45-48 GB/s alone and the round-1 default) fell to 36 GB/s and slowed the trunk forward it
     // shares CUs with from 63 to 190-210 us (rocprofv3 kernel trace, r04hs).
@@ -1494,6 +1559,8 @@ int impala_stage_init(impala_learner* h, int nslots) {
       h->h2d_pull_threads = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
     h->h2d_small_pull = h->cfg.world_size == 1;
     if (const char* e = std::getenv("IMPALA_H2D_SMALL_PULL")) h->h2d_small_pull = e[0] == '1';
+    if (const char* e = std::getenv("IMPALA_STAGE_ROWS"))
+      h->stage_rows_mode = std::strcmp(e, "rows") == 0 ? 1 : 0;
     int n = h->h2d_pull_wg > 0 ? 1 : 2;
     if (const char* e = std::getenv("IMPALA_H2D_STREAMS")) n = std::atoi(e);
     n = std::max(1, std::min(n, (int)impala_learner::kMaxH2D));
@@ -1614,6 +1681,126 @@ int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
   return 0;
 }
 
+// Row staging (impala_stage_rows): the batch is B trajectories scattered in host memory (the
+// replay's rows), not one collated host batch.  Default (collate): the host's thread pool
+// copies the rows into the slot's page-locked block -- obs, then the four small fields, in
+// impala_stage's layout -- and impala_stage's copies follow (obs over the SDMA streams, the
+// small fields in one pull launch).  One thread's memcpy moves the 15.7 MB of a C2 batch in
+// ~1 ms, over three times the PCIe copy it feeds; the pool's threads share it.  The rows modes
+// instead copy each obs row by SDMA straight from its own memory (runs of adjacent rows merged)
+// and collate only the small fields.
+int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slot) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (slot < 0 || slot >= h->n_slots)
+    return fail(IMPALA_E_INVALID, "slot out of range (impala_stage_init not called?)");
+  const bool ppo = h->cfg.algo == IMPALA_ALGO_PPO;
+  const int B = h->cfg.batch_size;
+  if (!rows || n != B)
+    return fail(IMPALA_E_INVALID, "impala_stage_rows: n must equal the handle's batch_size");
+  if (!rows->obs || !rows->actions || !rows->rewards || (!ppo && !rows->discounts) ||
+      !rows->behaviour_logits)
+    return fail(IMPALA_E_INVALID, "impala_stage_rows: null row array");
+  for (int b = 0; b < n; ++b)
+    if (!rows->obs[b] || !rows->actions[b] || !rows->rewards[b] ||
+        (!ppo && !rows->discounts[b]) || !rows->behaviour_logits[b])
+      return fail(IMPALA_E_INVALID, "impala_stage_rows: null row pointer");
+  CK(hipSetDevice(h->device));
+  auto& s = h->ring[slot];
+  const size_t T = (size_t)h->cfg.rollout_length, N = (size_t)h->N, A = (size_t)h->A;
+  const size_t rb[5] = {T * 3 * 64 * 64, T * 8, T * 4, T * 4, T * A * 4};
+  // host block layout: obs | actions | rewards | discounts | behaviour logits (256-B aligned)
+  size_t off[6];
+  off[0] = 0;
+  for (int f = 0; f < 5; ++f) off[f + 1] = off[f] + ((N * rb[f] / T + 255) & ~(size_t)255);
+  if (!s.host_blk) {
+    void* p = nullptr;
+    CK(hipHostMalloc(&p, off[5], hipHostMallocMapped | hipHostMallocPortable));
+    s.host_blk = (char*)p;
+  }
+  // the slot's previous copies (out of its host block too) have finished before it is rewritten
+  CK(hipEventSynchronize(s.ready));
+  const void* const* src[5] = {rows->obs, rows->actions, rows->rewards, rows->discounts,
+                               rows->behaviour_logits};
+  char* hb = s.host_blk;
+  const bool collate = h->stage_rows_mode == 0;
+  // host copies: obs rows in 64 KB pieces (collate mode), each small field as one task
+  constexpr size_t kPiece = 65536;
+  const int per_row = collate ? (int)((rb[0] + kPiece - 1) / kPiece) : 0;
+  const int n_obs_tasks = per_row * n;
+  auto task = [&](int i) {
+    if (i < n_obs_tasks) {
+      const int b = i / per_row;
+      const size_t o = (size_t)(i - b * per_row) * kPiece, len = std::min(kPiece, rb[0] - o);
+      impala_host::copy_stream(hb + (size_t)b * rb[0] + o, (const char*)src[0][b] + o, len);
+      return;
+    }
+    const int f = 1 + (i - n_obs_tasks);
+    if (f == 3 && ppo) return;
+    for (int b = 0; b < n; ++b) std::memcpy(hb + off[f] + (size_t)b * rb[f], src[f][b], rb[f]);
+  };
+  const int ntasks = n_obs_tasks + 4;
+  if (collate && !h->pool) {
+    int nt = 7;
+    if (const char* e = std::getenv("IMPALA_STAGE_THREADS")) nt = std::max(0, std::atoi(e) - 1);
+    h->pool = new (std::nothrow) impala_host::HostPool(nt);
+    if (!h->pool) return fail(IMPALA_E_STATE, "impala_stage_rows: thread pool");
+  }
+  if (h->pool && collate) {
+    h->pool->run(ntasks, task);
+  } else {
+    for (int i = 0; i < ntasks; ++i) task(i);
+  }
+  if (collate) {
+    const impala_batch hbat{(const uint8_t*)(hb + off[0]), (const int64_t*)(hb + off[1]),
+                            (const float*)(hb + off[2]),
+                            ppo ? nullptr : (const float*)(hb + off[3]), (const float*)(hb + off[4])};
+    return impala_stage(h, &hbat, slot);
+  }
+  const int ns = h->n_h2d;
+  for (int i = 0; i < ns; ++i)  // the steps that read the slot have run
+    CK(hipStreamWaitEvent(h->h2d_s[i], s.done, 0));
+  void* dst[5] = {(void*)s.dev.obs, (void*)s.dev.actions, (void*)s.dev.rewards,
+                  (void*)s.dev.discounts, (void*)s.dev.behaviour_logits};
+  void* hb_dev = nullptr;
+  if (hipHostGetDevicePointer(&hb_dev, hb, 0) != hipSuccess || (((uintptr_t)hb_dev) & 15) != 0) {
+    (void)hipGetLastError();
+    hb_dev = nullptr;
+  }
+  if (hb_dev && (h->h2d_small_pull || h->h2d_pull_wg > 0)) {
+    PullArgs pa{};
+    for (int f = 1; f < 5; ++f) {
+      if (f == 3 && ppo) continue;
+      pa.src[pa.nf] = (const char*)hb_dev + off[f];
+      pa.dst[pa.nf] = (char*)dst[f];
+      pa.bytes[pa.nf] = (long long)(N * rb[f] / T);
+      ++pa.nf;
+    }
+    h2d_pull_kernel<<<8, 256, 0, h->h2d>>>(pa);
+    CK_LAUNCH("h2d_pull");
+  } else {
+    for (int f = 1; f < 5; ++f)
+      if (!(f == 3 && ppo))
+        CK(hipMemcpyAsync(dst[f], hb + off[f], N * rb[f] / T, hipMemcpyDefault, h->h2d));
+  }
+  // obs rows: runs of adjacent source rows become one copy, dealt round-robin over the streams
+  const char* const* ob = reinterpret_cast<const char* const*>(rows->obs);
+  int k = 0;
+  for (int b = 0; b < n;) {
+    int e = b + 1;
+    while (e < n && ob[e] == ob[e - 1] + rb[0]) ++e;
+    char* d = (char*)dst[0] + (size_t)b * rb[0];
+    const size_t len = (size_t)(e - b) * rb[0];
+    CK(hipMemcpyAsync(d, ob[b], len, hipMemcpyDefault, h->h2d_s[k++ % ns]));
+    b = e;
+  }
+  for (int i = 1; i < ns; ++i) {
+    CK(hipEventRecord(h->h2d_join[i], h->h2d_s[i]));
+    CK(hipStreamWaitEvent(h->h2d, h->h2d_join[i], 0));
+  }
+  CK(hipEventRecord(s.ready, h->h2d));
+  return 0;
+}
+
 int impala_stage_wait(impala_learner* h, int slot) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (slot < 0 || slot >= h->n_slots) return fail(IMPALA_E_INVALID, "slot out of range");
@@ -1692,6 +1879,8 @@ int impala_timer_read_kernel(impala_learner* h, int kernel_id, float* total_ms, 
 int impala_step_clock(impala_learner* h, unsigned long long* stamps, int n) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (n < 0 || (n > 0 && !stamps)) return fail(IMPALA_E_INVALID, "bad step clock buffer / count");
+  if (n > 0 && h->fwd_chain)  // the A/B forward-chain launch takes no stamp
+    return fail(IMPALA_E_UNSUPPORTED, "the step clock does not stamp the IMPALA_FWD_CHAIN forward");
   h->clock_buf = n > 0 ? stamps : nullptr;
   h->clock_n = n;
   h->clock_i = 0;

@@ -312,6 +312,7 @@ DEV void finalize_loss_metrics(const float* part, int nparts, int B, int T, floa
   metrics[3] = pg;
   metrics[4] = s[3] * c_ent;
   metrics[5] = s[4] * c_ent;
+  metrics[8] = 0.f;  // (PPO's train/target slot) every slot is written each step
 }
 
 __global__ void finalize_loss_kernel(const float* part, int nparts, int B, int T, float ent_coef,
@@ -1164,13 +1165,21 @@ __global__ __launch_bounds__(256) void act_heads_kernel(const float* __restrict_
 // Replay gather: dst_f[i] = src_f[idx[i]] for up to 8 fields of fixed row size (bytes, multiple
 // of 4).  One workgroup per (row, field); 16-byte vector copies for the aligned bulk.
 // =========================================================================================
+// A row is copied in pieces of GATHER_PIECE bytes, one workgroup per (field, row, piece), so a
+// 245 KB obs row is spread over 15 workgroups.  Indices come from device memory (idx) or, for
+// up to GATHER_HIDX rows, from the launch's own arguments (hidx: no index upload).
+constexpr int GATHER_PIECE = 16384;
+constexpr int GATHER_HIDX = 256;
 struct GatherArgs {
   const char* src[8];
   char* dst[8];
   long long row_bytes[8];
+  int pieces[8];     // pieces per row of each field
+  int unit0[9];      // first workgroup of each field: unit0[f] + row * pieces[f] + piece
   int nfields;
   const int64_t* idx;
   int n;
+  int hidx[GATHER_HIDX];
 };
 
 // Host -> HBM pull copy for the staging ring (impala_stage, IMPALA_H2D_KERNEL=1): a few
@@ -1221,18 +1230,25 @@ __global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* __r
 }
 
 __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
-  const int i = blockIdx.x, f = blockIdx.y;
-  if (i >= a.n || f >= a.nfields) return;
+  const int u = blockIdx.x;
+  int f = 0;
+  while (f + 1 < a.nfields && u >= a.unit0[f + 1]) ++f;
+  const int r = u - a.unit0[f];
+  const int i = r / a.pieces[f], piece = r - i * a.pieces[f];
+  if (f >= a.nfields || i >= a.n) return;
   const long long rb = a.row_bytes[f];
-  const char* s = a.src[f] + (size_t)a.idx[i] * rb;
-  char* d = a.dst[f] + (size_t)i * rb;
-  const bool al16 = ((((uintptr_t)s) | ((uintptr_t)d) | (uintptr_t)rb) & 15) == 0;
+  const long long o0 = (long long)piece * GATHER_PIECE;
+  const long long len = min((long long)GATHER_PIECE, rb - o0);
+  const long long row = a.idx ? a.idx[i] : a.hidx[i];
+  const char* s = a.src[f] + (size_t)row * rb + o0;
+  char* d = a.dst[f] + (size_t)i * rb + o0;
+  const bool al16 = ((((uintptr_t)s) | ((uintptr_t)d) | (uintptr_t)len) & 15) == 0;
   if (al16) {
-    const long long nv = rb >> 4;
+    const long long nv = len >> 4;
     for (long long v = threadIdx.x; v < nv; v += 256)
       reinterpret_cast<f32x4*>(d)[v] = reinterpret_cast<const f32x4*>(s)[v];
   } else {
-    const long long nw = rb >> 2;
+    const long long nw = len >> 2;
     for (long long v = threadIdx.x; v < nw; v += 256)
       reinterpret_cast<float*>(d)[v] = reinterpret_cast<const float*>(s)[v];
   }

@@ -26,18 +26,21 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("WORLD_SIZE", "1")))
 
 
-def init_process_group(backend: str = "nccl"):
+def init_process_group(backend: str = "nccl", init_method: str | None = None):
     """Initialise the default group from the environment (MASTER_ADDR=127.0.0.1 on one node).
-    ``nccl`` is RCCL on ROCm; ``gloo`` for CPU tests."""
+    ``nccl`` is RCCL on ROCm; ``gloo`` for CPU tests.  ``init_method`` (e.g. a ``file://``
+    store) replaces the MASTER_ADDR / MASTER_PORT rendezvous."""
     import torch.distributed as dist
     rank, local_rank, world = env_rank()
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if init_method is None:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {} if init_method is None else {"init_method": init_method}
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local_rank))
+                                device_id=torch.device("cuda", local_rank), **kw)
     else:
-        dist.init_process_group(backend, rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return dist.group.WORLD
 
 
@@ -61,7 +64,7 @@ def compute_grads_allreduced(engine, batch, flat_grad: torch.Tensor, group=None,
     collectives before it continues (apply_update).
 
     One bucket (default): the whole backward, then one all-reduce of the flat fp32 gradient
-    (1.38 MB).  Measured at world size 1 (RCCL group of one, `tools/dp_hosttime.py`,
+    (1.38 MB).  Measured at world size 1 (RCCL group of one, host-time A/B recorded in
     `profiles/r02j/dp_hosttime.txt`): 114-130 us per step (bench: 0.1132 ms) against 105 us
     for the fused single-replica step, while every bucketed arrangement costs more than the
     overlap it can buy: each extra all-reduce adds a pair of cross-stream dependencies (~12 us of GPU idle

@@ -12,7 +12,7 @@ from typing import Optional, Sequence, Tuple
 import torch
 
 from impala_amd import _lib
-from impala_amd._lib import ImpalaBatch, ImpalaConfig, check, ptr, stream_ptr
+from impala_amd._lib import ImpalaBatch, ImpalaConfig, ImpalaRows, check, ptr, stream_ptr
 
 DTYPES = {"fp32": _lib.IMPALA_DTYPE_F32, "f32": _lib.IMPALA_DTYPE_F32,
           "float32": _lib.IMPALA_DTYPE_F32, "bf16": _lib.IMPALA_DTYPE_BF16,
@@ -105,6 +105,16 @@ class Engine:
     def _sync_weights(self, stream=None):
         if self._version != self.model._version:
             self.refresh_weights(stream)
+
+    def bind_metrics(self, metrics: torch.Tensor):
+        """The following steps write their metrics into `metrics` (a device float32 vector of
+        NUM_METRICS, impala_set_metrics; no device work), which becomes ``self.metrics``."""
+        if metrics.dtype != torch.float32 or metrics.device != self.device or \
+                metrics.numel() < _lib.NUM_METRICS or not metrics.is_contiguous():
+            raise ValueError(f"metrics must be a contiguous float32 vector of >= "
+                             f"{_lib.NUM_METRICS} on {self.device}")
+        check(_lib.lib().impala_set_metrics(self._h, ptr(metrics)), "impala_set_metrics")
+        self.metrics = metrics
 
     def set_step(self, step: int, stream=None):
         check(_lib.lib().impala_set_step(self._h, int(step), stream_ptr(stream)), "impala_set_step")
@@ -313,6 +323,22 @@ class Engine:
         check(_lib.lib().impala_stage(self._h, C.byref(b), int(slot)), "impala_stage")
         self._staged[slot] = host_batch  # the copies read these until stage_wait(slot)
 
+    def stage_rows(self, slot: int, row_ptrs):
+        """Enqueue the H2D copies of B trajectories that are NOT collated (impala_stage_rows):
+        ``row_ptrs`` = five arrays of B host addresses (numpy uint64, or sequences of ints),
+        trajectory b's obs / actions / rewards / discounts / behaviour-logits rows (discounts
+        None on PPO handles).  The rows must stay unchanged until stage_wait(slot)."""
+        import numpy as np
+        arrs = [None if p is None else np.ascontiguousarray(p, dtype=np.uint64) for p in row_ptrs]
+        B = self.batch_size
+        for a in arrs:
+            if a is not None and a.shape != (B,):
+                raise ValueError(f"row pointer arrays must hold {B} addresses")
+        rows = ImpalaRows(*[0 if a is None else a.ctypes.data for a in arrs])
+        check(_lib.lib().impala_stage_rows(self._h, C.byref(rows), B, int(slot)),
+              "impala_stage_rows")
+        self._staged[slot] = arrs
+
     def stage_wait(self, slot: int):
         """Block until the copies into `slot` are done (its host batch may be reused)."""
         check(_lib.lib().impala_stage_wait(self._h, int(slot)), "impala_stage_wait")
@@ -361,6 +387,7 @@ class Engine:
         the device's 100 MHz clock as it starts (impala_step_clock); nothing is enqueued
         between the steps."""
         self._clock = torch.zeros(int(n) + 1, dtype=torch.int64, device=self.device)
+        self._clock_steps = None  # set by step_clock_end for this region
         check(_lib.lib().impala_step_clock(self._h, ptr(self._clock), int(n)), "impala_step_clock")
 
     def step_clock_end(self, stream=None):
@@ -373,7 +400,10 @@ class Engine:
 
     def step_clock_read(self):
         """-> the per-step device times in ms of the last clocked region (a host sync)."""
+        if getattr(self, "_clock", None) is None or getattr(self, "_clock_steps", None) is None:
+            raise RuntimeError("step_clock_read: no clocked region closed by step_clock_end")
         st = self._clock[: self._clock_steps + 1].cpu().tolist()
+        self._clock_steps = None
         self._clock = None
         return [(b - a) * 1e-5 for a, b in zip(st, st[1:])]  # 10 ns ticks -> ms
 
@@ -449,14 +479,27 @@ def ppo_loss_head(logits, values, actions, targets, mu, entropy_coeff=0.01, clip
 
 def gather_rollouts(fields, idx, stream=None):
     """HIP gather of replay rows: ``[f[idx] for f in fields]`` for device tensors whose first
-    dim indexes slots (impala_gather_rows)."""
-    n = int(idx.numel())
+    dim indexes slots.  ``idx``: a device tensor (impala_gather_rows), or host indices -- a
+    numpy array or CPU tensor -- passed in the launch arguments (impala_gather_rows_hidx: no
+    index upload on the stream)."""
+    import numpy as np
+    host = not (isinstance(idx, torch.Tensor) and idx.device.type != "cpu")
+    if host:
+        idx = np.ascontiguousarray(idx.numpy() if isinstance(idx, torch.Tensor) else idx,
+                                   dtype=np.int64)
+        n = int(idx.size)
+    else:
+        idx = idx.to(torch.int64).contiguous()
+        n = int(idx.numel())
     outs = [torch.empty((n,) + tuple(f.shape[1:]), dtype=f.dtype, device=f.device) for f in fields]
     k = len(fields)
     src = (C.c_void_p * k)(*[ptr(f) for f in fields])
     dst = (C.c_void_p * k)(*[ptr(o) for o in outs])
     rb = (C.c_size_t * k)(*[f[0].numel() * f.element_size() for f in fields])
-    idx = idx.to(torch.int64).contiguous()
-    check(_lib.lib().impala_gather_rows(src, dst, rb, k, ptr(idx), n, stream_ptr(stream)),
-          "impala_gather_rows")
+    if host:
+        check(_lib.lib().impala_gather_rows_hidx(src, dst, rb, k, idx.ctypes.data, n,
+                                                 stream_ptr(stream)), "impala_gather_rows_hidx")
+    else:
+        check(_lib.lib().impala_gather_rows(src, dst, rb, k, ptr(idx), n, stream_ptr(stream)),
+              "impala_gather_rows")
     return tuple(outs)

@@ -7,6 +7,7 @@ all-reduce of the flat gradient + ``impala_apply_update``.
 """
 from __future__ import annotations
 
+import functools
 import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Sequence, Tuple
@@ -122,17 +123,36 @@ class ImpalaLearner(Learner):
     def prepare(self):  # learning.py:116-117
         self._replay_buffer.warm_up(self._learning_starts)
 
+    def _row_key(self):
+        """The (dtypes, byte sizes) of one trajectory's fields impala_stage_rows copies: obs u8
+        (T,3,64,64), actions i64 (T,1), rewards / discounts f32 (T,1), logits f32 (T,A)."""
+        T, A = self._rollout_length, self._engine.num_actions
+        return ((torch.uint8, torch.int64, torch.float32, torch.float32, torch.float32),
+                (T * 3 * 64 * 64, T * 8, T * 4, T * 4, T * A * 4))
+
     def _stage_host(self, batch):
-        """learning.py:121-123,142 for host trajectories: collate into this step's page-locked
-        ring buffers and stage them through the library's H2D ring (impala_stage, two slots:
-        the copies of step k+1 wait only for the step that last read the slot).
+        """learning.py:121-123,142 for host trajectories, staged through the library's H2D ring
+        (two slots: the copies of step k+1 wait only for the step that last read the slot).
+        Rows of a page-locked replay arena (PinnedReplayBuffer: the batch carries their
+        addresses) are copied by impala_stage_rows straight from the arena, with no host copy
+        of the frames; any other list of trajectories is collated into this slot's page-locked
+        buffers (one torch.stack per field) and staged by impala_stage.
         -> (slot, the slot's device ImpalaBatch)."""
         e = self._engine
         if getattr(e, "n_slots", 0) == 0:
             e.stage_init(2)
             self._host_bufs = [None] * e.n_slots
+            self._row_batches = [None] * e.n_slots
         self._slot = slot = (getattr(self, "_slot", -1) + 1) % e.n_slots
-        e.stage_wait(slot)  # the previous copies out of this slot's host buffers are done
+        e.stage_wait(slot)  # the previous copies out of this slot's host memory are done
+        rows = getattr(batch, "row_ptrs", None)
+        if rows is not None and len(batch) == e.batch_size and batch.row_key == self._row_key():
+            e.stage_rows(slot, rows)
+            # the rows stay alive, and the replay does not overwrite them, until their copies
+            # are done (impala_stage_rows' SDMA-per-row modes read them after it returns)
+            self._row_batches[slot] = batch
+            batch.fence = functools.partial(e.stage_wait, slot)
+            return slot, e.slot_batch(slot)
         if self._host_bufs[slot] is None:
             B, T, A = self._batch_size, self._rollout_length, e.num_actions
             pin = torch.cuda.is_available()
@@ -145,9 +165,13 @@ class ImpalaLearner(Learner):
         bufs = self._host_bufs[slot]
         if len(batch) != bufs[0].shape[0]:
             raise ValueError(f"replay returned {len(batch)} trajectories, expected {bufs[0].shape[0]}")
-        for i, item in enumerate(batch):
-            for j, buf in enumerate(bufs):
-                buf[i].copy_(item[j].reshape(buf.shape[1:]))
+        for j, buf in enumerate(bufs):
+            xs = [item[j] for item in batch]
+            try:  # one collate per field (learning.py:142 torch.stack), into the pinned buffer
+                torch.stack(xs, out=buf.view((len(xs),) + tuple(xs[0].shape)))
+            except (RuntimeError, TypeError):  # other dtype / shape spelling: per trajectory
+                for i, x in enumerate(xs):
+                    buf[i].copy_(x.reshape(buf.shape[1:]))
         e.stage(slot, *bufs)
         return slot, e.slot_batch(slot)
 
@@ -185,6 +209,10 @@ class ImpalaLearner(Learner):
 
     def _train_step(self, batch) -> Dict[str, torch.Tensor]:  # learning.py:140-177
         e = self._engine
+        # this step's metrics go to a vector of its own, which the returned values are views
+        # of (impala_set_metrics: no device copy after the step)
+        m = torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device)
+        e.bind_metrics(m)
         if self._world_size == 1:
             e.train_step(*batch)
         else:
@@ -200,8 +228,9 @@ class ImpalaLearner(Learner):
             else:
                 compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
                 e.apply_update()
-        m = e.metrics.clone()  # device scalars; float(v) synchronises lazily
-        return {name: m[i] for i, name in enumerate(_lib.METRIC_NAMES)}
+        # device scalars, views of the step's metrics vector: float(v) synchronises lazily, and
+        # DistributedAgent moves all of a step's values with one copy (agent._host_floats)
+        return dict(zip(_lib.METRIC_NAMES, m.unbind(0)))
 
     # ---------------------------------------------------------------- checkpoint
     def optimizer_state(self) -> dict:

@@ -131,6 +131,9 @@ class PPOLearner(Learner):
 
     def _train_step(self, batch) -> Dict[str, torch.Tensor]:  # learning.py:130-143
         e = self._engine
+        # this step's metrics vector (impala_set_metrics), which the returned values are views of
+        m = torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device)
+        e.bind_metrics(m)
         if self._world_size == 1:
             e.train_step(*batch)
         else:
@@ -146,5 +149,5 @@ class PPOLearner(Learner):
             else:
                 compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
                 e.apply_update()
-        m = e.metrics.clone()  # device scalars; float(v) synchronises lazily
-        return {name: m[i] for name, i in _lib.PPO_METRIC_SLOTS}
+        v = m.unbind(0)  # device scalars; float(v) synchronises lazily
+        return {name: v[i] for name, i in _lib.PPO_METRIC_SLOTS}

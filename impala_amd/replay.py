@@ -5,9 +5,13 @@ UniformSampler())``; actors ``async_append`` one trajectory ``[s, a, r, discount
 (``agents/impala/learning.py:71-80``); the learner calls ``warm_up(learning_starts)`` and
 ``sample(batch_size) -> (keys, batch, probs)`` (``learning.py:116-121``).
 
-Two implementations with that interface:
+Three implementations with that interface:
 
 * ``ReplayBuffer``        host memory, returns the reference's list-of-trajectories batch.
+* ``PinnedReplayBuffer``  the same list-of-trajectories batch, its rows views into one
+  page-locked host arena; the batch also carries the rows' addresses, so the learner stages
+  them with ``impala_stage_rows`` (one SDMA copy per trajectory straight from the arena into
+  the device slot, no host collate of the 15.7 MB of frames).
 * ``DeviceReplayBuffer``  MI355X-first: the circular store lives in HBM (1000 x 247 KB =
   247 MB of 288 GB); an appended trajectory is written into a pinned-host staging ring and
   copied to its HBM slot with an async H2D on a side stream, so each trajectory crosses PCIe
@@ -24,12 +28,37 @@ import numpy as np
 import torch
 
 
+def _row_info(item):
+    """(host addresses, (dtypes, byte sizes)) of a trajectory's fields when every field is a
+    contiguous CPU tensor, else None: what impala_stage_rows needs to read the rows in place."""
+    if not all(isinstance(t, torch.Tensor) and t.device.type == "cpu" and t.is_contiguous()
+               for t in item):
+        return None
+    return ([t.data_ptr() for t in item],
+            (tuple(t.dtype for t in item), tuple(t.numel() * t.element_size() for t in item)))
+
+
+class RowBatch(list):
+    """The list of B trajectories a replay's ``sample`` returns (the reference's batch format),
+    plus, when every sampled trajectory's fields are contiguous host tensors of one layout,
+    ``row_ptrs`` -- per field the B rows' host addresses (numpy uint64) -- and ``row_key`` --
+    the fields' (dtypes, byte sizes) -- for ``impala_stage_rows``.  A consumer whose copies read
+    the rows after it returns sets ``fence`` to a callable that returns once they are done; the
+    replay calls it before overwriting one of the rows."""
+    row_ptrs = None
+    row_key = None
+    fence = None
+
+
 class ReplayBuffer:
     """CircularBuffer + UniformSampler semantics on the host (reference-compatible)."""
 
     def __init__(self, capacity: int = 1000, seed: Optional[int] = None):
         self.capacity = int(capacity)
         self._data: List[Optional[list]] = [None] * self.capacity
+        # per slot: the fields' host addresses and layout key (_row_info), when known
+        self._ptr_tab = np.zeros((self.capacity, 5), dtype=np.uint64)
+        self._row_keys: List[Optional[tuple]] = [None] * self.capacity
         self._keys = np.zeros(self.capacity, dtype=np.int64)
         self._next_key = 0
         self._size = 0
@@ -47,6 +76,12 @@ class ReplayBuffer:
         with self._cv:
             slot = self._cursor
             self._data[slot] = list(item)
+            info = _row_info(self._data[slot]) if len(item) == 5 else None
+            if info is None:
+                self._row_keys[slot] = None
+            else:
+                self._ptr_tab[slot] = info[0]
+                self._row_keys[slot] = info[1]
             key = self._next_key
             self._keys[slot] = key
             self._next_key += 1
@@ -83,18 +118,91 @@ class ReplayBuffer:
     def sample(self, batch_size: int):
         with self._cv:
             idx = self._indices(batch_size)
-            batch = [self._data[i] for i in idx]
+            batch = RowBatch(self._data[i] for i in idx)
+            rk = {self._row_keys[i] for i in idx}
+            if len(rk) == 1 and None not in rk:
+                batch.row_key = rk.pop()
+                batch.row_ptrs = tuple(np.ascontiguousarray(self._ptr_tab[idx, f]) for f in range(5))
             keys = self._keys[idx].copy()
         probs = np.full(batch_size, 1.0 / self._size)
         return keys, batch, probs
 
 
+class PinnedReplayBuffer(ReplayBuffer):
+    """Host circular store in one page-locked arena (1000 x 247 KB at C2), CircularBuffer +
+    UniformSampler semantics (``agents/impala/builder.py:30-36``).  ``append`` copies the
+    trajectory into its arena slot once; ``sample`` returns the reference's list of B
+    trajectories -- views into the arena, valid until the slot is overwritten (clone to keep
+    one) -- as a ``RowBatch`` whose ``row_ptrs`` let the learner's H2D copies read the rows in
+    place."""
+
+    _READERS_MAX = 8  # batches whose staged copies are tracked (older ones are fenced)
+
+    def __init__(self, capacity: int = 1000, rollout_length: int = 20, num_actions: int = 15,
+                 seed: Optional[int] = None):
+        super().__init__(capacity, seed)
+        C, T, A = self.capacity, int(rollout_length), int(num_actions)
+        self.T, self.A = T, A
+        pin = torch.cuda.is_available()
+        self.fields = (torch.empty(C, T, 3, 64, 64, dtype=torch.uint8, pin_memory=pin),
+                       torch.zeros(C, T, 1, dtype=torch.int64, pin_memory=pin),
+                       torch.zeros(C, T, 1, dtype=torch.float32, pin_memory=pin),
+                       torch.zeros(C, T, 1, dtype=torch.float32, pin_memory=pin),
+                       torch.zeros(C, T, A, dtype=torch.float32, pin_memory=pin))
+        self._base = np.array([f.data_ptr() for f in self.fields], dtype=np.uint64)
+        self._row_bytes = np.array([f[0].numel() * f.element_size() for f in self.fields],
+                                   dtype=np.uint64)
+        self._row_key = (tuple(f.dtype for f in self.fields),
+                         tuple(int(b) for b in self._row_bytes))
+        self._readers: List[Tuple[set, RowBatch]] = []
+
+    def _fence_readers(self, slot: Optional[int] = None) -> None:
+        """Wait for the staged copies of every tracked batch that reads arena row `slot` (all
+        tracked batches beyond the newest _READERS_MAX when `slot` is None)."""
+        keep = []
+        for i, (rows, b) in enumerate(self._readers):
+            old = slot is None and i < len(self._readers) - self._READERS_MAX
+            if old or (slot is not None and slot in rows):
+                if b.fence is not None:
+                    b.fence()
+            else:
+                keep.append((rows, b))
+        self._readers = keep
+
+    def append(self, item: Sequence[torch.Tensor]) -> int:
+        with self._cv:
+            slot = self._cursor
+            self._fence_readers(slot)
+            for f, x in zip(self.fields, item):
+                f[slot].copy_(x.reshape(f.shape[1:]))
+            self._data[slot] = [f[slot] for f in self.fields]
+            self._row_keys[slot] = self._row_key
+            key = self._next_key
+            self._keys[slot] = key
+            self._next_key += 1
+            self._cursor = (slot + 1) % self.capacity
+            self._size = min(self._size + 1, self.capacity)
+            self._cv.notify_all()
+            return key
+
+    def sample(self, batch_size: int):
+        with self._cv:
+            idx = self._indices(batch_size)
+            batch = RowBatch(self._data[i] for i in idx)
+            u = idx.astype(np.uint64)
+            batch.row_ptrs = tuple(self._base[f] + u * self._row_bytes[f] for f in range(5))
+            batch.row_key = self._row_key
+            keys = self._keys[idx].copy()
+            self._readers.append((set(idx.tolist()), batch))
+            if len(self._readers) > self._READERS_MAX:
+                self._fence_readers(None)
+            size = self._size
+        probs = np.full(batch_size, 1.0 / size)
+        return keys, batch, probs
+
+
 class DeviceReplayBuffer(ReplayBuffer):
     """HBM-resident circular rollout store with pinned-host staging (see module doc)."""
-
-    # the most entries the page-locked index ring grows to (_indices_to_device) before sample()
-    # waits for the oldest one's copy
-    _IDX_RING_MAX = 64
 
     def __init__(self, capacity: int = 1000, rollout_length: int = 20, num_actions: int = 15,
                  device="cuda", seed: Optional[int] = None, staging_slots: int = 64):
@@ -117,17 +225,11 @@ class DeviceReplayBuffer(ReplayBuffer):
         self._st_next = 0
         self._stream = torch.cuda.Stream(device=d)
         self._pending: List[torch.cuda.Event] = []
-        # the last gather enqueued by sample(): an append must not overwrite a slot that a
-        # queued gather still reads (gathers run in order on the learner's stream, so waiting
-        # for the latest one covers every earlier read)
-        self._last_read: Optional[torch.cuda.Event] = None
-        # page-locked ring for the sampled slot indices: their H2D is a true asynchronous copy
-        # (from pageable memory it would wait behind the learner stream's queued work while
-        # sample() holds the lock); a ring entry is reused after its copy has run.  It starts
-        # at 4 entries and grows when the learner's stream runs further ahead than that
-        self._idx_buf: List[Optional[torch.Tensor]] = [None] * 4
-        self._idx_ev: List[Optional[torch.cuda.Event]] = [None] * 4
-        self._idx_next = 0
+        # the stream of the last gather enqueued by sample(): an append must not overwrite a
+        # slot that a queued gather still reads, so its copy waits for an event recorded on that
+        # stream at append time (it follows every gather enqueued so far; recorded only when an
+        # append comes, so a learner sampling with no appends gets nothing but its gathers)
+        self._read_stream = None
 
     def append(self, item: Sequence[torch.Tensor]) -> int:
         s, a, r, g, mu = item
@@ -146,8 +248,10 @@ class DeviceReplayBuffer(ReplayBuffer):
             sm[:, 3:].copy_(mu.reshape(T, self.A))
             slot = self._cursor
             with torch.cuda.stream(self._stream):
-                if self._last_read is not None:
-                    self._stream.wait_event(self._last_read)
+                if self._read_stream is not None:
+                    read = torch.cuda.Event()
+                    read.record(self._read_stream)
+                    self._stream.wait_event(read)
                 self.obs[slot].copy_(self._st_obs[j], non_blocking=True)
                 self.act[slot].copy_(self._st_act[j], non_blocking=True)
                 small = sm.to(self.device, non_blocking=True)
@@ -166,45 +270,17 @@ class DeviceReplayBuffer(ReplayBuffer):
             self._cv.notify_all()
             return key
 
-    def _indices_to_device(self, idx: np.ndarray, stream) -> torch.Tensor:
-        """Slot indices -> a device int64 tensor, copied on `stream` from a page-locked ring
-        entry (asynchronous: nothing here waits for the stream's queued work).  Called with
-        ``_cv`` held, so it never blocks on the device: when the next entry's previous copy is
-        still queued (the learner runs more than the ring's length ahead), the ring grows by a
-        fresh entry instead, up to ``_IDX_RING_MAX`` entries."""
-        k = self._idx_next
-        ev = self._idx_ev[k]
-        if ev is not None and not ev.query():
-            if len(self._idx_buf) < self._IDX_RING_MAX:
-                # the busy entry (the oldest) moves one place on and stays next in line
-                self._idx_buf.insert(k, None)
-                self._idx_ev.insert(k, None)
-                ev = None
-            else:  # bounded: only a learner thousands of steps ahead reaches this
-                ev.synchronize()
-        self._idx_next = (k + 1) % len(self._idx_buf)
-        n = len(idx)
-        buf = self._idx_buf[k]
-        if buf is None or buf.numel() < n:
-            buf = torch.empty(n, dtype=torch.int64, pin_memory=torch.cuda.is_available())
-            self._idx_buf[k] = buf
-        host = buf[:n]
-        host.copy_(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)))
-        with torch.cuda.stream(stream):
-            dev = host.to(self.device, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        self._idx_ev[k] = ev
-        return dev
-
     def sample(self, batch_size: int, stream=None):
         """-> (keys, (obs, act, rew, disc, mu) collated on the device, probs).
 
-        The lock is held from picking the slots until the gather's completion event is
-        published as ``_last_read`` (both are asynchronous enqueues, so this is cheap): an
-        append either lands before -- its H2D event is among the ``pending`` the gather waits
-        for -- or after, and then its copy waits for this gather.  No append can slip between
-        the two and overwrite a slot the gather is reading."""
+        The sampled slot indices travel in the gather launch's own arguments
+        (impala_gather_rows_hidx), so the learner's stream gets the gather and nothing else: no
+        index upload, no event, and nothing here ever waits on the device.  The lock is held
+        from picking the slots until the gather is enqueued and its stream published as
+        ``_read_stream``: an append either lands before -- its H2D event is among the
+        ``pending`` the gather waits for -- or after, and then its copy waits for an event
+        recorded on that stream behind this gather.  No append can slip between the two and
+        overwrite a slot the gather is reading."""
         from impala_amd.engine import gather_rollouts
         cur = torch.cuda.current_stream(self.device) if stream is None else stream
         with self._cv:
@@ -213,12 +289,9 @@ class DeviceReplayBuffer(ReplayBuffer):
             pending, self._pending = self._pending, []
             for ev in pending:  # the learner's stream waits for every staged H2D
                 cur.wait_event(ev)
-            idx_t = self._indices_to_device(idx, cur)
-            batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx_t,
+            batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx,
                                     stream)
-            read = torch.cuda.Event()
-            read.record(cur)
-            self._last_read = read
+            self._read_stream = cur
             size = self._size
         probs = np.full(batch_size, 1.0 / size)
         return keys, batch, probs

@@ -139,6 +139,11 @@ int impala_destroy(impala_learner* h);
  * impala_apply_update, grads hold the post-clip gradient afterwards (as p.grad does). */
 int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp_avg,
                       float* exp_avg_sq, float* metrics, void* stream);
+/* Point the following steps' metrics (IMPALA_NUM_METRICS floats, every slot written by each
+ * step) at another caller-owned device buffer, host-side only: a learner hands every step a
+ * fresh vector -- the values it returns (agents/impala/learning.py:161-174) -- instead of
+ * copying the bound one after the step (a device copy of 36 bytes costs ~5 us of the stream). */
+int impala_set_metrics(impala_learner* h, float* metrics);
 /* Re-derive the kernel-layout weights after the caller changed `params` (load_state_dict). */
 int impala_refresh_weights(impala_learner* h, void* stream);
 /* Adam step counter (torch state['step']); for checkpoint resume. */
@@ -221,6 +226,11 @@ int impala_dp_train_step(impala_learner* h, const impala_batch* batch, int bucke
  * row i of dst[f], rows of row_bytes[f] bytes (multiple of 4); idx is a device int64 [n]. */
 int impala_gather_rows(const void* const* src, void* const* dst, const size_t* row_bytes,
                        int nfields, const int64_t* idx, int n, void* stream);
+/* The same gather with the row indices in HOST memory, read during the call and passed in the
+ * launches' own arguments (256 rows per launch): no index upload, so nothing but the gather
+ * itself is enqueued on `stream` (DeviceReplayBuffer.sample). */
+int impala_gather_rows_hidx(const void* const* src, void* const* dst, const size_t* row_bytes,
+                            int nfields, const int64_t* host_idx, int n, void* stream);
 
 /* Host staging ring (SURVEY.md §8(b) impala_stage; replaces the 5·B pageable `.to(device)`
  * copies of learning.py:121-123).  The handle owns `nslots` device batch slots of B*T frames
@@ -246,6 +256,23 @@ int impala_gather_rows(const void* const* src, void* const* dst, const size_t* r
  * must: a host that stages without ever waiting runs ahead and the runtime stalls the copies. */
 int impala_stage_init(impala_learner* h, int nslots);
 int impala_stage(impala_learner* h, const impala_batch* host, int slot);
+/* Row staging: the same as impala_stage for a batch the caller has NOT collated -- the list of
+ * B trajectories that replay_buffer.sample(B) returns (agents/impala/learning.py:121-123,142;
+ * rlmeta CircularBuffer rows).  rows->obs[b] .. rows->behaviour_logits[b] point at trajectory
+ * b's T-row fields in host memory (obs T*3*64*64 bytes, actions T int64, rewards / discounts T
+ * floats, behaviour_logits T*A floats; discounts may be NULL on PPO handles); n must equal the
+ * batch size.  Each obs row is copied by SDMA straight from its own memory into the slot (rows
+ * in page-locked memory -- e.g. a pinned replay arena -- make the copies asynchronous;
+ * adjacent rows are merged into one copy); the small fields are collated by the host into a
+ * page-locked block of the slot (the call waits for the slot's previous copies first). */
+typedef struct {
+  const void* const* obs;
+  const void* const* actions;
+  const void* const* rewards;
+  const void* const* discounts;
+  const void* const* behaviour_logits;
+} impala_rows;
+int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slot);
 int impala_stage_wait(impala_learner* h, int slot);
 int impala_slot_batch(impala_learner* h, int slot, void* stream, impala_batch* out);
 int impala_slot_release(impala_learner* h, int slot, void* stream);

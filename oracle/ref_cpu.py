@@ -195,10 +195,12 @@ def train_step(model: nn.Module, optimizer: torch.optim.Optimizer, batch,
 
 
 def train_step_fp64(flat: np.ndarray, batch_np, A: int = 15, steps: int = 1,
-                    capture: Optional[dict] = None, grad_mode: str = DEFAULT_GRAD_MODE):
+                    capture: Optional[dict] = None, grad_mode: str = DEFAULT_GRAD_MODE,
+                    metrics_each: Optional[list] = None):
     """The same step in float64 (model, batch floats, autograd, Adam): the exact-arithmetic
     yardstick against which both the fp32 oracle and the HIP fp32 path are measured.
-    -> (final flat params, flat post-clip grads (p.grad after clip_grad_norm_) of the last step, metrics of the last step)."""
+    -> (final flat params, flat post-clip grads (p.grad after clip_grad_norm_) of the last step, metrics of the last step).
+    ``metrics_each`` (a list) receives every step's metrics as floats."""
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.float64)
     try:
@@ -216,6 +218,8 @@ def train_step_fp64(flat: np.ndarray, batch_np, A: int = 15, steps: int = 1,
              torch.from_numpy(mu.astype(np.float64))]
         for _ in range(steps):
             met = train_step(ref, opt, b, collated=True, capture=capture, grad_mode=grad_mode)
+            if metrics_each is not None:
+                metrics_each.append({k: float(v) for k, v in met.items()})
         grads = torch.cat([p.grad.detach().reshape(-1) for p in ref.parameters()]).numpy().copy()
         params = torch.cat([p.detach().reshape(-1) for p in ref.parameters()]).numpy().copy()
         return params, grads, {k: float(v) for k, v in met.items()}

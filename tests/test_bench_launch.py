@@ -14,12 +14,13 @@ def _args(gpus):
 
 
 def test_launch_cmd_shape():
-    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "20", "--warmup", "5"], 29555)
+    """The launcher binds its own rendezvous port (c10d store on port 0, 127.0.0.1): no port
+    number is picked before the socket that uses it exists."""
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "20", "--warmup", "5"])
     assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
-    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
-    i = cmd.index("--master-addr")
-    assert cmd[i + 1] == "127.0.0.1"
-    assert "--master-port=29555" in cmd
+    assert "--nproc-per-node=8" in cmd and "--standalone" in cmd
+    assert "--local-addr=127.0.0.1" in cmd
+    assert not any(c.startswith("--master-port") for c in cmd)
     assert cmd[-7].endswith("bench.py")
     assert cmd[-6:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
 
@@ -88,12 +89,11 @@ def test_frac_mix_of_the_executed_instruction_mix():
     assert abs(sr["frac_mix"] - 0.428) < 0.002
 
 
-def _fingerprint_worker(rank, world, port, q):
+def _fingerprint_worker(rank, world, store, q):
     import os
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     x = torch.arange(1000, dtype=torch.float32) / 7
     same = bench.replicas_bitwise_equal(x, dist)
     if rank == 1:
@@ -103,18 +103,14 @@ def _fingerprint_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_replicas_bitwise_equal_over_gloo():
+def test_replicas_bitwise_equal_over_gloo(tmp_path):
     """The cross-rank check the N-GPU record carries, at world size 2 on the CPU: equal
     buffers agree, a one-ulp difference on one rank is caught."""
     import multiprocessing as mp
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    store = str(tmp_path / "store")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_fingerprint_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_fingerprint_worker, args=(r, 2, store, q)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)
@@ -123,14 +119,13 @@ def test_replicas_bitwise_equal_over_gloo():
     assert res == [(0, True, False), (1, True, False)]
 
 
-def _settle_worker(rank, world, port, q):
+def _settle_worker(rank, world, store, q):
     import os
     import time
 
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     calls = [0]
 
     def step():  # a collective per step, and rank-dependent step times
@@ -146,19 +141,15 @@ def _settle_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_settle_keeps_ranks_in_lockstep_over_gloo():
+def test_settle_keeps_ranks_in_lockstep_over_gloo(tmp_path):
     """bench.settle (the untimed clock-settling steps before each timed region) runs the same
     number of steps on every rank when ranks run at different speeds: each step holds a
     collective, so a per-rank time check would leave one rank in an all-reduce alone."""
     import multiprocessing as mp
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    store = str(tmp_path / "store")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_settle_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_settle_worker, args=(r, 2, store, q)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)

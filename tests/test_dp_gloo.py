@@ -7,21 +7,12 @@ Two shapes: world 2 at B=4, T=6 in fp32, and C3's replica count -- world 8, B=8 
 T=20 (global B=64) -- in float64, where the only difference between the mean of the 8 shard
 gradients and the B=64 gradient is the summation order: bound 1e-12 rel-L2 (measured 4.8e-15)."""
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _batch(B, T, A, seed, f64):
@@ -38,15 +29,15 @@ def _model(A, f64):
     return m.double() if f64 else m
 
 
-def _worker(rank, world, port, out_dir, B=4, T=6, f64=False):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+def _worker(rank, world, out_dir, B=4, T=6, f64=False):
+    # rendezvous through a file store in the test's own directory: no TCP port to pick
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     if f64:  # obs / 255. follows the default dtype
         torch.set_default_dtype(torch.float64)
     from impala_amd.distributed import allreduce_grads, init_process_group, shard_range, params_checksum
     from oracle import ref_cpu
-    init_process_group("gloo")
+    init_process_group("gloo", init_method=f"file://{os.path.join(out_dir, 'store')}")
     A = 15
     full = _batch(B, T, A, 77, f64)
     lo, hi = shard_range(B, world, rank)
@@ -78,7 +69,7 @@ def _worker(rank, world, port, out_dir, B=4, T=6, f64=False):
                          ids=["w2_B4_T6_fp32", "w8_B64_T20_fp64"])
 def test_dp_shard_gradients_equal_full_batch(tmp_path, world, B, T, f64, tol):
     from oracle import ref_cpu
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), B, T, f64), nprocs=world,
+    mp.spawn(_worker, args=(world, str(tmp_path), B, T, f64), nprocs=world,
              join=True)
     prev, prev_dt = torch.get_num_threads(), torch.get_default_dtype()
     torch.set_num_threads(min(8, os.cpu_count() or 1))

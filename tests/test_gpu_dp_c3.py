@@ -4,12 +4,13 @@
   `compute_grads_allreduced` (one bucket, the default; and the two- and three-bucket
   arrangements) + `impala_apply_update`; a one-rank all-reduce is the identity, so two steps
   must be bitwise equal to `impala_train_step` on the same batches.
-* C3's per-replica shape (B=64 per replica, T=20; BASELINE config 3 is 8 replicas x 64): two
-  replicas on the box's one GPU over gloo (RCCL refuses two ranks on one device), bf16 and
-  fp32, each on its half of a B=128 batch, against one learner on the whole B=128 batch.
-  Replicas stay bitwise identical; the all-reduced mean gradient equals the full-batch
-  gradient up to fp32 summation order (bounds below); params after two steps within Adam's
-  one-lr-step bound.
+* BASELINE config 3 itself (8 replicas x B=64 = global B=512, T=20) on the HIP path: eight
+  replica processes on the box's one GPU over gloo (RCCL refuses two ranks on one device),
+  bf16 and fp32, each on its shard (shard_range) of a B=512 batch, against one learner on the
+  whole B=512 batch; and the same with two replicas on a B=128 batch.  Replicas stay bitwise
+  identical (parameters, and the clip norm and step of the reduced gradient); the all-reduced
+  mean gradient equals the full-batch gradient up to fp32 summation order (bounds below);
+  params after two steps within Adam's one-lr-step bound.
 8-GPU scaling itself is unmeasured here (the driver runs it on an 8-GPU node).
 """
 import json
@@ -218,23 +219,30 @@ dist.barrier()
 dist.destroy_process_group()
 """
 
-# all-reduced mean of two B=64 shard gradients vs the B=128 gradient: the same per-frame
+# all-reduced mean of the B=64 shard gradients vs the full-batch gradient: the same per-frame
 # arithmetic (the 1/B loss scale differs by an exact power of two), summed in another order
-# (slab splits, two-way sum).  Measured: 4.0e-7 fp32, 1.2e-7 bf16 (profiles/r02a)
+# (slab splits, the W-way sum).  Measured: 4.0e-7 fp32, 1.2e-7 bf16 at 2 replicas
+# (profiles/r02a)
 C3_GRAD_RL2 = {"fp32": 2e-6, "bf16": 2e-6}
 
 
+@pytest.mark.parametrize("world", [8, 2], ids=["C3_w8_GB512", "w2_GB128"])
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-def test_c3_per_replica_shape_two_replicas_match_full_batch(dtype, tmp_path):
+def test_c3_replicas_match_full_batch(dtype, world, tmp_path):
     dev = _dev()
-    GB = 128
-    _launch(tmp_path, C3_WORKER, 2, {"DTYPE": dtype, "GB": str(GB)}, timeout=400)
-    p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
-    np.testing.assert_array_equal(p0, p1)
-    # grad_norm (of the reduced gradient) and the step agree bitwise; the loss metrics are
-    # each replica's own shard means
-    m0, m1 = np.load(tmp_path / "m0.npy"), np.load(tmp_path / "m1.npy")
-    np.testing.assert_array_equal(m0[6:8], m1[6:8])
+    GB = 64 * world
+    _launch(tmp_path, C3_WORKER, world, {"DTYPE": dtype, "GB": str(GB)}, timeout=500)
+    ps = [np.load(tmp_path / f"p{r}.npy") for r in range(world)]
+    ms = [np.load(tmp_path / f"m{r}.npy") for r in range(world)]
+    p0 = ps[0]
+    for r in range(1, world):
+        np.testing.assert_array_equal(ps[r], p0)
+        # grad_norm (of the reduced gradient) and the step agree bitwise; the loss metrics are
+        # each replica's own shard means
+        np.testing.assert_array_equal(ms[r][6:8], ms[0][6:8])
+    gs = [np.load(tmp_path / f"g{r}.npy") for r in range(world)]
+    for r in range(1, world):  # every replica holds the same reduced gradient
+        np.testing.assert_array_equal(gs[r], gs[0])
     from impala_amd.engine import Engine
     from impala_amd.model import AtariPPOModel
     m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype=dtype, seed=0)
@@ -247,7 +255,8 @@ def test_c3_per_replica_shape_two_replicas_match_full_batch(dtype, tmp_path):
     g_full = m.flat_grad.cpu().numpy().astype(np.float64)
     g_dp = np.load(tmp_path / "g0.npy").astype(np.float64)
     rl2 = float(np.linalg.norm(g_dp - g_full) / np.linalg.norm(g_full))
-    print(f"C3 {dtype}: all-reduced mean gradient vs B={GB} gradient rel-L2 {rl2:.2e}")
+    print(f"C3 {dtype} world {world}: all-reduced mean gradient vs B={GB} gradient rel-L2 "
+          f"{rl2:.2e} (bound {C3_GRAD_RL2[dtype]:.0e})")
     assert rl2 < C3_GRAD_RL2[dtype], rl2
     e.apply_update()
     b1 = [torch.from_numpy(np.ascontiguousarray(x)).to(dev)
@@ -256,7 +265,7 @@ def test_c3_per_replica_shape_two_replicas_match_full_batch(dtype, tmp_path):
     torch.cuda.synchronize()
     p = m.flat.cpu().numpy()
     d = np.abs(p0 - p)
-    print(f"C3 {dtype}: params after 2 steps max |dp - full| {d.max():.2e}, "
+    print(f"C3 {dtype} world {world}: params after 2 steps max |dp - full| {d.max():.2e}, "
           f"frac > 1e-6 {np.mean(d > 1e-6):.2e}")
     # measured max 2.2e-8 (fp32) / 1.5e-8 (bf16); Adam could amplify a near-zero gradient
     # element's rounding to ~lr, so the bound is one lr step with almost all within 1e-6

@@ -43,34 +43,69 @@ def _cfg(**over):
     return load_config(o)
 
 
+# the drop-in path (ImpalaBuilder -> ImpalaLearner.train_step -> replay.sample -> host staging)
+# against the float64 oracle, the yardstick test_gpu_parity_full.py uses.  Every step's metrics
+# are checked against float64 run from the parameters the learner held before that step (the
+# metrics are functions of the parameters and the batch): every key of every step within the
+# north_star's 1e-5 relative, except train/pg, bounded NORMWISE (as test_gpu_parity_full.py
+# bounds the V-trace outputs): |d| <= 1e-5 (|pg| + mean|log pi(a) adv|).  pg is a mean of
+# mixed-sign terms of magnitude ~0.1-1 that cancels to -3e-3 at step 3 of this batch; there the
+# fp32 path's 3.7e-7 absolute (1.2e-6 of the terms' mean magnitude, r06a) is 1.2e-4 of the
+# cancelled value.  Over several steps the two trajectories part at rounding level (Adam turns a
+# rounding-level difference in a near-zero gradient element into an O(lr) move), so the
+# multi-step trajectory is bounded on the parameters, with test_gpu_parity_full.py's 3-step
+# bound (max 5e-5, at most 100 parameters beyond 1e-6).
+LEARNER_RTOL = 1e-5
+KEYS = ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl", "train/ratio",
+        "train/grad_norm")
+
+
 def test_builder_learner_step_matches_oracle():
     _dev()
     from impala_amd.builder import ImpalaBuilder
-    B, T = 4, 20
+    B, T, steps = 4, 20, 4
     cfg = _cfg(agent={"batch_size": B})
     b = ImpalaBuilder(cfg)
     torch.manual_seed(0)
     model = b.make_network(None)
     flat0 = model.flat.cpu().numpy().copy()
     batch_np = ref_cpu.synthetic_batch(B, T, 15, seed=3)
-    rb = _FixedReplay([ref_cpu.to_trajectories(*batch_np) for _ in range(4)])
+    rb = _FixedReplay([ref_cpu.to_trajectories(*batch_np) for _ in range(steps)])
     learner = b.make_learner(model, rb)
     learner.prepare()
     assert rb.warm == cfg.agent.learning_starts
-    ref = ref_cpu.RefModel(15)
-    ref_cpu.load_flat(ref, flat0)
-    opt = ref_cpu.make_optimizer(ref)
-    for step in range(4):
+    traj = []
+    p64, _, _ = ref_cpu.train_step_fp64(flat0, batch_np, 15, steps=steps, metrics_each=traj)
+    worst, worst_traj, fails = {}, {}, []
+    for step in range(steps):
+        flat_k = model.flat.cpu().numpy().copy()
+        cap = {}
+        _, _, exp = ref_cpu.train_step_fp64(flat_k, batch_np, 15, steps=1, capture=cap)
+        logp = torch.log_softmax(cap["logits"], -1).gather(
+            -1, torch.from_numpy(batch_np[1]).unsqueeze(-1)).squeeze(-1)
+        pg_scale = float((logp[:, :-1] * cap["adv"]).abs().mean())
         met = learner.train_step()
-        exp = ref_cpu.train_step(ref, opt, ref_cpu.to_trajectories(*batch_np))
-        for k in ("train/loss", "train/entropy", "train/td", "train/pg", "train/kl",
-                  "train/ratio", "train/grad_norm"):
-            np.testing.assert_allclose(float(met[k]), float(exp[k]), rtol=2e-4, atol=1e-6,
-                                       err_msg=f"{k} step {step}")
+        for k in KEYS:
+            got, want = float(met[k]), exp[k]
+            scale = abs(want) + (pg_scale if k == "train/pg" else 0.0)
+            rel = abs(got - want) / max(scale, 1e-30)
+            worst[k] = max(worst.get(k, 0.0), rel)
+            worst_traj[k] = max(worst_traj.get(k, 0.0),
+                                abs(got - traj[step][k]) / max(abs(traj[step][k]), 1e-30))
+            if rel > LEARNER_RTOL:
+                fails.append((k, step, got, want, rel))
         for k in ("debug/replay_sample_per_second", "debug/gradient_per_second",
                   "debug/total_time", "debug/forward_dt", "debug/update_time"):
             assert k in met
-    np.testing.assert_allclose(model.flat.cpu().numpy(), ref_cpu.flat_params(ref), atol=5e-6)
+    print("learner vs fp64 from the same parameters, worst rel over 4 steps (pg normwise): " +
+          ", ".join(f"{k[6:]} {v:.2e}" for k, v in worst.items()))
+    print("learner vs the fp64 4-step trajectory (for the record): " +
+          ", ".join(f"{k[6:]} {v:.2e}" for k, v in worst_traj.items()))
+    assert not fails, fails
+    d = np.abs(model.flat.cpu().numpy() - p64)
+    print(f"learner params after {steps} steps vs fp64: max |d| {d.max():.2e}, "
+          f"n > 1e-6 {int(np.sum(d > 1e-6))}")
+    assert d.max() <= 5e-5 and int(np.sum(d > 1e-6)) <= 100
     # push every model_push_period (4) steps: the actor copy now equals the learner weights
     torch.cuda.synchronize()
     np.testing.assert_array_equal(b.actor_model.flat.cpu().numpy(), model.flat.cpu().numpy())
@@ -291,11 +326,11 @@ def test_device_replay_overwrite_waits_for_queued_gather():
         np.testing.assert_array_equal(batch[4][j].cpu().numpy(), old[k][4].numpy())
 
 
-def test_device_replay_index_ring_grows_instead_of_waiting():
-    """sample() holds the replay lock, so it must never wait on the device for its
-    page-locked index ring.  With the learner stream blocked behind queued work, ten samples in
-    a row find the 4-entry ring's next entry still queued: the ring grows (no host wait) and
-    every sample still gathers the rows its keys name."""
+def test_device_replay_sample_never_waits_on_the_stream():
+    """sample() holds the replay lock, so it must never wait on the device.  The
+    sampled indices travel in the gather launch's arguments (impala_gather_rows_hidx): with
+    the learner stream blocked behind queued work, ten samples in a row return while that work
+    is still running, and every sample gathers the rows its keys name."""
     dev = _dev()
     from impala_amd.replay import DeviceReplayBuffer
     T, A = 4, 3
@@ -309,15 +344,33 @@ def test_device_replay_index_ring_grows_instead_of_waiting():
     for _ in range(16):  # a few ms of queued work on the learner (current) stream
         busy = busy @ busy
         busy = busy / busy.norm()
+    done = torch.cuda.Event()
+    done.record()
     out = [rb.sample(4) for _ in range(10)]
-    grown = len(rb._idx_buf)
+    assert not done.query(), "sample() waited for the learner stream's queued work"
     torch.cuda.synchronize()
-    assert grown > 4, "the index ring did not grow while the stream was busy"
-    assert grown <= rb._IDX_RING_MAX
     for keys, batch, _ in out:
         for j, k in enumerate(keys.tolist()):
             assert int(batch[0][j].float().mean().item()) == k
             assert float(batch[4][j].mean().item()) == float(k)
+
+
+def test_gather_rows_host_and_device_indices_agree():
+    """impala_gather_rows (device indices) and impala_gather_rows_hidx (indices in the launch
+    arguments, 256 rows per launch) copy the same rows: 300 rows of fields with row sizes
+    below, at and above the 16 KB piece."""
+    dev = _dev()
+    from impala_amd.engine import gather_rollouts
+    g = torch.Generator(device=dev).manual_seed(1)
+    fields = [torch.randint(0, 255, (50, 3 * 16384 + 64), dtype=torch.uint8, device=dev, generator=g),
+              torch.randn(50, 20, device=dev, generator=g),
+              torch.randint(0, 1 << 30, (50, 16384 // 8), dtype=torch.int64, device=dev, generator=g)]
+    idx = np.random.default_rng(0).integers(0, 50, size=300)
+    a = gather_rollouts(fields, idx)
+    b = gather_rollouts(fields, torch.from_numpy(idx).to(dev))
+    ti = torch.from_numpy(idx).to(dev)
+    for f, x, y in zip(fields, a, b):
+        assert torch.equal(x, f[ti]) and torch.equal(y, f[ti])
 
 
 def test_device_replay_append_during_sample_threaded():
@@ -396,3 +449,85 @@ def test_whole_model_checkpoint_after_learner_step(tmp_path):
     assert w.grad.data_ptr() == m2.flat_grad[off:].data_ptr()
     lg1, v1 = m2(obs)
     assert torch.equal(lg0, lg1) and torch.equal(v0, v1)
+
+
+@pytest.mark.parametrize("h2d", ["default", "sdma_only"])
+def test_pinned_replay_rows_staged_in_place_match_device_batches(h2d, monkeypatch):
+    """ImpalaLearner over a PinnedReplayBuffer: each step's B trajectories are copied by
+    impala_stage_rows straight from the page-locked arena rows (one SDMA copy per row, the small
+    fields collated by the host).  An actor-side append overwrites the oldest arena row before
+    every step, so rows the previous step staged are rewritten while the learner runs ahead;
+    the replay fences them first.  Weights and metrics must be bitwise those of the same
+    trajectories (as sampled) handed over already collated in HBM."""
+    dev = _dev()
+    for k, v in H2D_MODES[h2d].items():
+        monkeypatch.setenv(k, v)
+    from impala_amd.engine import Engine
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    from impala_amd.replay import PinnedReplayBuffer
+    B, T, A, C, steps = 4, 20, 15, 6, 8
+    trajs = [ref_cpu.to_trajectories(*ref_cpu.synthetic_batch(1, T, A, seed=700 + i))[0]
+             for i in range(C + steps)]
+    rb = PinnedReplayBuffer(capacity=C, rollout_length=T, num_actions=A, seed=4)
+    for i in range(C):
+        rb.append(trajs[i])
+    seen = []
+    sample = rb.sample
+
+    def recording_sample(n):
+        keys, batch, probs = sample(n)
+        seen.append(keys.copy())
+        return keys, batch, probs
+
+    rb.sample = recording_sample
+    m1 = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+    ln = ImpalaLearner(m1, rb, batch_size=B, rollout_length=T, model_push_period=1000)
+    mets = []
+    for s in range(steps):
+        mets.append(ln.train_step())
+        rb.append(trajs[C + s])  # overwrites the oldest row while step s may still be staging
+    m2 = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+    e2 = Engine(m2, batch_size=B, rollout_length=T)
+    m2._train_engine = e2
+    for s, keys in enumerate(seen):
+        items = [trajs[int(k)] for k in keys]
+        b = [torch.stack([it[j] for it in items]).to(dev) for j in range(5)]
+        b = [x.squeeze(-1) if j in (1, 2, 3) else x for j, x in enumerate(b)]
+        e2.train_step(*[x.contiguous() for x in b])
+        torch.cuda.synchronize()
+        assert float(mets[s]["train/loss"]) == float(e2.metrics[0]), s
+    torch.cuda.synchronize()
+    assert torch.equal(m1.flat, m2.flat)
+
+
+def test_agent_train_over_learner_floats_match_device_metrics():
+    """DistributedAgent.train over ImpalaLearner (distributed_agent.py:26-41): the stats it
+    folds in, read through one copy per step (sync_every 1) or per 3 steps, equal float(v) of
+    the learner's own device metrics."""
+    dev = _dev()
+    from impala_amd.agent import DistributedAgent
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    B, T = 2, 20
+    batches = [tuple(torch.from_numpy(x).to(dev) for x in ref_cpu.synthetic_batch(B, T, 15, seed=s))
+               for s in range(5)]
+    for sync in (1, 3):
+        m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+        ln = ImpalaLearner(m, _FixedReplay(list(batches)), batch_size=B)
+        got = []
+        step = ln.train_step
+
+        def recording():
+            met = step()
+            got.append({k: float(v) for k, v in met.items() if k.startswith("train/")})
+            return met
+
+        ln.train_step = recording
+        ag = DistributedAgent(None, ln, sync_every=sync)
+        ag.train(5)
+        st = ag.stats.dict()
+        for k in got[0]:
+            assert st[k]["count"] == 5
+            assert abs(st[k]["mean"] - sum(g[k] for g in got) / 5) <= 1e-6 * (1 + abs(st[k]["mean"]))
+            assert st[k]["min"] == min(g[k] for g in got) and st[k]["max"] == max(g[k] for g in got)

@@ -135,6 +135,46 @@ def test_replay_circular_uniform_sampling():
     assert all(2 <= f <= 6 for f in fills)
 
 
+def test_pinned_replay_rows_are_arena_views_with_addresses():
+    """PinnedReplayBuffer (the host arena the learner's impala_stage_rows reads in place):
+    sample returns the reference's list of trajectories as views into the arena plus each
+    row's address; overwriting a row a tracked batch still reads calls that batch's fence
+    first."""
+    from impala_amd.replay import PinnedReplayBuffer, RowBatch
+    rb = PinnedReplayBuffer(capacity=5, rollout_length=20, num_actions=15, seed=1)
+    for i in range(7):
+        t = _traj(fill=i)
+        t[2] = torch.full((20, 1), float(i))
+        rb.append(t)
+    keys, batch, probs = rb.sample(4)
+    assert isinstance(batch, RowBatch) and len(batch) == 4 and np.allclose(probs, 0.2)
+    assert all(k >= 2 for k in keys)
+    for b, item in enumerate(batch):  # reference format, and the views' addresses
+        assert item[0].shape == (20, 3, 64, 64) and item[1].shape == (20, 1)
+        assert item[4].shape == (20, 15) and item[1].dtype == torch.int64
+        assert int(item[0][0, 0, 0, 0]) == int(keys[b]) == int(item[2][0, 0])
+        for f in range(5):
+            assert int(batch.row_ptrs[f][b]) == item[f].data_ptr()
+    fenced = []
+    batch.fence = lambda: fenced.append(1)
+    slot = rb._cursor  # the next append overwrites this row
+    rb.append(_traj(fill=9))
+    assert fenced == ([1] if any(item[0].data_ptr() == rb.fields[0][slot].data_ptr()
+                                 for item in batch) else [])
+
+
+def test_agent_host_floats_one_copy_per_vector():
+    """DistributedAgent turns a step's device metric scalars (views of one metrics vector, as
+    ImpalaLearner returns them) into floats from one stacked copy, and plain values through
+    float(v), with the values float(v) gives."""
+    from impala_amd.agent import _host_floats
+    vecs = [torch.arange(9, dtype=torch.float32) * (k + 1) for k in range(3)]
+    pend = [dict(zip(("a", "b", "c"), v.unbind(0)), d=0.5, e=torch.tensor(2.0)) for v in vecs]
+    got = _host_floats(pend)
+    for k, g in enumerate(got):
+        assert g == {"a": 0.0, "b": 1.0 * (k + 1), "c": 2.0 * (k + 1), "d": 0.5, "e": 2.0}
+
+
 def test_replay_warm_up_times_out():
     rb = ReplayBuffer(capacity=4)
     rb.append(_traj())
@@ -312,23 +352,22 @@ def test_adam_block_partition_covers_every_parameter_once(A):
     assert (hits == 1).all(), np.nonzero(hits != 1)[0][:10]
 
 
-def test_torchrun_relaunches_only_on_a_rendezvous_port_race(monkeypatch):
-    """tests/torchrun_util.py launches again only when the launcher's store lost its port
-    (EADDRINUSE at rendezvous, before any worker starts); any other failure is returned."""
-    import subprocess
+def test_torchrun_launcher_binds_its_own_port(tmp_path):
+    """tests/torchrun_util.py: the launcher's c10d store binds port 0 itself (--standalone on
+    127.0.0.1), so no port number is chosen before the socket that uses it exists.  Two gloo
+    ranks rendezvous through it and all-reduce."""
+    import os
     import torchrun_util
 
-    race = subprocess.CompletedProcess([], 1, "", "next_rendezvous ... EADDRINUSE, address already in use")
-    crash = subprocess.CompletedProcess([], 1, "", "worker raised RuntimeError")
-    ok = subprocess.CompletedProcess([], 0, "", "")
-    for seq, want_calls, want_rc in (([race, ok], 2, 0), ([crash, ok], 1, 1), ([race] * 3, 3, 1)):
-        calls = []
-
-        def run(cmd, seq=seq, calls=calls, **kw):
-            calls.append(cmd)
-            return seq[len(calls) - 1]
-
-        monkeypatch.setattr(torchrun_util.subprocess, "run", run)
-        r = torchrun_util.torchrun("w.py", 2, {}, ".")
-        assert (len(calls), r.returncode) == (want_calls, want_rc)
-        assert all("--master-addr=127.0.0.1" in c for c in calls)
+    cmd = torchrun_util.torchrun_cmd("w.py", 2)
+    assert "--standalone" in cmd and "--local-addr=127.0.0.1" in cmd
+    assert not any(c.startswith("--master-port") for c in cmd)
+    w = tmp_path / "w.py"
+    w.write_text("import os, torch, torch.distributed as dist\n"
+                 "dist.init_process_group('gloo')\n"
+                 "t = torch.ones(1) * (dist.get_rank() + 1)\n"
+                 "dist.all_reduce(t)\n"
+                 "assert t.item() == 3.0 and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                 "dist.destroy_process_group()\n")
+    r = torchrun_util.torchrun(w, 2, dict(os.environ), str(tmp_path), timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
