@@ -458,7 +458,7 @@ def _synthetic_np(B, T, A, seed):
     return obs, act, rew, disc, mu
 
 
-LOOP_REPLAYS = ("device_replay", "pinned_replay", "host_list_replay")
+LOOP_REPLAYS = ("device_replay", "host_list_replay")
 
 
 def run_learner_loop(args, dev, headline_ms):
@@ -468,20 +468,19 @@ def run_learner_loop(args, dev, headline_ms):
     stage, _train_step, push every 4 steps, debug timings) -> a replay of 1000 trajectories
     (builder.py:30-36), for each replay the learner can be given:
     * device_replay     DeviceReplayBuffer: HBM ring, device-side gather of the sampled slots;
-    * pinned_replay     PinnedReplayBuffer: page-locked host arena, the sampled rows copied
-                        in place by impala_stage_rows (SDMA, one copy per trajectory);
-    * host_list_replay  ReplayBuffer: the reference's list of pageable CPU tensors, collated
-                        by one torch.stack per field into a page-locked slot, then staged.
-    Each with sync_every 1 (the reference: the metrics read every step) and 100.  Per-step
-    device times from the step clock (each step's first learner kernel stamps it)."""
+    * host_list_replay  ReplayBuffer: the reference's list of pageable CPU tensors, the rows
+                        collated by the library's thread pool into a page-locked slot and
+                        copied by SDMA (impala_stage_rows).
+    Each with sync_every 1 (the reference: the metrics read every step) and 100; the learner
+    prefetches the next batch (ImpalaLearner prefetch=1, the default).  Per-step device times
+    from the step clock (each step's first learner kernel stamps it)."""
     from impala_amd.agent import DistributedAgent
     from impala_amd.learner import ImpalaLearner
     from impala_amd.model import AtariPPOModel
-    from impala_amd.replay import DeviceReplayBuffer, PinnedReplayBuffer, ReplayBuffer
+    from impala_amd.replay import DeviceReplayBuffer, ReplayBuffer
     B, T, A, cap = args.batch, args.rollout, args.actions, args.loop_capacity
     trajs = synthetic_trajectories(cap, T, A, 4242)
     makers = {"device_replay": lambda: DeviceReplayBuffer(cap, T, A, device=dev, seed=5),
-              "pinned_replay": lambda: PinnedReplayBuffer(cap, T, A, seed=5),
               "host_list_replay": lambda: ReplayBuffer(cap, seed=5)}
     out = {"steps": args.loop_steps, "capacity": cap, "headline_ms_per_step": headline_ms,
            "note": "DistributedAgent.train -> ImpalaLearner.train_step -> replay.sample(B) on a "

@@ -57,7 +57,8 @@ EXPORTS = (
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
     "impala_gather_rows_hidx",
-    "impala_stage_init", "impala_stage", "impala_stage_rows", "impala_stage_wait",
+    "impala_stage_init", "impala_stage", "impala_stage_rows", "impala_stage_rows_async",
+    "impala_stage_wait",
     "impala_slot_batch",
     "impala_slot_release", "impala_act", "impala_set_debug_vtrace",
     "impala_timer_read_kernel", "impala_dp_unique_id", "impala_dp_init", "impala_dp_train_step",
@@ -177,6 +178,7 @@ def _declare(lib):
     lib.impala_stage_init.argtypes = [_P, C.c_int]
     lib.impala_stage.argtypes = [_P, C.POINTER(ImpalaBatch), C.c_int]
     lib.impala_stage_rows.argtypes = [_P, C.POINTER(ImpalaRows), C.c_int, C.c_int]
+    lib.impala_stage_rows_async.argtypes = [_P, C.POINTER(ImpalaRows), C.c_int, C.c_int]
     lib.impala_stage_wait.argtypes = [_P, C.c_int]
     lib.impala_slot_batch.argtypes = [_P, C.c_int, _P, C.POINTER(ImpalaBatch)]
     lib.impala_slot_release.argtypes = [_P, C.c_int, _P]

@@ -15,7 +15,7 @@ import torch
 from impala_amd.core import Actor, Builder
 from impala_amd.learner import ImpalaAdam, ImpalaLearner
 from impala_amd.model import AtariPPOModel
-from impala_amd.replay import DeviceReplayBuffer, PinnedReplayBuffer, ReplayBuffer
+from impala_amd.replay import DeviceReplayBuffer, ReplayBuffer
 
 
 class ImpalaActor(Actor):
@@ -103,8 +103,6 @@ class ImpalaBuilder(Builder):
         if kind == "device" and torch.cuda.is_available():
             dev = self.cfg.distributed.train_device
             return DeviceReplayBuffer(cap, self.cfg.agent.rollout_length, A, device=dev, seed=seed)
-        if kind == "pinned":
-            return PinnedReplayBuffer(cap, self.cfg.agent.rollout_length, A, seed=seed)
         return ReplayBuffer(cap, seed=seed)
 
     def make_actor(self, model, rb=None, deterministic: bool = False):  # builder.py:38-40
@@ -130,7 +128,9 @@ class ImpalaBuilder(Builder):
                              rollout_length=self.cfg.agent.rollout_length,
                              dtype=self._learner_cfg("dtype", None), process_group=pg,
                              world_size=ws,
-                             vtrace_grad_mode=self._learner_cfg("vtrace_grad_mode", None), **kw)
+                             vtrace_grad_mode=self._learner_cfg("vtrace_grad_mode", None),
+                             prefetch=1 if int(self.cfg.training.get("prefetch", 1) or 0) > 0 else 0,
+                             **kw)
 
     def make_network(self, env_spec=None):  # builder.py:51-59
         obs_shape, n_act = (3, 64, 64), 15

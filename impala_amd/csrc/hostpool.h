@@ -6,6 +6,8 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <deque>
+#include <string>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -109,6 +111,89 @@ class HostPool {
   std::atomic<int> next_{0};
   uint64_t gen_ = 0;
   bool stop_ = false;
+};
+
+// One background thread that runs staging jobs in order (impala_stage_rows_async): the caller
+// hands over a job and returns at once; `pending(slot)` jobs per slot are waited for by the
+// calls that use the slot.  A job's status and error text are kept for the next waiter.
+class Stager {
+ public:
+  Stager() : th_([this] { loop(); }) {}
+  ~Stager() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void submit(int slot, std::function<int(std::string&)> job) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++pending_[slot];
+      q_.push_back({slot, std::move(job)});
+    }
+    cv_.notify_all();
+  }
+  // wait until `slot` (every slot when < 0) has no job queued or running; -> the first failed
+  // job's status since the last wait (0 = ok), its message in `msg`
+  int wait(int slot, std::string& msg) {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] {
+      if (slot >= 0) return pending_[slot] == 0;
+      for (int p : pending_)
+        if (p) return false;
+      return true;
+    });
+    int r = 0;
+    for (int i = 0; i < kSlots; ++i)
+      if ((slot < 0 || i == slot) && err_[i]) {
+        if (!r) {
+          r = err_[i];
+          msg = msg_[i];
+        }
+        err_[i] = 0;
+      }
+    return r;
+  }
+  static constexpr int kSlots = 8;
+
+ private:
+  struct Job {
+    int slot;
+    std::function<int(std::string&)> fn;
+  };
+  void loop() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop, and nothing left to run
+        j = std::move(q_.front());
+        q_.pop_front();
+      }
+      std::string m;
+      const int r = j.fn(m);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (r && !err_[j.slot]) {
+          err_[j.slot] = r;
+          msg_[j.slot] = m;
+        }
+        --pending_[j.slot];
+      }
+      done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::deque<Job> q_;
+  int pending_[kSlots] = {};
+  int err_[kSlots] = {};
+  std::string msg_[kSlots];
+  bool stop_ = false;
+  std::thread th_;
 };
 
 }  // namespace impala_host

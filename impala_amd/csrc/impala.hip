@@ -15,8 +15,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <memory>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/impala_hip.h"
 #include "head.h"
@@ -233,6 +235,7 @@ struct impala_learner {
   // API, hipMemcpyBatchAsync, is newer than the HIP runtime torch loads.)
   int stage_rows_mode = 0;
   impala_host::HostPool* pool = nullptr;
+  impala_host::Stager* stager = nullptr;  // impala_stage_rows_async's thread (lazily started)
   // native data-parallel step (impala_dp_*): the library's own RCCL communicator, so the
   // gradient all-reduces are enqueued with no host round trip and no c10d bookkeeping; the FC +
   // heads bucket is all-reduced on dp_stream while the per-frame backward runs
@@ -710,6 +713,10 @@ void drop_graphs(impala_learner* h) {
 }
 
 void free_ring(impala_learner* h) {
+  if (h->stager) {  // no staging job may still be writing into the ring
+    std::string m;
+    (void)h->stager->wait(-1, m);
+  }
   for (int i = 0; i < h->n_h2d; ++i) (void)hipStreamSynchronize(h->h2d_s[i]);
   for (auto& s : h->ring) {
     if (s.done) (void)hipEventSynchronize(s.done);
@@ -1107,6 +1114,7 @@ int impala_destroy(impala_learner* h) {
     (void)hipStreamDestroy(h->side);
   }
   dp_release(h);
+  delete h->stager;  // (free_ring above already waited for its jobs)
   delete h->pool;
   if (h->ws) (void)hipFree(h->ws);
   delete h;
@@ -1606,10 +1614,33 @@ int impala_stage_init(impala_learner* h, int nslots) {
   return 0;
 }
 
+namespace {
+// the staging jobs of `slot` (every slot when < 0) queued by impala_stage_rows_async have run;
+// a failed one's status is returned here
+int wait_staged(impala_learner* h, int slot) {
+  if (!h->stager) return 0;
+  std::string m;
+  if (int r = h->stager->wait(slot, m)) return fail(r, "impala_stage_rows_async: " + m);
+  return 0;
+}
+}  // namespace
+
+namespace {
+int stage_now(impala_learner* h, const impala_batch* b, int slot);
+}  // namespace
+
 int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (slot < 0 || slot >= h->n_slots)
     return fail(IMPALA_E_INVALID, "slot out of range (impala_stage_init not called?)");
+  if (int r = wait_staged(h, -1)) return r;  // one staging at a time per handle
+  return stage_now(h, b, slot);
+}
+
+namespace {
+// impala_stage's copies (also run by the staging thread's jobs, which must not wait on
+// themselves)
+int stage_now(impala_learner* h, const impala_batch* b, int slot) {
   const bool ppo = h->cfg.algo == IMPALA_ALGO_PPO;
   if (!b || !b->obs || !b->actions || !b->rewards || (!ppo && !b->discounts) ||
       !b->behaviour_logits)
@@ -1680,6 +1711,7 @@ int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
   CK(hipEventRecord(s.ready, h->h2d));
   return 0;
 }
+}  // namespace
 
 // Row staging (impala_stage_rows): the batch is B trajectories scattered in host memory (the
 // replay's rows), not one collated host batch.  Default (collate): the host's thread pool
@@ -1689,13 +1721,13 @@ int impala_stage(impala_learner* h, const impala_batch* b, int slot) {
 // ~1 ms, over three times the PCIe copy it feeds; the pool's threads share it.  The rows modes
 // instead copy each obs row by SDMA straight from its own memory (runs of adjacent rows merged)
 // and collate only the small fields.
-int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slot) {
+namespace {
+int check_rows(impala_learner* h, const impala_rows* rows, int n, int slot) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (slot < 0 || slot >= h->n_slots)
     return fail(IMPALA_E_INVALID, "slot out of range (impala_stage_init not called?)");
   const bool ppo = h->cfg.algo == IMPALA_ALGO_PPO;
-  const int B = h->cfg.batch_size;
-  if (!rows || n != B)
+  if (!rows || n != h->cfg.batch_size)
     return fail(IMPALA_E_INVALID, "impala_stage_rows: n must equal the handle's batch_size");
   if (!rows->obs || !rows->actions || !rows->rewards || (!ppo && !rows->discounts) ||
       !rows->behaviour_logits)
@@ -1704,6 +1736,44 @@ int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slo
     if (!rows->obs[b] || !rows->actions[b] || !rows->rewards[b] ||
         (!ppo && !rows->discounts[b]) || !rows->behaviour_logits[b])
       return fail(IMPALA_E_INVALID, "impala_stage_rows: null row pointer");
+  return 0;
+}
+int stage_rows_now(impala_learner* h, const impala_rows* rows, int n, int slot);
+}  // namespace
+
+int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slot) {
+  if (int r = check_rows(h, rows, n, slot)) return r;
+  if (int r = wait_staged(h, -1)) return r;  // one staging at a time per handle
+  return stage_rows_now(h, rows, n, slot);
+}
+
+int impala_stage_rows_async(impala_learner* h, const impala_rows* rows, int n, int slot) {
+  if (int r = check_rows(h, rows, n, slot)) return r;
+  if (int r = wait_staged(h, slot)) return r;  // the slot's previous job
+  if (!h->stager) {
+    h->stager = new (std::nothrow) impala_host::Stager();
+    if (!h->stager) return fail(IMPALA_E_STATE, "impala_stage_rows_async: staging thread");
+  }
+  // the job owns copies of the five pointer arrays; the rows themselves stay the caller's
+  auto p = std::make_shared<std::vector<const void*>>();
+  p->reserve(5 * (size_t)n);
+  const void* const* f[5] = {rows->obs, rows->actions, rows->rewards, rows->discounts,
+                             rows->behaviour_logits};
+  for (int k = 0; k < 5; ++k)
+    for (int b = 0; b < n; ++b) p->push_back(f[k] ? f[k][b] : nullptr);
+  h->stager->submit(slot, [h, p, n, slot](std::string& msg) {
+    const void* const* d = p->data();
+    const impala_rows r{d, d + n, d + 2 * n, d[3 * n] ? d + 3 * n : nullptr, d + 4 * n};
+    const int st = stage_rows_now(h, &r, n, slot);
+    if (st) msg = impala_last_error();
+    return st;
+  });
+  return 0;
+}
+
+namespace {
+int stage_rows_now(impala_learner* h, const impala_rows* rows, int n, int slot) {
+  const bool ppo = h->cfg.algo == IMPALA_ALGO_PPO;
   CK(hipSetDevice(h->device));
   auto& s = h->ring[slot];
   const size_t T = (size_t)h->cfg.rollout_length, N = (size_t)h->N, A = (size_t)h->A;
@@ -1754,7 +1824,7 @@ int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slo
     const impala_batch hbat{(const uint8_t*)(hb + off[0]), (const int64_t*)(hb + off[1]),
                             (const float*)(hb + off[2]),
                             ppo ? nullptr : (const float*)(hb + off[3]), (const float*)(hb + off[4])};
-    return impala_stage(h, &hbat, slot);
+    return stage_now(h, &hbat, slot);
   }
   const int ns = h->n_h2d;
   for (int i = 0; i < ns; ++i)  // the steps that read the slot have run
@@ -1800,10 +1870,12 @@ int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slo
   CK(hipEventRecord(s.ready, h->h2d));
   return 0;
 }
+}  // namespace
 
 int impala_stage_wait(impala_learner* h, int slot) {
   if (!h) return fail(IMPALA_E_INVALID, "null handle");
   if (slot < 0 || slot >= h->n_slots) return fail(IMPALA_E_INVALID, "slot out of range");
+  if (int r = wait_staged(h, slot)) return r;
   CK(hipEventSynchronize(h->ring[slot].ready));
   return 0;
 }
@@ -1811,6 +1883,7 @@ int impala_stage_wait(impala_learner* h, int slot) {
 int impala_slot_batch(impala_learner* h, int slot, void* stream, impala_batch* out) {
   if (!h || !out) return fail(IMPALA_E_INVALID, "null argument");
   if (slot < 0 || slot >= h->n_slots) return fail(IMPALA_E_INVALID, "slot out of range");
+  if (int r = wait_staged(h, slot)) return r;  // its copies are enqueued (ready recorded)
   CK(hipSetDevice(h->device));
   CK(hipStreamWaitEvent((hipStream_t)stream, h->ring[slot].ready, 0));
   *out = h->ring[slot].dev;

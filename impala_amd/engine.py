@@ -323,11 +323,13 @@ class Engine:
         check(_lib.lib().impala_stage(self._h, C.byref(b), int(slot)), "impala_stage")
         self._staged[slot] = host_batch  # the copies read these until stage_wait(slot)
 
-    def stage_rows(self, slot: int, row_ptrs):
+    def stage_rows(self, slot: int, row_ptrs, background: bool = False):
         """Enqueue the H2D copies of B trajectories that are NOT collated (impala_stage_rows):
         ``row_ptrs`` = five arrays of B host addresses (numpy uint64, or sequences of ints),
         trajectory b's obs / actions / rewards / discounts / behaviour-logits rows (discounts
-        None on PPO handles).  The rows must stay unchanged until stage_wait(slot)."""
+        None on PPO handles).  The rows must stay unchanged until stage_wait(slot).
+        ``background``: the handle's staging thread does the host collate and the enqueue
+        (impala_stage_rows_async); slot_batch / stage_wait wait for it."""
         import numpy as np
         arrs = [None if p is None else np.ascontiguousarray(p, dtype=np.uint64) for p in row_ptrs]
         B = self.batch_size
@@ -335,8 +337,8 @@ class Engine:
             if a is not None and a.shape != (B,):
                 raise ValueError(f"row pointer arrays must hold {B} addresses")
         rows = ImpalaRows(*[0 if a is None else a.ctypes.data for a in arrs])
-        check(_lib.lib().impala_stage_rows(self._h, C.byref(rows), B, int(slot)),
-              "impala_stage_rows")
+        fn = "impala_stage_rows_async" if background else "impala_stage_rows"
+        check(getattr(_lib.lib(), fn)(self._h, C.byref(rows), B, int(slot)), fn)
         self._staged[slot] = arrs
 
     def stage_wait(self, slot: int):

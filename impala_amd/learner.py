@@ -7,7 +7,6 @@ all-reduce of the flat gradient + ``impala_apply_update``.
 """
 from __future__ import annotations
 
-import functools
 import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Sequence, Tuple
@@ -66,13 +65,17 @@ class ImpalaLearner(Learner):
                  learning_starts: Optional[int] = None, model_push_period: int = 4,
                  rollout_length: int = 20, dtype: Optional[str] = None,
                  process_group=None, world_size: Optional[int] = None,
-                 vtrace_grad_mode: Optional[str] = None):
+                 vtrace_grad_mode: Optional[str] = None, prefetch: int = 1):
         """The reference's constructor (learning.py:88-96) plus keyword-only extensions:
         ``rollout_length``, ``dtype`` ("fp32" | "bf16"), the data-parallel ``process_group`` /
-        ``world_size``, and ``vtrace_grad_mode`` -- what the V-trace backward treats as constant
+        ``world_size``, ``vtrace_grad_mode`` -- what the V-trace backward treats as constant
         (``_lib.VTRACE_GRAD_MODES``; default "sg_advantage": targets and pg advantages constant,
         SURVEY.md §8(c); "sg_targets" / "sg_none" for rlax's stop_target_gradients=True / False
-        with the advantage live)."""
+        with the advantage live) -- and ``prefetch``: 1 (default) samples and stages the next
+        step's batch right after this step is enqueued, so the sampling, the host collate and
+        the H2D copies run while the GPU computes (the reference's replay client prefetches
+        its samples the same way, conf/config.yaml ``prefetch: 5``); 0 samples inside each
+        train_step, as learning.py:121 does."""
         self._model = model
         self._replay_buffer = replay_buffer
         if optimizer is None:
@@ -95,6 +98,8 @@ class ImpalaLearner(Learner):
                 world_size = dist.get_world_size(process_group)
         self._world_size = int(world_size)
         self._device = None
+        self._prefetch = int(prefetch) > 0
+        self._next = None  # the prefetched (batch, slot, n_samples, sample seconds)
         self._step_count = 0
         self._step_counter = 0
         self.can_train = True
@@ -133,11 +138,14 @@ class ImpalaLearner(Learner):
     def _stage_host(self, batch):
         """learning.py:121-123,142 for host trajectories, staged through the library's H2D ring
         (two slots: the copies of step k+1 wait only for the step that last read the slot).
-        Rows of a page-locked replay arena (PinnedReplayBuffer: the batch carries their
-        addresses) are copied by impala_stage_rows straight from the arena, with no host copy
-        of the frames; any other list of trajectories is collated into this slot's page-locked
-        buffers (one torch.stack per field) and staged by impala_stage.
-        -> (slot, the slot's device ImpalaBatch)."""
+        A batch that carries its rows' host addresses (ReplayBuffer.sample's RowBatch) is
+        staged by impala_stage_rows: the library's thread pool collates the rows into the slot's
+        page-locked block, then the SDMA copies; any other list of trajectories is collated into
+        this slot's page-locked buffers (one torch.stack per field) and staged by impala_stage.
+        -> the slot (its device batch: Engine.slot_batch, on the stream that runs the step).
+        Row batches return before their host collate: impala_stage_rows_async hands it to the
+        library's staging thread, so with the prefetch it runs beside this thread's enqueue of
+        the step and the device's work."""
         e = self._engine
         if getattr(e, "n_slots", 0) == 0:
             e.stage_init(2)
@@ -147,12 +155,11 @@ class ImpalaLearner(Learner):
         e.stage_wait(slot)  # the previous copies out of this slot's host memory are done
         rows = getattr(batch, "row_ptrs", None)
         if rows is not None and len(batch) == e.batch_size and batch.row_key == self._row_key():
-            e.stage_rows(slot, rows)
-            # the rows stay alive, and the replay does not overwrite them, until their copies
-            # are done (impala_stage_rows' SDMA-per-row modes read them after it returns)
+            # the library's staging thread collates and enqueues (slot_batch waits for it); the
+            # rows stay alive until the slot is restaged, after its copies are done
+            e.stage_rows(slot, rows, background=True)
             self._row_batches[slot] = batch
-            batch.fence = functools.partial(e.stage_wait, slot)
-            return slot, e.slot_batch(slot)
+            return slot
         if self._host_bufs[slot] is None:
             B, T, A = self._batch_size, self._rollout_length, e.num_actions
             pin = torch.cuda.is_available()
@@ -173,25 +180,56 @@ class ImpalaLearner(Learner):
                 for i, x in enumerate(xs):
                     buf[i].copy_(x.reshape(buf.shape[1:]))
         e.stage(slot, *bufs)
-        return slot, e.slot_batch(slot)
+        return slot
 
-    def train_step(self):  # learning.py:119-138
+    def _fetch(self):
+        """learning.py:121-123: replay.sample(B) and its staging -> (a device batch for
+        _train_step, or None when it sits in a staging slot; the slot or None; frames; seconds
+        spent).  Host batches are staged (copies enqueued) here; their slot's device views are
+        taken by _resolve on the thread that runs the step."""
         t0 = time.perf_counter()
         _, batch, _ = self._replay_buffer.sample(self._batch_size)
         slot = None
         if isinstance(batch, list) and batch and isinstance(batch[0][0], torch.Tensor) \
                 and batch[0][0].device.type == "cpu":
-            slot, b = self._stage_host(batch)
-            batch = (b,)
+            slot = self._stage_host(batch)
+            batch = None
             n_samples = self._batch_size * self._rollout_length
         else:
             batch = _collate(batch, self.device())
             n_samples = self._batch_size * batch[0].shape[1]
+        return batch, slot, n_samples, time.perf_counter() - t0
+
+    def _resolve(self, item):
+        batch, slot, n_samples, sample_s = item
+        if slot is not None:  # the step's stream waits for the slot's copies
+            batch = (self._engine.slot_batch(slot),)
+        return batch, slot, n_samples, sample_s
+
+    def _start_prefetch(self):
+        """Sample and stage the next step's batch now (a device replay's gather goes on the
+        learner's stream behind this step; a host batch's collate and copies are handed to the
+        library's staging thread).  A replay that cannot give a batch now is asked again,
+        synchronously, by the next call (which raises if it still cannot)."""
+        try:
+            self._next = self._fetch()
+        except Exception:  # noqa: BLE001 -- re-raised by the next call's own sample
+            self._next = None
+
+    def _take_next(self):
+        nxt, self._next = self._next, None
+        return nxt if nxt is not None else self._fetch()
+
+    def train_step(self):  # learning.py:119-138
+        t0 = time.perf_counter()
+        batch, slot, n_samples, sample_s = self._resolve(self._take_next())
         t1 = time.perf_counter()
         metrics = self._train_step(batch)
         if slot is not None:
             self._engine.slot_release(slot)
         t2 = time.perf_counter()
+        if self._prefetch:  # the next step's batch, while this step runs on the device
+            self._start_prefetch()
         update_time = 0
         self._step_count += 1
         self._step_counter = self._step_count
@@ -199,8 +237,9 @@ class ImpalaLearner(Learner):
             start = time.perf_counter()
             self._model.push()
             update_time = time.perf_counter() - start
-        # same definitions (and units) as the reference, learning.py:133-137
-        metrics["debug/replay_sample_per_second"] = (n_samples / ((t1 - t0) * 1000))
+        # same definitions (and units) as the reference, learning.py:133-137 (the sample time
+        # is this batch's own, also when it was prefetched by the previous call)
+        metrics["debug/replay_sample_per_second"] = (n_samples / (max(sample_s, 1e-9) * 1000))
         metrics["debug/gradient_per_second"] = (n_samples / ((t2 - t1) * 1000))
         metrics["debug/total_time"] = (time.perf_counter() - t0) * 1000
         metrics["debug/forward_dt"] = (t2 - t1) * 1000 / self._batch_size

@@ -5,13 +5,11 @@ UniformSampler())``; actors ``async_append`` one trajectory ``[s, a, r, discount
 (``agents/impala/learning.py:71-80``); the learner calls ``warm_up(learning_starts)`` and
 ``sample(batch_size) -> (keys, batch, probs)`` (``learning.py:116-121``).
 
-Three implementations with that interface:
+Two implementations with that interface:
 
-* ``ReplayBuffer``        host memory, returns the reference's list-of-trajectories batch.
-* ``PinnedReplayBuffer``  the same list-of-trajectories batch, its rows views into one
-  page-locked host arena; the batch also carries the rows' addresses, so the learner stages
-  them with ``impala_stage_rows`` (one SDMA copy per trajectory straight from the arena into
-  the device slot, no host collate of the 15.7 MB of frames).
+* ``ReplayBuffer``        host memory, returns the reference's list-of-trajectories batch; the
+  batch also carries the rows' host addresses, so the learner stages them with
+  ``impala_stage_rows`` (the library's thread pool collates them into a page-locked slot).
 * ``DeviceReplayBuffer``  MI355X-first: the circular store lives in HBM (1000 x 247 KB =
   247 MB of 288 GB); an appended trajectory is written into a pinned-host staging ring and
   copied to its HBM slot with an async H2D on a side stream, so each trajectory crosses PCIe
@@ -42,12 +40,11 @@ class RowBatch(list):
     """The list of B trajectories a replay's ``sample`` returns (the reference's batch format),
     plus, when every sampled trajectory's fields are contiguous host tensors of one layout,
     ``row_ptrs`` -- per field the B rows' host addresses (numpy uint64) -- and ``row_key`` --
-    the fields' (dtypes, byte sizes) -- for ``impala_stage_rows``.  A consumer whose copies read
-    the rows after it returns sets ``fence`` to a callable that returns once they are done; the
-    replay calls it before overwriting one of the rows."""
+    the fields' (dtypes, byte sizes) -- for ``impala_stage_rows``.  The rows are the replay's
+    own tensors: an append replaces a slot's list and never writes into a stored tensor, so a
+    consumer that keeps the batch keeps its rows."""
     row_ptrs = None
     row_key = None
-    fence = None
 
 
 class ReplayBuffer:
@@ -125,79 +122,6 @@ class ReplayBuffer:
                 batch.row_ptrs = tuple(np.ascontiguousarray(self._ptr_tab[idx, f]) for f in range(5))
             keys = self._keys[idx].copy()
         probs = np.full(batch_size, 1.0 / self._size)
-        return keys, batch, probs
-
-
-class PinnedReplayBuffer(ReplayBuffer):
-    """Host circular store in one page-locked arena (1000 x 247 KB at C2), CircularBuffer +
-    UniformSampler semantics (``agents/impala/builder.py:30-36``).  ``append`` copies the
-    trajectory into its arena slot once; ``sample`` returns the reference's list of B
-    trajectories -- views into the arena, valid until the slot is overwritten (clone to keep
-    one) -- as a ``RowBatch`` whose ``row_ptrs`` let the learner's H2D copies read the rows in
-    place."""
-
-    _READERS_MAX = 8  # batches whose staged copies are tracked (older ones are fenced)
-
-    def __init__(self, capacity: int = 1000, rollout_length: int = 20, num_actions: int = 15,
-                 seed: Optional[int] = None):
-        super().__init__(capacity, seed)
-        C, T, A = self.capacity, int(rollout_length), int(num_actions)
-        self.T, self.A = T, A
-        pin = torch.cuda.is_available()
-        self.fields = (torch.empty(C, T, 3, 64, 64, dtype=torch.uint8, pin_memory=pin),
-                       torch.zeros(C, T, 1, dtype=torch.int64, pin_memory=pin),
-                       torch.zeros(C, T, 1, dtype=torch.float32, pin_memory=pin),
-                       torch.zeros(C, T, 1, dtype=torch.float32, pin_memory=pin),
-                       torch.zeros(C, T, A, dtype=torch.float32, pin_memory=pin))
-        self._base = np.array([f.data_ptr() for f in self.fields], dtype=np.uint64)
-        self._row_bytes = np.array([f[0].numel() * f.element_size() for f in self.fields],
-                                   dtype=np.uint64)
-        self._row_key = (tuple(f.dtype for f in self.fields),
-                         tuple(int(b) for b in self._row_bytes))
-        self._readers: List[Tuple[set, RowBatch]] = []
-
-    def _fence_readers(self, slot: Optional[int] = None) -> None:
-        """Wait for the staged copies of every tracked batch that reads arena row `slot` (all
-        tracked batches beyond the newest _READERS_MAX when `slot` is None)."""
-        keep = []
-        for i, (rows, b) in enumerate(self._readers):
-            old = slot is None and i < len(self._readers) - self._READERS_MAX
-            if old or (slot is not None and slot in rows):
-                if b.fence is not None:
-                    b.fence()
-            else:
-                keep.append((rows, b))
-        self._readers = keep
-
-    def append(self, item: Sequence[torch.Tensor]) -> int:
-        with self._cv:
-            slot = self._cursor
-            self._fence_readers(slot)
-            for f, x in zip(self.fields, item):
-                f[slot].copy_(x.reshape(f.shape[1:]))
-            self._data[slot] = [f[slot] for f in self.fields]
-            self._row_keys[slot] = self._row_key
-            key = self._next_key
-            self._keys[slot] = key
-            self._next_key += 1
-            self._cursor = (slot + 1) % self.capacity
-            self._size = min(self._size + 1, self.capacity)
-            self._cv.notify_all()
-            return key
-
-    def sample(self, batch_size: int):
-        with self._cv:
-            idx = self._indices(batch_size)
-            batch = RowBatch(self._data[i] for i in idx)
-            u = idx.astype(np.uint64)
-            batch.row_ptrs = tuple(self._base[f] + u * self._row_bytes[f] for f in range(5))
-            batch.row_key = self._row_key
-            keys = self._keys[idx].copy()
-            self._readers.append((set(idx.tolist()), batch))
-            if len(self._readers) > self._READERS_MAX:
-                self._fence_readers(None)
-            size = self._size
-        probs = np.full(batch_size, 1.0 / size)
         return keys, batch, probs
 
 

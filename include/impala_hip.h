@@ -273,6 +273,12 @@ typedef struct {
   const void* const* behaviour_logits;
 } impala_rows;
 int impala_stage_rows(impala_learner* h, const impala_rows* rows, int n, int slot);
+/* The same staging run by the handle's staging thread: returns once the row pointers are
+ * copied, before the host collate; the rows must stay unchanged until impala_stage_wait(slot).
+ * impala_slot_batch / impala_stage_wait on the slot (and every other staging call) first wait
+ * for its job, and report the job's failure if it failed.  The host's collate of step k+1 then
+ * runs beside the caller's enqueue of step k (ImpalaLearner's prefetch). */
+int impala_stage_rows_async(impala_learner* h, const impala_rows* rows, int n, int slot);
 int impala_stage_wait(impala_learner* h, int slot);
 int impala_slot_batch(impala_learner* h, int slot, void* stream, impala_batch* out);
 int impala_slot_release(impala_learner* h, int slot, void* stream);

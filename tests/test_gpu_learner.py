@@ -451,25 +451,24 @@ def test_whole_model_checkpoint_after_learner_step(tmp_path):
     assert torch.equal(lg0, lg1) and torch.equal(v0, v1)
 
 
-@pytest.mark.parametrize("h2d", ["default", "sdma_only"])
-def test_pinned_replay_rows_staged_in_place_match_device_batches(h2d, monkeypatch):
-    """ImpalaLearner over a PinnedReplayBuffer: each step's B trajectories are copied by
-    impala_stage_rows straight from the page-locked arena rows (one SDMA copy per row, the small
-    fields collated by the host).  An actor-side append overwrites the oldest arena row before
-    every step, so rows the previous step staged are rewritten while the learner runs ahead;
-    the replay fences them first.  Weights and metrics must be bitwise those of the same
-    trajectories (as sampled) handed over already collated in HBM."""
+@pytest.mark.parametrize("mode", ["collate", "rows"])
+def test_replay_rows_staged_match_device_batches(mode, monkeypatch):
+    """ImpalaLearner over the host ReplayBuffer: each step's B trajectories are staged by
+    impala_stage_rows from their own host rows -- collated by the library's thread pool into the
+    slot's page-locked block (default), or one SDMA copy per row (IMPALA_STAGE_ROWS=rows).  An
+    actor-side append replaces the oldest trajectory before every step while the learner
+    prefetches ahead.  Weights and metrics must be bitwise those of the same trajectories (as
+    sampled) handed over already collated in HBM."""
     dev = _dev()
-    for k, v in H2D_MODES[h2d].items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("IMPALA_STAGE_ROWS", mode)
     from impala_amd.engine import Engine
     from impala_amd.learner import ImpalaLearner
     from impala_amd.model import AtariPPOModel
-    from impala_amd.replay import PinnedReplayBuffer
+    from impala_amd.replay import ReplayBuffer
     B, T, A, C, steps = 4, 20, 15, 6, 8
     trajs = [ref_cpu.to_trajectories(*ref_cpu.synthetic_batch(1, T, A, seed=700 + i))[0]
              for i in range(C + steps)]
-    rb = PinnedReplayBuffer(capacity=C, rollout_length=T, num_actions=A, seed=4)
+    rb = ReplayBuffer(capacity=C, seed=4)
     for i in range(C):
         rb.append(trajs[i])
     seen = []
@@ -477,6 +476,7 @@ def test_pinned_replay_rows_staged_in_place_match_device_batches(h2d, monkeypatc
 
     def recording_sample(n):
         keys, batch, probs = sample(n)
+        assert batch.row_ptrs is not None
         seen.append(keys.copy())
         return keys, batch, probs
 
@@ -486,17 +486,17 @@ def test_pinned_replay_rows_staged_in_place_match_device_batches(h2d, monkeypatc
     mets = []
     for s in range(steps):
         mets.append(ln.train_step())
-        rb.append(trajs[C + s])  # overwrites the oldest row while step s may still be staging
+        rb.append(trajs[C + s])  # replaces the oldest trajectory (the learner sampled ahead)
     m2 = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
     e2 = Engine(m2, batch_size=B, rollout_length=T)
     m2._train_engine = e2
-    for s, keys in enumerate(seen):
+    for s, (keys, met) in enumerate(zip(seen, mets)):  # (the last sample is the prefetch)
         items = [trajs[int(k)] for k in keys]
         b = [torch.stack([it[j] for it in items]).to(dev) for j in range(5)]
         b = [x.squeeze(-1) if j in (1, 2, 3) else x for j, x in enumerate(b)]
         e2.train_step(*[x.contiguous() for x in b])
         torch.cuda.synchronize()
-        assert float(mets[s]["train/loss"]) == float(e2.metrics[0]), s
+        assert float(met["train/loss"]) == float(e2.metrics[0]), s
     torch.cuda.synchronize()
     assert torch.equal(m1.flat, m2.flat)
 
@@ -531,3 +531,34 @@ def test_agent_train_over_learner_floats_match_device_metrics():
             assert st[k]["count"] == 5
             assert abs(st[k]["mean"] - sum(g[k] for g in got) / 5) <= 1e-6 * (1 + abs(st[k]["mean"]))
             assert st[k]["min"] == min(g[k] for g in got) and st[k]["max"] == max(g[k] for g in got)
+
+
+@pytest.mark.parametrize("kind", ["device", "host_list"])
+def test_learner_prefetch_matches_sampling_inside_the_step(kind):
+    """ImpalaLearner(prefetch=1) samples and stages step k+1's batch right after step k is
+    enqueued; with no appends in between it samples the same sequence as prefetch=0 (the
+    reference's order, learning.py:121), so weights and metrics are bitwise equal, for each
+    replay the learner can be given."""
+    dev = _dev()
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    from impala_amd.replay import DeviceReplayBuffer, ReplayBuffer
+    B, T, A, C, steps = 4, 20, 15, 12, 5
+    trajs = [ref_cpu.to_trajectories(*ref_cpu.synthetic_batch(1, T, A, seed=800 + i))[0]
+             for i in range(C)]
+
+    def run(prefetch):
+        rb = {"device": lambda: DeviceReplayBuffer(C, T, A, device=dev, seed=9),
+              "host_list": lambda: ReplayBuffer(C, seed=9)}[kind]()
+        for t in trajs:
+            rb.append(t)
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+        ln = ImpalaLearner(m, rb, batch_size=B, rollout_length=T, prefetch=prefetch)
+        losses = [float(ln.train_step()["train/loss"]) for _ in range(steps)]
+        torch.cuda.synchronize()
+        return m.flat.clone(), losses
+
+    p0, l0 = run(0)
+    p1, l1 = run(1)
+    assert l0 == l1
+    assert torch.equal(p0, p1)

@@ -135,13 +135,12 @@ def test_replay_circular_uniform_sampling():
     assert all(2 <= f <= 6 for f in fills)
 
 
-def test_pinned_replay_rows_are_arena_views_with_addresses():
-    """PinnedReplayBuffer (the host arena the learner's impala_stage_rows reads in place):
-    sample returns the reference's list of trajectories as views into the arena plus each
-    row's address; overwriting a row a tracked batch still reads calls that batch's fence
-    first."""
-    from impala_amd.replay import PinnedReplayBuffer, RowBatch
-    rb = PinnedReplayBuffer(capacity=5, rollout_length=20, num_actions=15, seed=1)
+def test_replay_rows_carry_their_addresses():
+    """ReplayBuffer.sample returns the reference's list of trajectories as a RowBatch that also
+    carries each row's host address and layout key (what impala_stage_rows reads); a sample
+    that includes a non-contiguous trajectory carries none."""
+    from impala_amd.replay import RowBatch
+    rb = ReplayBuffer(capacity=5, seed=1)
     for i in range(7):
         t = _traj(fill=i)
         t[2] = torch.full((20, 1), float(i))
@@ -149,18 +148,18 @@ def test_pinned_replay_rows_are_arena_views_with_addresses():
     keys, batch, probs = rb.sample(4)
     assert isinstance(batch, RowBatch) and len(batch) == 4 and np.allclose(probs, 0.2)
     assert all(k >= 2 for k in keys)
-    for b, item in enumerate(batch):  # reference format, and the views' addresses
-        assert item[0].shape == (20, 3, 64, 64) and item[1].shape == (20, 1)
-        assert item[4].shape == (20, 15) and item[1].dtype == torch.int64
+    assert batch.row_key == ((torch.uint8, torch.int64, torch.float32, torch.float32, torch.float32),
+                             (20 * 3 * 64 * 64, 20 * 8, 20 * 4, 20 * 4, 20 * 15 * 4))
+    for b, item in enumerate(batch):
         assert int(item[0][0, 0, 0, 0]) == int(keys[b]) == int(item[2][0, 0])
         for f in range(5):
             assert int(batch.row_ptrs[f][b]) == item[f].data_ptr()
-    fenced = []
-    batch.fence = lambda: fenced.append(1)
-    slot = rb._cursor  # the next append overwrites this row
-    rb.append(_traj(fill=9))
-    assert fenced == ([1] if any(item[0].data_ptr() == rb.fields[0][slot].data_ptr()
-                                 for item in batch) else [])
+    odd = _traj(fill=9)
+    odd[4] = torch.zeros(15, 20).t()  # non-contiguous logits
+    rb2 = ReplayBuffer(capacity=1, seed=0)
+    rb2.append(odd)
+    _, b2, _ = rb2.sample(1)
+    assert b2.row_ptrs is None and b2.row_key is None
 
 
 def test_agent_host_floats_one_copy_per_vector():
