@@ -844,7 +844,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   // FC weight-gradient splits: 96 workgroups for bf16; fp32 128 (8 splits: fc_bwd 20.3 us and
   // the reduction 7.55 against 20.7 / 7.75 for 256 workgroups, 27.8 us for 64;
   // tools/var_specs/{fc32b,spfc32}.py)
-  h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), h->bf16 ? 96 : 128);
+  int fc_wg = h->bf16 ? 96 : 128;
+  if (const char* e = std::getenv("IMPALA_FC_WG")) fc_wg = std::max(16, std::atoi(e));
+  h->spfc = plan_split(N, (FLAT / 256) * (HID / 64), fc_wg);
   // one-split FC weight gradient written straight into the canonical gradient (opt-in,
   // IMPALA_FC_DIRECT=1, up to 8192 frames): it drops the 6.3 MB FC slab and 256 reduction
   // workgroups, but the one-split GEMM is latency-bound on its per-CU load concurrency and the

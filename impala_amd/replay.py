@@ -149,11 +149,17 @@ class DeviceReplayBuffer(ReplayBuffer):
         self._st_next = 0
         self._stream = torch.cuda.Stream(device=d)
         self._pending: List[torch.cuda.Event] = []
-        # the stream of the last gather enqueued by sample(): an append must not overwrite a
-        # slot that a queued gather still reads, so its copy waits for an event recorded on that
-        # stream at append time (it follows every gather enqueued so far; recorded only when an
-        # append comes, so a learner sampling with no appends gets nothing but its gathers)
+        # An append must not overwrite a slot that a queued gather still reads.  sample() numbers
+        # its gathers (_gen) and marks the slots each one reads (_slot_gen); an append into a
+        # slot read by a gather not yet fenced records ONE event on the gathers' stream (it
+        # follows every gather enqueued so far) and its copy waits for it; later appends into
+        # slots read before that fence wait for the same event.  So the learner's stream gets
+        # at most one event per sample, and none while nothing is appended.
         self._read_stream = None
+        self._gen = 0
+        self._slot_gen = np.zeros(self.capacity, dtype=np.int64)
+        self._fence_gen = 0
+        self._fence_ev: Optional[torch.cuda.Event] = None
 
     def append(self, item: Sequence[torch.Tensor]) -> int:
         s, a, r, g, mu = item
@@ -172,10 +178,13 @@ class DeviceReplayBuffer(ReplayBuffer):
             sm[:, 3:].copy_(mu.reshape(T, self.A))
             slot = self._cursor
             with torch.cuda.stream(self._stream):
-                if self._read_stream is not None:
-                    read = torch.cuda.Event()
-                    read.record(self._read_stream)
-                    self._stream.wait_event(read)
+                read_gen = int(self._slot_gen[slot])
+                if read_gen > self._fence_gen:  # read by a gather not yet fenced
+                    fence = torch.cuda.Event()
+                    fence.record(self._read_stream)
+                    self._fence_ev, self._fence_gen = fence, self._gen
+                if read_gen > 0:
+                    self._stream.wait_event(self._fence_ev)
                 self.obs[slot].copy_(self._st_obs[j], non_blocking=True)
                 self.act[slot].copy_(self._st_act[j], non_blocking=True)
                 small = sm.to(self.device, non_blocking=True)
@@ -200,10 +209,10 @@ class DeviceReplayBuffer(ReplayBuffer):
         The sampled slot indices travel in the gather launch's own arguments
         (impala_gather_rows_hidx), so the learner's stream gets the gather and nothing else: no
         index upload, no event, and nothing here ever waits on the device.  The lock is held
-        from picking the slots until the gather is enqueued and its stream published as
-        ``_read_stream``: an append either lands before -- its H2D event is among the
-        ``pending`` the gather waits for -- or after, and then its copy waits for an event
-        recorded on that stream behind this gather.  No append can slip between the two and
+        from picking the slots until the gather is enqueued and its slots marked with its
+        generation: an append either lands before -- its H2D event is among the ``pending``
+        the gather waits for -- or after, and then its copy waits for a fence event recorded
+        behind this gather (see ``__init__``).  No append can slip between the two and
         overwrite a slot the gather is reading."""
         from impala_amd.engine import gather_rollouts
         cur = torch.cuda.current_stream(self.device) if stream is None else stream
@@ -216,6 +225,8 @@ class DeviceReplayBuffer(ReplayBuffer):
             batch = gather_rollouts((self.obs, self.act, self.rew, self.disc, self.mu), idx,
                                     stream)
             self._read_stream = cur
+            self._gen += 1
+            self._slot_gen[idx] = self._gen
             size = self._size
         probs = np.full(batch_size, 1.0 / size)
         return keys, batch, probs
