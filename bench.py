@@ -472,7 +472,7 @@ def run_learner_loop(args, dev, headline_ms):
                         collated by the library's thread pool into a page-locked slot and
                         copied by SDMA (impala_stage_rows).
     Each with sync_every 1 (the reference: the metrics read every step) and 100; the learner
-    prefetches the next batch (ImpalaLearner prefetch=1, the default).  Per-step device times
+    prefetches two batches ahead (ImpalaLearner prefetch=2, the default).  Per-step device times
     from the step clock (each step's first learner kernel stamps it)."""
     from impala_amd.agent import DistributedAgent
     from impala_amd.learner import ImpalaLearner
@@ -957,10 +957,14 @@ def main():
             out["dp_variants"] = dp_variants(args, B, T, A, dev, dist, world, batch)
         except Exception as ex:  # noqa: BLE001
             out["dp_variants"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
-    if not args.no_host_staged:
-        out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
+    # the drop-in loop before host_staged: its engines are closed afterwards, and the headline
+    # engine's staging ring (host_staged's two copy streams) does not exist yet.  A process's
+    # streams share GPU_MAX_HW_QUEUES (4) hardware queues; with the ring's streams alive the
+    # loop's copies ran 0.42 instead of 0.30-0.32 ms per step (profiles/r06v)
     if world == 1 and dist is None and not ppo and not args.no_learner_loop:
         out["learner_loop"] = run_learner_loop(args, dev, round(ms_step, 4))
+    if not args.no_host_staged:
+        out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if ppo:
             out["cpu_baseline"] = cpu_baseline_ppo(B, A, args.cpu_seconds,

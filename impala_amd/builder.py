@@ -129,7 +129,7 @@ class ImpalaBuilder(Builder):
                              dtype=self._learner_cfg("dtype", None), process_group=pg,
                              world_size=ws,
                              vtrace_grad_mode=self._learner_cfg("vtrace_grad_mode", None),
-                             prefetch=1 if int(self.cfg.training.get("prefetch", 1) or 0) > 0 else 0,
+                             prefetch=min(2, max(0, int(self.cfg.training.get("prefetch", 2) or 0))),
                              **kw)
 
     def make_network(self, env_spec=None):  # builder.py:51-59

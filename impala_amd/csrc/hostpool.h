@@ -4,8 +4,13 @@
 // a C2 batch in ~1 ms (below PCIe's 0.3 ms for the same bytes).  Host code only.
 #pragma once
 
+#include <pthread.h>
+#include <sched.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <condition_variable>
+#include <cstdio>
 #include <deque>
 #include <string>
 #include <cstdint>
@@ -48,10 +53,69 @@ inline void copy_stream(char* dst, const char* src, size_t n) {
 #endif
 }
 
+// The CPUs of a NUMA node, within the process's affinity set (empty when the topology cannot be
+// read): where the staging threads run (impala_stage_rows_async; impala.hip stage_cpus).
+// node < 0: the node of the CPU the calling thread runs on
+inline std::vector<int> local_node_cpus(int node = -1) {
+  std::vector<int> out;
+#ifndef __HIP_DEVICE_COMPILE__
+  if (node < 0) {
+    const int cpu = sched_getcpu();
+    if (cpu < 0) return out;
+    for (int n = 0; n < 64 && node < 0; ++n) {
+      char path[96];
+      std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", cpu, n);
+      if (access(path, F_OK) == 0) node = n;
+    }
+  }
+  if (node < 0) return out;
+  char path[96];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return out;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) {
+    std::fclose(f);
+    return out;
+  }
+  int a = 0, b = 0;
+  char sep = 0;
+  while (std::fscanf(f, "%d", &a) == 1) {
+    b = a;
+    if (std::fscanf(f, "%c", &sep) == 1 && sep == '-') {
+      if (std::fscanf(f, "%d", &b) != 1) break;
+      if (std::fscanf(f, "%c", &sep) != 1) sep = 0;
+    }
+    for (int c = a; c <= b; ++c)
+      if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    if (sep != ',') break;
+  }
+  std::fclose(f);
+#endif
+  return out;
+}
+
+// pin the calling thread to `cpus` (no-op when empty)
+inline void pin_to(const std::vector<int>& cpus) {
+#ifndef __HIP_DEVICE_COMPILE__
+  if (cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus) CPU_SET(c, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+#endif
+}
+
 class HostPool {
  public:
-  explicit HostPool(int nthreads) {
-    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
+  // nthreads workers, kept on `cpus` (the creating thread's NUMA node, local_node_cpus) when
+  // non-empty
+  explicit HostPool(int nthreads, std::vector<int> cpus = {}) {
+    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this, cpus] {
+      pin_to(cpus);
+      worker();
+    });
   }
   ~HostPool() {
     {
@@ -118,7 +182,10 @@ class HostPool {
 // calls that use the slot.  A job's status and error text are kept for the next waiter.
 class Stager {
  public:
-  Stager() : th_([this] { loop(); }) {}
+  explicit Stager(std::vector<int> cpus = {}) : th_([this, cpus] {
+    pin_to(cpus);
+    loop();
+  }) {}
   ~Stager() {
     {
       std::lock_guard<std::mutex> lk(mu_);

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <cctype>
 #include <memory>
 #include <new>
 #include <string>
@@ -1617,6 +1618,28 @@ int impala_stage_init(impala_learner* h, int nslots) {
 }
 
 namespace {
+// Where the staging threads run (IMPALA_STAGE_PIN): "gpu" (default) the CPUs of the NUMA node
+// the device's PCIe link hangs off, so the page-locked blocks they first touch and fill sit
+// next to the DMA engines that read them; "caller" the calling thread's node; "0" anywhere.
+std::vector<int> stage_cpus(const impala_learner* h) {
+  const char* pin = std::getenv("IMPALA_STAGE_PIN");
+  if (pin && pin[0] == '0') return {};
+  if (pin && std::strcmp(pin, "caller") == 0) return impala_host::local_node_cpus();
+  char bus[64] = {};
+  int node = -1;
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), h->device) == hipSuccess) {
+    for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    if (FILE* f = std::fopen(path.c_str(), "r")) {
+      if (std::fscanf(f, "%d", &node) != 1) node = -1;
+      std::fclose(f);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  return impala_host::local_node_cpus(node);  // (node -1: the caller's)
+}
+
 // the staging jobs of `slot` (every slot when < 0) queued by impala_stage_rows_async have run;
 // a failed one's status is returned here
 int wait_staged(impala_learner* h, int slot) {
@@ -1753,7 +1776,7 @@ int impala_stage_rows_async(impala_learner* h, const impala_rows* rows, int n, i
   if (int r = check_rows(h, rows, n, slot)) return r;
   if (int r = wait_staged(h, slot)) return r;  // the slot's previous job
   if (!h->stager) {
-    h->stager = new (std::nothrow) impala_host::Stager();
+    h->stager = new (std::nothrow) impala_host::Stager(stage_cpus(h));
     if (!h->stager) return fail(IMPALA_E_STATE, "impala_stage_rows_async: staging thread");
   }
   // the job owns copies of the five pointer arrays; the rows themselves stay the caller's
@@ -1786,7 +1809,12 @@ int stage_rows_now(impala_learner* h, const impala_rows* rows, int n, int slot) 
   for (int f = 0; f < 5; ++f) off[f + 1] = off[f] + ((N * rb[f] / T + 255) & ~(size_t)255);
   if (!s.host_blk) {
     void* p = nullptr;
-    CK(hipHostMalloc(&p, off[5], hipHostMallocMapped | hipHostMallocPortable));
+    // IMPALA_STAGE_HOSTMEM=1: mapped + portable (the round-6 first form); default flags
+    // otherwise (as torch's page-locked tensors, which impala_stage copies from)
+    const char* hm = std::getenv("IMPALA_STAGE_HOSTMEM");
+    const unsigned flags = hm && hm[0] == '1' ? (hipHostMallocMapped | hipHostMallocPortable)
+                                              : hipHostMallocDefault;
+    CK(hipHostMalloc(&p, off[5], flags));
     s.host_blk = (char*)p;
   }
   // the slot's previous copies (out of its host block too) have finished before it is rewritten
@@ -1814,7 +1842,7 @@ int stage_rows_now(impala_learner* h, const impala_rows* rows, int n, int slot) 
   if (collate && !h->pool) {
     int nt = 7;
     if (const char* e = std::getenv("IMPALA_STAGE_THREADS")) nt = std::max(0, std::atoi(e) - 1);
-    h->pool = new (std::nothrow) impala_host::HostPool(nt);
+    h->pool = new (std::nothrow) impala_host::HostPool(nt, stage_cpus(h));
     if (!h->pool) return fail(IMPALA_E_STATE, "impala_stage_rows: thread pool");
   }
   if (h->pool && collate) {

@@ -7,6 +7,7 @@ all-reduce of the flat gradient + ``impala_apply_update``.
 """
 from __future__ import annotations
 
+import collections
 import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Sequence, Tuple
@@ -65,17 +66,18 @@ class ImpalaLearner(Learner):
                  learning_starts: Optional[int] = None, model_push_period: int = 4,
                  rollout_length: int = 20, dtype: Optional[str] = None,
                  process_group=None, world_size: Optional[int] = None,
-                 vtrace_grad_mode: Optional[str] = None, prefetch: int = 1):
+                 vtrace_grad_mode: Optional[str] = None, prefetch: int = 2):
         """The reference's constructor (learning.py:88-96) plus keyword-only extensions:
         ``rollout_length``, ``dtype`` ("fp32" | "bf16"), the data-parallel ``process_group`` /
         ``world_size``, ``vtrace_grad_mode`` -- what the V-trace backward treats as constant
         (``_lib.VTRACE_GRAD_MODES``; default "sg_advantage": targets and pg advantages constant,
         SURVEY.md §8(c); "sg_targets" / "sg_none" for rlax's stop_target_gradients=True / False
-        with the advantage live) -- and ``prefetch``: 1 (default) samples and stages the next
-        step's batch right after this step is enqueued, so the sampling, the host collate and
-        the H2D copies run while the GPU computes (the reference's replay client prefetches
-        its samples the same way, conf/config.yaml ``prefetch: 5``); 0 samples inside each
-        train_step, as learning.py:121 does."""
+        with the advantage live) -- and ``prefetch``: the batches sampled and staged ahead,
+        right after a step is enqueued (default 2), so the sampling, the host collate and the
+        H2D copies of the next steps run while the GPU computes (the reference's replay client
+        prefetches its samples the same way, conf/config.yaml ``prefetch: 5``); host batches
+        then use prefetch + 1 staging slots.  0 samples inside each train_step, as
+        learning.py:121 does."""
         self._model = model
         self._replay_buffer = replay_buffer
         if optimizer is None:
@@ -98,8 +100,9 @@ class ImpalaLearner(Learner):
                 world_size = dist.get_world_size(process_group)
         self._world_size = int(world_size)
         self._device = None
-        self._prefetch = int(prefetch) > 0
-        self._next = None  # the prefetched (batch, slot, n_samples, sample seconds)
+        self._prefetch = max(0, int(prefetch))
+        # the prefetched (batch, slot, n_samples, sample seconds), oldest first
+        self._queue = collections.deque()
         self._step_count = 0
         self._step_counter = 0
         self.can_train = True
@@ -148,7 +151,7 @@ class ImpalaLearner(Learner):
         the step and the device's work."""
         e = self._engine
         if getattr(e, "n_slots", 0) == 0:
-            e.stage_init(2)
+            e.stage_init(max(2, self._prefetch + 1))  # the prefetched batches + the step's
             self._host_bufs = [None] * e.n_slots
             self._row_batches = [None] * e.n_slots
         self._slot = slot = (getattr(self, "_slot", -1) + 1) % e.n_slots
@@ -206,19 +209,20 @@ class ImpalaLearner(Learner):
             batch = (self._engine.slot_batch(slot),)
         return batch, slot, n_samples, sample_s
 
-    def _start_prefetch(self):
-        """Sample and stage the next step's batch now (a device replay's gather goes on the
-        learner's stream behind this step; a host batch's collate and copies are handed to the
-        library's staging thread).  A replay that cannot give a batch now is asked again,
-        synchronously, by the next call (which raises if it still cannot)."""
-        try:
-            self._next = self._fetch()
-        except Exception:  # noqa: BLE001 -- re-raised by the next call's own sample
-            self._next = None
+    def _refill(self):
+        """Sample and stage batches until `prefetch` are queued (a device replay's gathers go on
+        the learner's stream behind this step; host batches' collates and copies are handed to
+        the library's staging thread, which runs them back to back).  A replay that cannot give
+        a batch now is asked again by the next call, synchronously when nothing is queued
+        (raising there if it still cannot)."""
+        while len(self._queue) < self._prefetch:
+            try:
+                self._queue.append(self._fetch())
+            except Exception:  # noqa: BLE001 -- re-raised by a later call's own sample
+                break
 
     def _take_next(self):
-        nxt, self._next = self._next, None
-        return nxt if nxt is not None else self._fetch()
+        return self._queue.popleft() if self._queue else self._fetch()
 
     def train_step(self):  # learning.py:119-138
         t0 = time.perf_counter()
@@ -228,8 +232,7 @@ class ImpalaLearner(Learner):
         if slot is not None:
             self._engine.slot_release(slot)
         t2 = time.perf_counter()
-        if self._prefetch:  # the next step's batch, while this step runs on the device
-            self._start_prefetch()
+        self._refill()  # the next steps' batches, while this step runs on the device
         update_time = 0
         self._step_count += 1
         self._step_counter = self._step_count

@@ -535,8 +535,8 @@ def test_agent_train_over_learner_floats_match_device_metrics():
 
 @pytest.mark.parametrize("kind", ["device", "host_list"])
 def test_learner_prefetch_matches_sampling_inside_the_step(kind):
-    """ImpalaLearner(prefetch=1) samples and stages step k+1's batch right after step k is
-    enqueued; with no appends in between it samples the same sequence as prefetch=0 (the
+    """ImpalaLearner(prefetch=1 or 2) samples and stages the next steps' batches right after a
+    step is enqueued; with no appends in between it samples the same sequence as prefetch=0 (the
     reference's order, learning.py:121), so weights and metrics are bitwise equal, for each
     replay the learner can be given."""
     dev = _dev()
@@ -559,6 +559,7 @@ def test_learner_prefetch_matches_sampling_inside_the_step(kind):
         return m.flat.clone(), losses
 
     p0, l0 = run(0)
-    p1, l1 = run(1)
-    assert l0 == l1
-    assert torch.equal(p0, p1)
+    for depth in (1, 2):
+        p1, l1 = run(depth)
+        assert l0 == l1, depth
+        assert torch.equal(p0, p1), depth
