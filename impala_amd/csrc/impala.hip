@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cctype>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -713,6 +714,58 @@ void drop_graphs(impala_learner* h) {
   }
 }
 
+// The staging rings' copy streams, shared by every handle on a device that asks for the same
+// number: a process's streams share GPU_MAX_HW_QUEUES (4) hardware queues, and each handle's own
+// pair of copy streams took a share of them (a second handle's staging ran at 0.42 instead of
+// 0.30 ms per step beside the first's, profiles/r06w).  Reference-counted; the last handle's
+// release destroys them.
+struct SharedH2D {
+  int device = -1, n = 0, refs = 0;
+  hipStream_t s[impala_learner::kMaxH2D] = {};
+};
+std::mutex g_h2d_mu;
+SharedH2D g_h2d[16];
+
+int acquire_h2d(impala_learner* h, int n) {
+  std::lock_guard<std::mutex> lk(g_h2d_mu);
+  SharedH2D* e = nullptr;
+  for (auto& x : g_h2d)
+    if (x.refs > 0 && x.device == h->device && x.n == n) e = &x;
+  if (!e) {
+    for (auto& x : g_h2d)
+      if (x.refs == 0) {
+        e = &x;
+        break;
+      }
+    if (!e) return fail(IMPALA_E_STATE, "impala_stage_init: too many staging stream sets");
+    e->device = h->device;
+    e->n = 0;
+    for (int i = 0; i < n; ++i) {
+      if (hipStreamCreateWithFlags(&e->s[i], hipStreamNonBlocking) != hipSuccess) {
+        for (int j = 0; j < i; ++j) (void)hipStreamDestroy(e->s[j]);
+        return fail(IMPALA_E_STATE, "impala_stage_init: hipStreamCreate failed");
+      }
+    }
+    e->n = n;
+  }
+  ++e->refs;
+  for (int i = 0; i < n; ++i) h->h2d_s[i] = e->s[i];
+  return 0;
+}
+
+void release_h2d(impala_learner* h) {
+  if (!h->n_h2d) return;
+  std::lock_guard<std::mutex> lk(g_h2d_mu);
+  for (auto& x : g_h2d)
+    if (x.refs > 0 && x.device == h->device && x.n == h->n_h2d && x.s[0] == h->h2d_s[0]) {
+      if (--x.refs == 0) {
+        for (int i = 0; i < x.n; ++i) (void)hipStreamDestroy(x.s[i]);
+        x = SharedH2D{};
+      }
+      break;
+    }
+}
+
 void free_ring(impala_learner* h) {
   if (h->stager) {  // no staging job may still be writing into the ring
     std::string m;
@@ -956,7 +1009,9 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   // on MI355X / ROCm 7 the replayed step ran slower on the device than direct launches
   // (174 vs 165 us), so direct launches are the default
   if (const char* g = std::getenv("IMPALA_GRAPH")) h->use_graph = g[0] == '1';
-  if (hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking) != hipSuccess) {
+  // the capture stream exists only for graph replay: every stream a process creates takes a
+  // share of its GPU_MAX_HW_QUEUES hardware queues (profiles/r06w)
+  if (h->use_graph && hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking) != hipSuccess) {
     impala_destroy(h);
     return fail(IMPALA_E_STATE, "hipStreamCreate (capture stream) failed");
   }
@@ -1100,10 +1155,9 @@ int impala_destroy(impala_learner* h) {
   (void)hipDeviceSynchronize();  // replays may still be in flight on the caller's streams
   drop_graphs(h);
   free_ring(h);
-  for (int i = 0; i < h->n_h2d; ++i) {
-    (void)hipStreamDestroy(h->h2d_s[i]);
+  release_h2d(h);  // (the shared copy streams; the join events are the handle's)
+  for (int i = 0; i < h->n_h2d; ++i)
     if (h->h2d_join[i]) (void)hipEventDestroy(h->h2d_join[i]);
-  }
   for (auto& t : h->timers) {
     for (int i = 0; i < 2 * t.cap; ++i) (void)hipEventDestroy(t.ev[i]);
     delete[] t.ev;
@@ -1575,11 +1629,9 @@ int impala_stage_init(impala_learner* h, int nslots) {
     int n = h->h2d_pull_wg > 0 ? 1 : 2;
     if (const char* e = std::getenv("IMPALA_H2D_STREAMS")) n = std::atoi(e);
     n = std::max(1, std::min(n, (int)impala_learner::kMaxH2D));
-    for (int i = 0; i < n; ++i) {
-      CK(hipStreamCreateWithFlags(&h->h2d_s[i], hipStreamNonBlocking));
-      h->n_h2d = i + 1;
-      CK(hipEventCreateWithFlags(&h->h2d_join[i], hipEventDisableTiming));
-    }
+    if (int r = acquire_h2d(h, n)) return r;
+    h->n_h2d = n;
+    for (int i = 0; i < n; ++i) CK(hipEventCreateWithFlags(&h->h2d_join[i], hipEventDisableTiming));
     h->h2d = h->h2d_s[0];
   }
   const size_t N = (size_t)h->N;
