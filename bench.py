@@ -39,6 +39,7 @@ Also reported, all from the same run:
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -310,7 +311,18 @@ class StepClock:
         self.eng, self.n = eng, n
         self.host = [] if host else None
         self._t = None
+        self.gc = []  # (generation, ms) of the Python collections inside the region (host=True)
+        self._gc0 = None
+        if host:
+            gc.callbacks.append(self._on_gc)
         eng.step_clock_start(n)
+
+    def _on_gc(self, phase, info):
+        if phase == "start":
+            self._gc0 = time.perf_counter()
+        elif self._gc0 is not None:
+            self.gc.append((info.get("generation", -1), (time.perf_counter() - self._gc0) * 1e3))
+            self._gc0 = None
 
     def mark(self):
         """Before every step and after the last (host times only)."""
@@ -323,6 +335,8 @@ class StepClock:
     def close(self):
         """After the last step, inside the timed region: the closing stamp."""
         self.eng.step_clock_end()
+        if self._on_gc in gc.callbacks:
+            gc.callbacks.remove(self._on_gc)
 
     def summary(self, digits=4):
         """-> per-step statistics in ms (call after the region's final synchronize); the raw
@@ -336,6 +350,10 @@ class StepClock:
             out["host_ms_per_iter_max"] = round(float(h.max()), digits)
             if len(h) <= 256:
                 out["host_ms"] = [round(float(x), digits) for x in h]
+            out["python_gc"] = {"collections": len(self.gc),
+                                "by_generation": [sum(1 for g, _ in self.gc if g == k) for k in range(3)],
+                                "ms": round(sum(t for _, t in self.gc), digits),
+                                "max_ms": round(max((t for _, t in self.gc), default=0.0), digits)}
         return out
 
 
@@ -497,7 +515,7 @@ def run_learner_loop(args, dev, headline_ms):
         rec = {}
         for sync in (1, 100):
             ag = DistributedAgent(None, ln, sync_every=sync)
-            ag.train(max(args.warmup, 5))
+            ag.train(args.loop_warmup if args.loop_warmup is not None else max(args.warmup, 5))
             torch.cuda.synchronize()
             clock = StepClock(ln.engine, args.loop_steps, host=True)
             step = ln.train_step
@@ -815,6 +833,9 @@ def main():
                          "-> replay, N=1 IMPALA only)")
     ap.add_argument("--loop-steps", type=int, default=100,
                     help="train_steps per learner_loop record")
+    ap.add_argument("--loop-warmup", type=int, default=None,
+                    help="untimed train_steps before each learner_loop record (default: "
+                         "max(--warmup, 5))")
     ap.add_argument("--loop-capacity", type=int, default=1000,
                     help="replay capacity of the learner_loop records (builder.py:30-36)")
     ap.add_argument("--algo", default="impala", choices=["impala", "ppo", "sac"],

@@ -1533,7 +1533,7 @@ int impala_gather_rows_hidx(const void* const* src, void* const* dst, const size
 }
 
 // Prime the copy path at init: the learner's staging loop (ImpalaLearner._stage_host) for
-// IMPALA_STAGE_PRIME rounds (default 24, 0 = off) on a page-locked scratch batch, with a
+// IMPALA_STAGE_PRIME rounds (default 24, 0 = off) in each of two shapes on a page-locked scratch batch, with a
 // 250 us spin kernel on a private stream standing in for each step.  An H2D hipMemcpyAsync is
 // given an SDMA engine by the runtime at issue time (hsa_amd_memory_get_preferred_copy_engine /
 // copy_engine_status, then hsa_amd_memory_async_copy_on_engine), and the first copy given an
@@ -1578,6 +1578,22 @@ int prime_copy_path(impala_learner* h) {
       e = hipGetLastError();
     }
     if (r == 0 && e == hipSuccess) e = hipEventRecord(h->ring[s].done, cs);  // slot_release(s)
+  }
+  // ... then the same rounds over every slot with the host running ahead, as a loop that reads
+  // its metrics only every k steps does (DistributedAgent sync_every > 1): the host waits only
+  // for a slot's previous copy (the collate's wait before it rewrites the slot's host block), so
+  // every copy is queued behind the event of a step still two slots back.  Without this phase
+  // that loop met one 7 ms queue-creation stall in its first dozen steps (profiles/r06y).
+  for (int k = 0; k < rounds && r == 0 && e == hipSuccess; ++k) {
+    const int s = k % h->n_slots;
+    e = hipEventSynchronize(h->ring[s].ready);
+    if (e == hipSuccess) r = impala_stage(h, &hb, s);
+    if (r == 0 && e == hipSuccess) e = hipStreamWaitEvent(cs, h->ring[s].ready, 0);
+    if (r == 0 && e == hipSuccess) {
+      stage_prime_spin_kernel<<<1, 64, 0, cs>>>(25000);
+      e = hipGetLastError();
+    }
+    if (r == 0 && e == hipSuccess) e = hipEventRecord(h->ring[s].done, cs);
   }
   if (cs) {
     const hipError_t es = hipStreamSynchronize(cs);
