@@ -133,12 +133,23 @@ template <typename T> DEV int wg_prow(int r) { if constexpr (sizeof(T) == 2) ret
 constexpr int F32_ROW_PAD = 8;
 template <typename T> constexpr int tile_pad() { return sizeof(T) == 2 ? 16 : F32_ROW_PAD; }
 template <typename T> constexpr int tile_pad_ak() { return sizeof(T) == 2 ? 16 : 4; }
-template <typename T, int BR, int BC, int BK, int WR, int WC, class Op>
+template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int NP = 1>
 constexpr int gemm_tile_smem() {
   constexpr int LD = BK + tile_pad<T>();
   constexpr int ASZ = Op::A_KMAJOR ? BK * (BR + tile_pad_ak<T>()) : BR * LD;
-  return 2 * (ASZ + BC * LD);
+  return 2 * NP * (ASZ + BC * LD);
 }
+// Split-plane products (NP = 3, bf16): an fp32 operand x is held as three bf16 planes
+// x = hi + mid + lo (split3, exact), plane p of every operand at a fixed element stride from
+// plane 0 (Op::a_ps / b_ps, x_ps / y_ps).  a * b is then the sum of the plane products with
+// (p, q) pairs in the order below, smallest terms first; each plane product is exact in
+// fp32 (8 x 8 significant bits), the MFMA accumulates them in fp32.  kSplitPairs[0..kSplitN)
+// lists (p, q).  9 terms: every product (a * b exact before the fp32 accumulation).
+// Measured for the fp32 FC forward (tools/probe/fc_split.hip, profiles/r06z): 13.6-19.8 us
+// against 12.3 for the f32 MFMA, and 2.4x its rel-L2 error against fp64 (the 9 terms' extra
+// fp32 roundings) -- the three planes triple the staged bytes.  Not used by the library.
+constexpr int kSplitN = 9;
+constexpr int kSplitPairs[9][2] = {{2, 2}, {2, 1}, {1, 2}, {2, 0}, {1, 1}, {0, 2}, {1, 0}, {0, 1}, {0, 0}};
 // PF: K chunks held in registers ahead of the one being computed (1: the next chunk; 2: the
 // next two, for a K loop whose chunks are too short to cover the L2 latency of one fetch).
 // KACC: accumulator chains per output fragment over alternating k-steps, their elements
@@ -150,8 +161,9 @@ constexpr int gemm_tile_smem() {
 // them; the NW partial tiles are summed in wave order through LDS at the end of the tile,
 // and fragment f's epilogue runs on wave f % NW.  Any BR, BC multiple of 16 (e.g. 32 x 48:
 // 216 tiles of the FC forward at N = 1280, one per CU, instead of 320 32 x 32 tiles).
+// NP = 3: split-plane operands (above; plain k loop only: KACC 1, no KW, no TILE_EPI).
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1,
-          bool KW = false>
+          bool KW = false, int NP = 1>
 DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __restrict__ smem) {
   constexpr int NT = 64 * WR * WC;
   constexpr bool AK = Op::A_KMAJOR;
@@ -178,7 +190,9 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
   constexpr int NOWN = (FR * FC + NW - 1) / NW;  // KW: fragments whose epilogue a wave runs
   static_assert(!KW || (KACC == 1 && !Op::TILE_EPI && BR % 16 == 0 && BC % 16 == 0 &&
                         (BK / F::KSTEP) % NW == 0), "KW: whole k-steps per wave per chunk");
-  constexpr int SMEM = 2 * (ASZ + BC * LD);
+  static_assert(NP == 1 || (NP == 3 && sizeof(T) == 2 && KACC == 1 && !KW && !Op::TILE_EPI), "split planes");
+  constexpr int PSZ = ASZ + BC * LD;  // one plane of a buffer (A then B)
+  constexpr int SMEM = 2 * NP * PSZ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
   // staging element e = tid + i*256 of a chunk -> (tile row e / KV, 16-byte vector e % KV)
@@ -202,36 +216,53 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 #pragma unroll
     for (int i = 0; i < NB; ++i) bctx[i] = op.col_ctx(min(fc0 + srow(i), op.C - 1));
   };
-  V ra[PF][NA], rb[PF][NB];
+  V ra[PF][NP][NA], rb[PF][NP][NB];
   auto fetch = [&](int k0, int sl) {
-    if constexpr (AK) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * NT, kr = e / RV, rv = e % RV;
-        ra[sl][i] = F::load(op.a_kptr(k0 + kr, fr0 + rv * VEC, fcw));
+    for (int p = 0; p < NP; ++p) {
+      if constexpr (AK) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int e = tid + i * NT, kr = e / RV, rv = e % RV;
+          const T* ap = op.a_kptr(k0 + kr, fr0 + rv * VEC, fcw);
+          if constexpr (NP > 1) ap += p * op.a_ps;
+          ra[sl][p][i] = F::load(ap);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const T* ap = arow[i] + k0 + skv(i) * VEC;
+          if constexpr (NP > 1) ap += p * op.a_ps;
+          ra[sl][p][i] = F::load(ap);
+        }
       }
-    } else {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) ra[sl][i] = F::load(arow[i] + k0 + skv(i) * VEC);
+      for (int i = 0; i < NB; ++i) {
+        if constexpr (NP > 1)
+          rb[sl][p][i] = op.load_b(bctx[i], k0 + skv(i) * VEC, p);
+        else
+          rb[sl][p][i] = op.load_b(bctx[i], k0 + skv(i) * VEC);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) rb[sl][i] = op.load_b(bctx[i], k0 + skv(i) * VEC);
   };
   auto stash = [&](int buf, int sl) {
-    T* As = smem + buf * (ASZ + BC * LD);
-    T* Bs = As + ASZ;
-    if constexpr (AK) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * NT, kr = e / RV, rv = e % RV;
-        *reinterpret_cast<V*>(As + wg_prow<T>(kr) * LDA + rv * VEC) = ra[sl][i];
+    for (int p = 0; p < NP; ++p) {
+      T* As = smem + (buf * NP + p) * PSZ;
+      T* Bs = As + ASZ;
+      if constexpr (AK) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int e = tid + i * NT, kr = e / RV, rv = e % RV;
+          *reinterpret_cast<V*>(As + wg_prow<T>(kr) * LDA + rv * VEC) = ra[sl][p][i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + srow(i) * LD + skv(i) * VEC) = ra[sl][p][i];
       }
-    } else {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) *reinterpret_cast<V*>(As + srow(i) * LD + skv(i) * VEC) = ra[sl][i];
+      for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + srow(i) * LD + skv(i) * VEC) = rb[sl][p][i];
     }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<V*>(Bs + srow(i) * LD + skv(i) * VEC) = rb[sl][i];
   };
   const int kl = F::KPL * (lane >> 4);
   set_ctx(ft);
@@ -290,7 +321,7 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
         if (kc + PF == NK) set_ctx(t + vgrid);
         fetch((kc + PF - NK) * BK, sl);
       }
-      const T* As = smem + buf * (ASZ + BC * LD);
+      const T* As = smem + buf * NP * PSZ;
       const T* Bs = As + ASZ;
       auto frags = [&](int kk, V (&a)[TRW], V (&b)[TCW]) {
 #pragma unroll
@@ -320,6 +351,32 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
             for (int i = 0; i < FR; ++i)
 #pragma unroll
               for (int j = 0; j < FC; ++j) accw[i][j] = F::mma_e(e, a[i], b[j], accw[i][j]);
+        }
+      } else if constexpr (NP > 1) {
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += F::KSTEP) {
+          V a[NP][TRW], b[NP][TCW];
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+#pragma unroll
+            for (int i = 0; i < TRW; ++i) {
+              const T* Ap = As + p * PSZ;
+              if constexpr (AK)
+                a[p][i] = lds_frag_k_sw(Ap + kk * LDA + (wr * TRW + i) * 16, LDA, lane);
+              else
+                a[p][i] = *reinterpret_cast<const V*>(Ap + ((wr * TRW + i) * 16 + (lane & 15)) * LD + kk + kl);
+            }
+#pragma unroll
+            for (int j = 0; j < TCW; ++j)
+              b[p][j] = *reinterpret_cast<const V*>(Bs + p * PSZ + ((wc * TCW + j) * 16 + (lane & 15)) * LD + kk + kl);
+          }
+#pragma unroll
+          for (int q = 0; q < kSplitN; ++q)
+#pragma unroll
+            for (int i = 0; i < TRW; ++i)
+#pragma unroll
+              for (int j = 0; j < TCW; ++j)
+                acc[i][j] = F::mma(a[kSplitPairs[q][0]][i], b[kSplitPairs[q][1]][j], acc[i][j]);
         }
       } else if constexpr (KACC == 1) {
 #pragma unroll
@@ -416,10 +473,10 @@ DEV void gemm_tile_body(const Op& op, int n_rtiles, int vbid, int vgrid, T* __re
 }
 
 template <typename T, int BR, int BC, int BK, int WR, int WC, class Op, int PF = 1, int KACC = 1,
-          bool KW = false>
+          bool KW = false, int NP = 1>
 __global__ __launch_bounds__(64 * WR * WC) void gemm_tile(const Op op, int n_rtiles) {
-  __shared__ __attribute__((aligned(16))) T smem[gemm_tile_smem<T, BR, BC, BK, WR, WC, Op>()];
-  gemm_tile_body<T, BR, BC, BK, WR, WC, Op, PF, KACC, KW>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
+  __shared__ __attribute__((aligned(16))) T smem[gemm_tile_smem<T, BR, BC, BK, WR, WC, Op, NP>()];
+  gemm_tile_body<T, BR, BC, BK, WR, WC, Op, PF, KACC, KW, NP>(op, n_rtiles, (int)blockIdx.x, (int)gridDim.x, smem);
 }
 
 // Weight-gradient GEMM  D[r][c] = sum_m X[m][r] * Y(m, c)  over the m range of split
