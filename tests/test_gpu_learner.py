@@ -184,6 +184,58 @@ def test_host_staging_ring_matches_device_batches(h2d, monkeypatch):
         e2.slot_batch(2)
 
 
+def test_two_handles_share_the_copy_streams():
+    """Two handles on one device share the staging copy streams (impala.hip acquire_h2d: one set
+    per device and stream count, reference-counted).  Interleaved staging of different batches
+    on both still gives each handle bitwise its device-batch result, and a handle keeps staging
+    after the other is closed (the streams outlive the first handle's release)."""
+    dev = _dev()
+    from impala_amd.engine import Engine
+    from impala_amd.model import AtariPPOModel
+    B, T, A, steps = 4, 20, 15, 4
+    batches = {w: [[torch.from_numpy(x) for x in ref_cpu.synthetic_batch(B, T, A, seed=70 + 10 * w + s)]
+                   for s in range(2 * steps)] for w in (0, 1)}
+
+    def make():
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+        e = Engine(m, batch_size=B, rollout_length=T, dtype="fp32")
+        m._train_engine = e
+        return m, e
+
+    refs = []
+    for w in (0, 1):
+        m, e = make()
+        n = 2 * steps if w == 1 else steps
+        for hb in batches[w][:n]:
+            e.train_step(*[t.to(dev) for t in hb])
+        torch.cuda.synchronize()
+        refs.append((m.flat.clone(), e.metrics.clone()))
+        e.close()
+    pinned = {w: [[t.pin_memory() for t in hb] for hb in batches[w]] for w in (0, 1)}
+    (m0, e0), (m1, e1) = make(), make()
+    e0.stage_init(2)
+    e1.stage_init(2)
+    for k in range(steps):  # both rings in flight at once, on the shared streams
+        s = k % 2
+        e0.stage(s, *pinned[0][k])
+        e1.stage(s, *pinned[1][k])
+        e0.train_step(e0.slot_batch(s))
+        e1.train_step(e1.slot_batch(s))
+        e0.slot_release(s)
+        e1.slot_release(s)
+    torch.cuda.synchronize()
+    assert torch.equal(m0.flat, refs[0][0]) and torch.equal(e0.metrics, refs[0][1])
+    e0.close()
+    for k in range(steps, 2 * steps):  # the other handle alone, after the first's release
+        s = k % 2
+        e1.stage(s, *pinned[1][k])
+        e1.train_step(e1.slot_batch(s))
+        e1.slot_release(s)
+    torch.cuda.synchronize()
+    assert torch.equal(m1.flat, refs[1][0]) and torch.equal(e1.metrics, refs[1][1])
+    e1.close()
+
+
 @pytest.mark.parametrize("A", [15, 6])
 def test_native_act_argmax_flags_and_sampling_distribution(A):
     """impala_act (distributed_models.py:21-32): logits / values equal the forward, argmax where
