@@ -1170,6 +1170,7 @@ __global__ __launch_bounds__(256) void act_heads_kernel(const float* __restrict_
 // up to GATHER_HIDX rows, from the launch's own arguments (hidx: no index upload).
 constexpr int GATHER_PIECE = 16384;
 constexpr int GATHER_HIDX = 256;
+static_assert(GATHER_PIECE % (16 * 256) == 0, "whole 16-byte vectors per thread");
 struct GatherArgs {
   const char* src[8];
   char* dst[8];
@@ -1244,9 +1245,24 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const GatherArgs a) {
   char* d = a.dst[f] + (size_t)i * rb + o0;
   const bool al16 = ((((uintptr_t)s) | ((uintptr_t)d) | (uintptr_t)len) & 15) == 0;
   if (al16) {
-    const long long nv = len >> 4;
-    for (long long v = threadIdx.x; v < nv; v += 256)
-      reinterpret_cast<f32x4*>(d)[v] = reinterpret_cast<const f32x4*>(s)[v];
+    // every load of the piece issued before any store (a load-store pair per iteration waited
+    // out one memory round trip each: source and destination may alias as far as the compiler
+    // knows); the replay rows are read once (nontemporal)
+    constexpr int NVT = GATHER_PIECE / 16 / 256;
+    const int nv = (int)(len >> 4);
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(s);
+    f32x4* d4 = reinterpret_cast<f32x4*>(d);
+    f32x4 v[NVT];
+#pragma unroll
+    for (int k = 0; k < NVT; ++k) {
+      const int e = (int)threadIdx.x + k * 256;
+      if (e < nv) v[k] = __builtin_nontemporal_load(s4 + e);
+    }
+#pragma unroll
+    for (int k = 0; k < NVT; ++k) {
+      const int e = (int)threadIdx.x + k * 256;
+      if (e < nv) d4[e] = v[k];
+    }
   } else {
     const long long nw = len >> 2;
     for (long long v = threadIdx.x; v < nw; v += 256)
