@@ -978,10 +978,10 @@ def main():
             out["dp_variants"] = dp_variants(args, B, T, A, dev, dist, world, batch)
         except Exception as ex:  # noqa: BLE001
             out["dp_variants"] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
-    # the drop-in loop before host_staged: its engines are closed afterwards, and the headline
-    # engine's staging ring (host_staged's two copy streams) does not exist yet.  A process's
-    # streams share GPU_MAX_HW_QUEUES (4) hardware queues; with the ring's streams alive the
-    # loop's copies ran 0.42 instead of 0.30-0.32 ms per step (profiles/r06v)
+    # the drop-in loop before host_staged: its engines are closed afterwards.  A process's
+    # streams share GPU_MAX_HW_QUEUES (4) hardware queues; when every handle had its own copy
+    # streams, the loop's copies ran 0.42 instead of 0.30-0.32 ms per step beside the headline
+    # engine's ring (profiles/r06w).  The copy streams are now one set per device (r06x)
     if world == 1 and dist is None and not ppo and not args.no_learner_loop:
         out["learner_loop"] = run_learner_loop(args, dev, round(ms_step, 4))
     if not args.no_host_staged:

@@ -66,7 +66,9 @@ def _host_floats(pending: List[Dict]) -> List[Dict[str, float]]:
     host = {}
     if bases:
         bl = list(bases.values())
-        if len({(b.numel(), b.dtype, b.device) for b in bl}) == 1:
+        if len(bl) == 1:  # one step's vector: copy it as it is (no stacking kernel)
+            rows = [bl[0].cpu().tolist()]
+        elif len({(b.numel(), b.dtype, b.device) for b in bl}) == 1:
             rows = torch.stack(bl).cpu().tolist()
         else:
             rows = [b.cpu().tolist() for b in bl]
