@@ -51,7 +51,8 @@ PPO_METRIC_SLOTS = (("train/loss", 0), ("train/entropy", 1), ("train/td", 2), ("
 EXPORTS = (
     "impala_abi_version", "impala_last_error", "impala_config_default", "impala_param_count",
     "impala_create", "impala_destroy", "impala_bind_state", "impala_refresh_weights",
-    "impala_set_step", "impala_set_metrics", "impala_forward", "impala_train_step", "impala_compute_grads",
+    "impala_set_step", "impala_set_metrics", "impala_set_metrics_host", "impala_forward",
+    "impala_train_step", "impala_compute_grads",
     "impala_apply_update", "impala_compute_grads_part", "impala_grad_bucket_offset",
     "impala_grad_bucket_offset_fc",
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
@@ -148,6 +149,7 @@ def _declare(lib):
     lib.impala_set_step.argtypes = [_P, C.c_int64, _P]
     lib.impala_set_debug_vtrace.argtypes = [_P, _P]
     lib.impala_set_metrics.argtypes = [_P, _P]
+    lib.impala_set_metrics_host.argtypes = [_P, _P]
     lib.impala_forward.argtypes = [_P, _P, C.c_int, _P, _P, _P]
     lib.impala_act.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_uint64, C.c_uint64, _P, _P, _P,
                                _P]

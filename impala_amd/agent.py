@@ -55,6 +55,31 @@ def _host_floats(pending: List[Dict]) -> List[Dict[str, float]]:
     one device-to-host copy for all of them: device scalars that are views of one metrics
     vector (ImpalaLearner._train_step) are read from a single stacked copy of those vectors,
     instead of one synchronising copy per value.  Anything else goes through float(v)."""
+    return _to_dicts(*_read_values(pending))
+
+
+def _read_values(pending: List[Dict]):
+    """The synchronising half of _host_floats: the one device-to-host copy -> (pending, host
+    rows by base id); _to_dicts builds the float dicts from them later.  Metrics dicts that
+    carry their step's host row (ImpalaLearner's StepMetrics) are read from it once the step's
+    event has completed, with no copy enqueued behind the work queued since."""
+    host = {}
+    rest = []
+    for m in pending:
+        hm = getattr(m, "host", None)
+        vals = hm.values() if hm is not None else None
+        base = next(iter(m.values()))._base if vals is not None and m else None
+        if vals is not None and base is not None:
+            host[id(base)] = (base, vals)
+        else:
+            rest.append(m)
+    if not rest:
+        return pending, host
+    host.update(_copy_values(rest))
+    return pending, host
+
+
+def _copy_values(pending: List[Dict]):
     bases = {}
     for m in pending:
         for v in m.values():
@@ -73,6 +98,10 @@ def _host_floats(pending: List[Dict]) -> List[Dict[str, float]]:
         else:
             rows = [b.cpu().tolist() for b in bl]
         host = {id(b): (b, r) for b, r in zip(bl, rows)}
+    return host
+
+
+def _to_dicts(pending: List[Dict], host) -> List[Dict[str, float]]:
     out = []
     for m in pending:
         d = {}
@@ -117,15 +146,25 @@ class DistributedAgent(Agent):
             self._controller.set_phase(Phase.TRAIN)
         self._learner.prepare()
         pending = []
+        read = None  # values read at the last sync, turned into floats after the next enqueue
         for local_steps in range(num_steps):
             metrics = self._learner.train_step()
+            if read is not None:
+                # the previous sync's floats, booked now that this step is enqueued: the device
+                # then runs while the host builds them (the values and order are unchanged)
+                for d in _to_dicts(*read):
+                    self._stats_dict.extend(d)
+                read = None
             pending.append(metrics)
             if len(pending) >= self._sync_every or local_steps == num_steps - 1:
-                for d in _host_floats(pending):
-                    self._stats_dict.extend(d)
+                read = _read_values(pending)  # the sync: every pending value on the host
                 pending = []
             if local_steps % 100 == 0:
-                self._log(_host_floats([metrics])[0])
+                just_read = read is not None and read[0][-1] is metrics
+                self._log(_to_dicts(*read)[-1] if just_read else _host_floats([metrics])[0])
+        if read is not None:
+            for d in _to_dicts(*read):
+                self._stats_dict.extend(d)
         if self._controller is None:
             # no actor side to ask: the frames this learner consumed
             total_samples = float(num_steps * getattr(self._learner, "samples_per_step", 0))

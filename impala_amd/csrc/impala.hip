@@ -130,6 +130,7 @@ struct impala_learner {
   // caller-owned (bound)
   float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr,
         *metrics = nullptr;
+  float* metrics_host = nullptr;  // impala_set_metrics_host: the step's metrics also to host memory
   // library-owned
   char* ws = nullptr;
   size_t ws_bytes = 0;
@@ -668,6 +669,7 @@ int launch_adam(impala_learner* h, hipStream_t st) {
   AdamArgs aa{};
   aa.params = h->params; aa.grads = h->grads; aa.m = h->exp_avg; aa.v = h->exp_avg_sq;
   aa.metrics = h->metrics; aa.sumsq_part = h->sumsq_part; aa.n_part = h->n_norm_part;
+  aa.metrics_host = h->metrics_host;
   aa.step = h->step;
   aa.sc = h->adam_sc; aa.b1 = dec(h->cfg.adam_beta1); aa.b2 = dec(h->cfg.adam_beta2);
   aa.eps = h->cfg.adam_eps; aa.max_norm = h->cfg.max_grad_norm;
@@ -1196,6 +1198,25 @@ int impala_set_metrics(impala_learner* h, float* metrics) {
   if (h->metrics != metrics) {
     h->metrics = metrics;
     h->red.metrics = metrics;
+    if (h->use_graph) drop_graphs(h);  // captured launches hold the previous pointer
+  }
+  return 0;
+}
+
+int impala_set_metrics_host(impala_learner* h, float* host) {
+  if (!h) return fail(IMPALA_E_INVALID, "null handle");
+  if (host) {
+    if (h->fused_update)  // the A/B fused reduce + Adam launch does not write it
+      return fail(IMPALA_E_UNSUPPORTED, "impala_set_metrics_host: not with IMPALA_FUSED_UPDATE");
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, host) != hipSuccess || at.type != hipMemoryTypeHost) {
+      (void)hipGetLastError();
+      return fail(IMPALA_E_INVALID, "impala_set_metrics_host: not page-locked host memory");
+    }
+    if (((uintptr_t)host & 3) != 0) return fail(IMPALA_E_INVALID, "impala_set_metrics_host: misaligned");
+  }
+  if (h->metrics_host != host) {
+    h->metrics_host = host;
     if (h->use_graph) drop_graphs(h);  // captured launches hold the previous pointer
   }
   return 0;

@@ -818,6 +818,7 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 // =========================================================================================
 struct AdamArgs {
   float *params, *grads, *m, *v, *metrics;
+  float* metrics_host;  // (or null) page-locked host copy of the step's metrics vector
   const float* sumsq_part;
   int n_part;
   const int64_t* step;
@@ -907,6 +908,15 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.metrics[6] = norm;
     a.metrics[7] = (float)step;
+  }
+  if (a.metrics_host && blockIdx.x == 0 && threadIdx.x < IMPALA_NUM_METRICS) {
+    // the whole vector (slots other than 6 and 7 were final when the reduction kernel ended) to
+    // host memory, with system-scope stores; the caller reads it once an event recorded after
+    // this kernel has completed (no device-to-host copy on the stream)
+    const int i = (int)threadIdx.x;
+    const float x = i == 6 ? norm : i == 7 ? (float)step : a.metrics[i];
+    __hip_atomic_store(reinterpret_cast<unsigned*>(a.metrics_host) + i, __float_as_uint(x),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (n == 0) return;  // (never an FC block: those are full)
   const float gscale = a.inv_world * coef;

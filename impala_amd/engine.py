@@ -78,6 +78,7 @@ class Engine:
                                       ptr(self.exp_avg_sq), ptr(self.metrics), stream_ptr(None)),
                   "impala_bind_state")
         self._version = model._version
+        self._metrics_host = False  # impala_set_metrics_host bound (bind_metrics)
         self._dp = False  # dp_init ran: the handle has its own RCCL communicator
 
     # ------------------------------------------------------------------ lifecycle
@@ -106,14 +107,26 @@ class Engine:
         if self._version != self.model._version:
             self.refresh_weights(stream)
 
-    def bind_metrics(self, metrics: torch.Tensor):
+    def bind_metrics(self, metrics: torch.Tensor, host: Optional[torch.Tensor] = None):
         """The following steps write their metrics into `metrics` (a device float32 vector of
-        NUM_METRICS, impala_set_metrics; no device work), which becomes ``self.metrics``."""
+        NUM_METRICS, impala_set_metrics; no device work), which becomes ``self.metrics``; and,
+        when `host` (a page-locked float32 CPU vector of NUM_METRICS) is given, also into
+        `host` (impala_set_metrics_host: readable once an event recorded after the step has
+        completed).  ``host=None`` stops the host copy."""
         if metrics.dtype != torch.float32 or metrics.device != self.device or \
                 metrics.numel() < _lib.NUM_METRICS or not metrics.is_contiguous():
             raise ValueError(f"metrics must be a contiguous float32 vector of >= "
                              f"{_lib.NUM_METRICS} on {self.device}")
-        check(_lib.lib().impala_set_metrics(self._h, ptr(metrics)), "impala_set_metrics")
+        if host is not None and (host.dtype != torch.float32 or host.device.type != "cpu" or
+                                 host.numel() < _lib.NUM_METRICS or not host.is_contiguous()):
+            raise ValueError(f"host metrics must be a contiguous float32 CPU vector of >= "
+                             f"{_lib.NUM_METRICS}")
+        L = _lib.lib()
+        check(L.impala_set_metrics(self._h, ptr(metrics)), "impala_set_metrics")
+        if host is not None or self._metrics_host:
+            check(L.impala_set_metrics_host(self._h, None if host is None else host.data_ptr()),
+                  "impala_set_metrics_host")
+            self._metrics_host = host is not None
         self.metrics = metrics
 
     def set_step(self, step: int, stream=None):

@@ -60,6 +60,35 @@ def _collate(batch, device) -> Tuple[torch.Tensor, ...]:
     return obs, act.to(torch.int64), rew.float(), disc.float(), mu.float()
 
 
+# rows of the page-locked metrics ring: a step's host row is valid until the step
+# HOST_METRICS_RING later is enqueued (DistributedAgent reads every sync_every < this)
+HOST_METRICS_RING = 1024
+
+
+@dataclass
+class HostMetrics:
+    """Where a step's metrics vector also lands in host memory (impala_set_metrics_host): the
+    ring row, the event recorded after the step, the learner and the step's index."""
+    row: torch.Tensor
+    event: "torch.cuda.Event"
+    learner: "ImpalaLearner"
+    index: int
+
+    def values(self):
+        """-> the row's NUM_METRICS floats once the step has completed, or None when the row
+        has been handed to a later step since (the caller then reads the device vector)."""
+        if self.learner._step_count - self.index > HOST_METRICS_RING - 1:
+            return None
+        self.event.synchronize()
+        return self.row[:_lib.NUM_METRICS].tolist()
+
+
+class StepMetrics(dict):
+    """The metrics dict train_step returns (learning.py:161-174: key -> device scalar), with
+    ``host``: the step's HostMetrics, or None."""
+    host: Optional[HostMetrics] = None
+
+
 class ImpalaLearner(Learner):
     def __init__(self, model, replay_buffer, optimizer=None, batch_size: int = 8,
                  max_grad_norm: float = 0.5, entropy_coeff: float = 0.01,
@@ -103,6 +132,7 @@ class ImpalaLearner(Learner):
         self._prefetch = max(0, int(prefetch))
         # the prefetched (batch, slot, n_samples, sample seconds), oldest first
         self._queue = collections.deque()
+        self._mhost = None  # the page-locked metrics ring (_host_row), False off the GPU
         self._step_count = 0
         self._step_counter = 0
         self.can_train = True
@@ -199,15 +229,19 @@ class ImpalaLearner(Learner):
             batch = None
             n_samples = self._batch_size * self._rollout_length
         else:
-            batch = _collate(batch, self.device())
-            n_samples = self._batch_size * batch[0].shape[1]
-        return batch, slot, n_samples, time.perf_counter() - t0
+            tensors = _collate(batch, self.device())
+            n_samples = self._batch_size * tensors[0].shape[1]
+            # checked and turned into the library's batch struct here, off the path from the
+            # previous step's metrics read to this step's first launch; the tensors stay
+            # referenced by the queue entry until the step is enqueued
+            return (self._engine._batch(*tensors),), None, n_samples, time.perf_counter() - t0, tensors
+        return batch, slot, n_samples, time.perf_counter() - t0, None
 
     def _resolve(self, item):
-        batch, slot, n_samples, sample_s = item
+        batch, slot, n_samples, sample_s, keep = item
         if slot is not None:  # the step's stream waits for the slot's copies
             batch = (self._engine.slot_batch(slot),)
-        return batch, slot, n_samples, sample_s
+        return batch, slot, n_samples, sample_s, keep
 
     def _refill(self):
         """Sample and stage batches until `prefetch` are queued (a device replay's gathers go on
@@ -226,9 +260,10 @@ class ImpalaLearner(Learner):
 
     def train_step(self):  # learning.py:119-138
         t0 = time.perf_counter()
-        batch, slot, n_samples, sample_s = self._resolve(self._take_next())
+        batch, slot, n_samples, sample_s, keep = self._resolve(self._take_next())
         t1 = time.perf_counter()
         metrics = self._train_step(batch)
+        del keep  # (the device batch's tensors: enqueued now, stream-ordered from here)
         if slot is not None:
             self._engine.slot_release(slot)
         t2 = time.perf_counter()
@@ -249,12 +284,26 @@ class ImpalaLearner(Learner):
         metrics["debug/update_time"] = update_time
         return metrics
 
+    def _host_row(self):
+        """This step's row of the page-locked metrics ring (impala_set_metrics_host), or None
+        off the GPU."""
+        if self._mhost is None:
+            if self._engine.device.type != "cuda":
+                self._mhost = False
+            else:
+                self._mhost = torch.zeros(HOST_METRICS_RING, 16, dtype=torch.float32, pin_memory=True)
+        if self._mhost is False:
+            return None
+        return self._mhost[self._step_count % HOST_METRICS_RING]
+
     def _train_step(self, batch) -> Dict[str, torch.Tensor]:  # learning.py:140-177
         e = self._engine
         # this step's metrics go to a vector of its own, which the returned values are views
-        # of (impala_set_metrics: no device copy after the step)
+        # of (impala_set_metrics: no device copy after the step), and to a row of a page-locked
+        # ring that the step's last kernel writes (impala_set_metrics_host)
         m = torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device)
-        e.bind_metrics(m)
+        row = self._host_row()
+        e.bind_metrics(m, host=row)
         if self._world_size == 1:
             e.train_step(*batch)
         else:
@@ -270,9 +319,15 @@ class ImpalaLearner(Learner):
             else:
                 compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
                 e.apply_update()
-        # device scalars, views of the step's metrics vector: float(v) synchronises lazily, and
-        # DistributedAgent moves all of a step's values with one copy (agent._host_floats)
-        return dict(zip(_lib.METRIC_NAMES, m.unbind(0)))
+        # device scalars, views of the step's metrics vector: float(v) synchronises lazily;
+        # DistributedAgent reads the host row once the event after the step has completed
+        # (agent._read_values), or moves all of a step's values with one copy
+        out = StepMetrics(zip(_lib.METRIC_NAMES, m.unbind(0)))
+        if row is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            out.host = HostMetrics(row, ev, self, self._step_count)
+        return out
 
     # ---------------------------------------------------------------- checkpoint
     def optimizer_state(self) -> dict:

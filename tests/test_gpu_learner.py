@@ -585,6 +585,58 @@ def test_agent_train_over_learner_floats_match_device_metrics():
             assert st[k]["min"] == min(g[k] for g in got) and st[k]["max"] == max(g[k] for g in got)
 
 
+def test_host_metrics_rows_match_device_vectors(monkeypatch):
+    """impala_set_metrics_host: the row of the page-locked ring the step's last kernel writes
+    is bitwise the step's device metrics vector; a row handed to a later step reads as None
+    (the ring of 4 here), and DistributedAgent then falls back to the device copy -- its stats
+    over a mix of both equal float(v) of every step."""
+    dev = _dev()
+    import impala_amd.learner as lmod
+    from impala_amd import _lib
+    from impala_amd.agent import DistributedAgent
+    from impala_amd.model import AtariPPOModel
+    monkeypatch.setattr(lmod, "HOST_METRICS_RING", 4)
+    B, T, n = 2, 20, 12
+    batches = [tuple(torch.from_numpy(x).to(dev) for x in ref_cpu.synthetic_batch(B, T, 15, seed=s))
+               for s in range(n)]
+    m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+    ln = lmod.ImpalaLearner(m, _FixedReplay(list(batches)), batch_size=B)
+    mets = [ln.train_step() for _ in range(n)]
+    torch.cuda.synchronize()
+    for i, met in enumerate(mets):
+        assert met.host is not None and met.host.index == i
+        vals = met.host.values()
+        dev_vals = met["train/loss"]._base.cpu().tolist()
+        if i >= n - 3:
+            assert vals == dev_vals[:_lib.NUM_METRICS], i
+            assert vals[7] == float(i + 1)  # the Adam step count
+        else:
+            assert vals is None, i
+    for sync in (1, 6):
+        m = AtariPPOModel((3, 64, 64), 15, device=dev, dtype="fp32", seed=0)
+        ln = lmod.ImpalaLearner(m, _FixedReplay(list(batches)), batch_size=B)
+        got = []
+        step = ln.train_step
+
+        def keep():
+            met = step()
+            got.append(met)
+            return met
+
+        ln.train_step = keep
+        agent = DistributedAgent(None, ln, sync_every=sync)
+        agent.train(n)
+        torch.cuda.synchronize()
+        floats = [{k: float(v) for k, v in g.items() if k.startswith("train/")} for g in got]
+        stats = agent.stats.dict()
+        for k in floats[0]:
+            assert stats[k]["count"] == n
+            assert stats[k]["min"] == min(f[k] for f in floats), (sync, k)
+            assert stats[k]["max"] == max(f[k] for f in floats), (sync, k)
+            mean = sum(f[k] for f in floats) / n
+            assert abs(stats[k]["mean"] - mean) <= 1e-6 * (1 + abs(mean)), (sync, k)
+
+
 @pytest.mark.parametrize("kind", ["device", "host_list"])
 def test_learner_prefetch_matches_sampling_inside_the_step(kind):
     """ImpalaLearner(prefetch=1 or 2) samples and stages the next steps' batches right after a

@@ -37,7 +37,7 @@ def bench_loop():
     """bench.py's learner_loop record alone, in a fresh process (no headline regions first)."""
     import argparse
     import json
-    args = argparse.Namespace(batch=64, rollout=20, actions=15, loop_capacity=1000, loop_steps=100,
+    args = argparse.Namespace(batch=64, rollout=20, actions=15, loop_capacity=1000, loop_steps=100, loop_warmup=None,
                               warmup=5, dtype="fp32")
     out = bench.run_learner_loop(args, torch.device("cuda:0"), 0.22)
     for r in bench.LOOP_REPLAYS:
