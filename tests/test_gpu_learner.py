@@ -642,7 +642,8 @@ def test_learner_prefetch_matches_sampling_inside_the_step(kind):
     """ImpalaLearner(prefetch=1 or 2) samples and stages the next steps' batches right after a
     step is enqueued; with no appends in between it samples the same sequence as prefetch=0 (the
     reference's order, learning.py:121), so weights and metrics are bitwise equal, for each
-    replay the learner can be given."""
+    replay the learner can be given.  No step is waited for inside the loop, so a batch buffer
+    reused while a queued step still reads it would show."""
     dev = _dev()
     from impala_amd.learner import ImpalaLearner
     from impala_amd.model import AtariPPOModel
@@ -658,9 +659,9 @@ def test_learner_prefetch_matches_sampling_inside_the_step(kind):
             rb.append(t)
         m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
         ln = ImpalaLearner(m, rb, batch_size=B, rollout_length=T, prefetch=prefetch)
-        losses = [float(ln.train_step()["train/loss"]) for _ in range(steps)]
+        losses = [ln.train_step()["train/loss"] for _ in range(steps)]
         torch.cuda.synchronize()
-        return m.flat.clone(), losses
+        return m.flat.clone(), [float(x) for x in losses]
 
     p0, l0 = run(0)
     for depth in (1, 2):
