@@ -986,6 +986,11 @@ def main():
         out["learner_loop"] = run_learner_loop(args, dev, round(ms_step, 4))
     if not args.no_host_staged:
         out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
+        if "learner_loop" in out and "host_list_replay" in out["learner_loop"]:
+            # the host-list loop against the same process's host-staged step
+            hs = out["host_staged"]["ms_per_step"]
+            for rec in out["learner_loop"]["host_list_replay"].values():
+                rec["ratio_to_host_staged"] = round(rec["ms_per_step"] / hs, 3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if ppo:
             out["cpu_baseline"] = cpu_baseline_ppo(B, A, args.cpu_seconds,
