@@ -57,7 +57,7 @@ EXPORTS = (
     "impala_grad_bucket_offset_fc",
     "impala_ppo_train_step", "impala_ppo_loss_head", "impala_vtrace", "impala_loss_head", "impala_kernel_count",
     "impala_kernel_name", "impala_timer_start", "impala_timer_read", "impala_gather_rows",
-    "impala_gather_rows_hidx",
+    "impala_gather_rows_hidx", "impala_train_step_rows",
     "impala_stage_init", "impala_stage", "impala_stage_rows", "impala_stage_rows_async",
     "impala_stage_wait",
     "impala_slot_batch",
@@ -150,6 +150,7 @@ def _declare(lib):
     lib.impala_set_debug_vtrace.argtypes = [_P, _P]
     lib.impala_set_metrics.argtypes = [_P, _P]
     lib.impala_set_metrics_host.argtypes = [_P, _P]
+    lib.impala_train_step_rows.argtypes = [_P, C.POINTER(ImpalaBatch), _P, C.c_int, C.c_int64, _P]
     lib.impala_forward.argtypes = [_P, _P, C.c_int, _P, _P, _P]
     lib.impala_act.argtypes = [_P, _P, C.c_int, _P, C.c_int, C.c_uint64, C.c_uint64, _P, _P, _P,
                                _P]
@@ -238,10 +239,18 @@ def lib():
         return _lib
 
 
+IMPALA_E_UNSUPPORTED = 1003
+
+
+class Unsupported(RuntimeError):
+    """IMPALA_E_UNSUPPORTED: the handle cannot run this entry point (its caller falls back)."""
+
+
 def check(status: int, what: str = "") -> None:
     if status != 0:
         msg = lib().impala_last_error().decode(errors="replace")
-        raise RuntimeError(f"{what or 'impala'} failed (status {status}): {msg}")
+        cls = Unsupported if status == IMPALA_E_UNSUPPORTED else RuntimeError
+        raise cls(f"{what or 'impala'} failed (status {status}): {msg}")
 
 
 def ptr(t) -> int:

@@ -68,6 +68,25 @@ DEV void c1_load_frame(const uint8_t* __restrict__ frame, int tid, uint4 v[3]) {
 #pragma unroll
   for (int i = 0; i < 3; ++i) v[i] = reinterpret_cast<const uint4*>(frame)[tid + i * 256];
 }
+// Which row of the batch arrays holds frame f.  ObsDirect: row f.  ObsRows
+// (impala_train_step_rows): the arrays are a replay ring read in place -- trajectory b of the
+// batch is ring slot rows[b], so frame f = b * T + t is ring row rows[b] * T + t (the same map
+// serves the per-frame actions, rewards, discounts and logits in head_step_kernel).  The map is
+// the kernels' last argument (dynamic indexing of a by-value kernel argument is a load from the
+// argument segment); ObsDirect is empty, so the other arguments keep their offsets.
+constexpr int kObsRowsMax = 256;
+struct ObsDirect {  // (empty: the identity map)
+  DEV size_t map(size_t f) const { return f; }
+};
+struct ObsRows {
+  int T;
+  int rows[kObsRowsMax];
+  DEV size_t map(size_t f) const {
+    const int b = (int)(f / (size_t)T);
+    return (size_t)rows[b] * (size_t)T + (f - (size_t)b * (size_t)T);
+  }
+};
+
 template <typename T, int LDI = c1::L<T>::LDI>
 DEV void c1_stash_frame(T* img, int tid, const uint4 v[3]) {
 #pragma unroll
@@ -312,12 +331,12 @@ template <typename T> struct C12FLds {
 // profiles/r05nt; nt on every activation store made the fp32 forward 60 -> 66 us)
 template <typename T> constexpr int kAct1Cpol = sizeof(T) == 2 ? 2 : 0;
 
-template <typename T>
+template <typename T, class O = ObsDirect>
 DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1,
                          const float* __restrict__ b1, const T* __restrict__ w2,
                          const float* __restrict__ b2, T* __restrict__ act1,
                          uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw,
-                         const C3Tail<T>& c3, int wg, T* __restrict__ smem) {
+                         const C3Tail<T>& c3, int wg, T* __restrict__ smem, const O& rm = O{}) {
   using F = Frag<T>;
   typedef typename F::vec V;
   constexpr int KPL = F::KPL, KS = F::KSTEP;
@@ -360,7 +379,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   const int f0 = wg * fpw, f1 = min(N, f0 + fpw);
   const int kl = KPL * (lane >> 4);
   uint4 nv[3];
-  if (ldr && f0 + grp < f1) c1_load_frame<T>(x + (size_t)(f0 + grp) * IMG, ltid, nv);
+  if (ldr && f0 + grp < f1) c1_load_frame<T>(x + rm.map(f0 + grp) * IMG, ltid, nv);
   // biases: 16-byte loads issued with the frame, ahead of the weights (waiting for the weights
   // then covers them: loads retire in order)
   float bb1[2][4], bb2[4];
@@ -412,7 +431,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
     }
     // the frame was loaded first: waiting for it leaves the weight loads in flight
     if (ldr && f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
-    if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, ltid, nv);
+    if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + rm.map(f0 + grp + G) * IMG, ltid, nv);
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int e = (int)threadIdx.x + i * NT;
@@ -564,7 +583,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   // during the previous frame's conv2
   if constexpr (!W2REG) {
     if (ldr && f0 + grp < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
-    if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + (size_t)(f0 + grp + G) * IMG, ltid, nv);
+    if (ldr && f0 + grp + G < f1) c1_load_frame<T>(x + rm.map(f0 + grp + G) * IMG, ltid, nv);
     __syncthreads();
   }
   for (int it = 0; it < n_it; ++it) {
@@ -640,7 +659,7 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
       }
       }
       if (ldr && f + G < f1) c1_stash_frame_rot<__bf16, ILDI>(img, ltid, nv);
-      if (ldr && f + 2 * G < f1) c1_load_frame<T>(x + (size_t)(f + 2 * G) * IMG, ltid, nv);
+      if (ldr && f + 2 * G < f1) c1_load_frame<T>(x + rm.map(f + 2 * G) * IMG, ltid, nv);
       if (!W2REG && wh == 0) {
         // the 4x4x1 blocks: lane 16 g + 4 og + j holds act2[pixel 32 + j][oc 16 w + 4 og + reg]
         // over k-phase g; ((g0 + g1) + (g2 + g3)) of reg q lands on row q (rows_sum4), so lane
@@ -800,18 +819,18 @@ DEV void conv12_fwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w1
   }
 }
 
-template <typename T>
+template <typename T, class O = ObsDirect>
 __global__ __launch_bounds__(c12f_threads<T>()) void conv12_fwd_s2d(
     const uint8_t* __restrict__ x, const T* __restrict__ w1, const float* __restrict__ b1,
     const T* __restrict__ w2, const float* __restrict__ b2, T* __restrict__ act1,
     uint32_t* __restrict__ mask, T* __restrict__ act2, int N, int fpw, const C3Tail<T> c3,
-    unsigned long long* __restrict__ step_stamp) {
+    unsigned long long* __restrict__ step_stamp, const O rm) {
   __shared__ __attribute__((aligned(16))) T smem[C12FLds<T>::ELEMS];
   // the device step clock (impala_step_clock): the learner step's first kernel stamps the
   // constant 100 MHz clock as its first workgroup starts (one vector store; nullptr = off)
   if (step_stamp != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
     *step_stamp = __builtin_amdgcn_s_memrealtime();
-  conv12_fwd_body<T>(x, w1, b1, w2, b2, act1, mask, act2, N, fpw, c3, (int)blockIdx.x, smem);
+  conv12_fwd_body<T, O>(x, w1, b1, w2, b2, act1, mask, act2, N, fpw, c3, (int)blockIdx.x, smem, rm);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -952,12 +971,13 @@ DEV void c12_load_w2(const float* __restrict__ w2t, Frag<float>::vec (&wb)[4][OC
 // sums ((z0 + z1) + z2) + z3, oc in MFMA order, pixels in k-step order.  Each workgroup writes
 // one fp32 partial slab [32][192] (k' order) + bias sums, reduced by reduce_grads.
 // ---------------------------------------------------------------------------------------
-template <int ROLE>
+template <int ROLE, class O = ObsDirect>
 DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restrict__ w2t,
                              const float* __restrict__ dy2, const uint32_t* __restrict__ mask1,
                              float* __restrict__ slab, float* __restrict__ slab_bias, int N,
                              int fpw, int wg, char* __restrict__ lds,
-                             Frag<float>::vec (&wb)[4][OC2 / Frag<float>::KSTEP][2], bool load_w2) {
+                             Frag<float>::vec (&wb)[4][OC2 / Frag<float>::KSTEP][2], bool load_w2,
+                             const O& rm = O{}) {
   using F = Frag<float>;
   typedef F::vec V;
   using L = C12B32;
@@ -1000,7 +1020,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
     uint4 nv[3];
     f32x4 nd2[ND2];
     uint32_t nmk = 0;
-    if (fi >= 0) c1_load_frame<float>(x + (size_t)fi * IMG, tid, nv);
+    if (fi >= 0) c1_load_frame<float>(x + rm.map(fi) * IMG, tid, nv);
     if (fd >= 0) {
       const float* src = dy2 + (size_t)fd * P2 * OC2;
 #pragma unroll
@@ -1044,7 +1064,7 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   };
   auto stage_ld = [&](int fi, int fd, StRegs& r) {
     r.nmk = 0;
-    if (fi >= 0) c1_load_frame<float>(x + (size_t)fi * IMG, tid, r.nv);
+    if (fi >= 0) c1_load_frame<float>(x + rm.map(fi) * IMG, tid, r.nv);
     if (fd >= 0) {
       const float* src = dy2 + (size_t)fd * P2 * OC2;
 #pragma unroll
@@ -1471,15 +1491,15 @@ DEV void conv12_bwd_body_f32(const uint8_t* __restrict__ x, const float* __restr
   }
 }
 
-template <typename T>
+template <typename T, class O = ObsDirect>
 DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2,
                          const T* __restrict__ w2t, const T* __restrict__ dy2, const uint32_t* __restrict__ mask1,
                          float* __restrict__ slab, float* __restrict__ slab_bias, int N, int fpw,
-                         int wg, char* __restrict__ lds) {
+                         int wg, char* __restrict__ lds, const O& rm = O{}) {
   if constexpr (sizeof(T) == 4) {  // fp32: the scatter-form body above
     Frag<float>::vec wb[4][OC2 / Frag<float>::KSTEP][2];
-    conv12_bwd_body_f32<-1>(x, reinterpret_cast<const float*>(w2t), reinterpret_cast<const float*>(dy2),
-                            mask1, slab, slab_bias, N, fpw, wg, lds, wb, true);
+    conv12_bwd_body_f32<-1, O>(x, reinterpret_cast<const float*>(w2t), reinterpret_cast<const float*>(dy2),
+                            mask1, slab, slab_bias, N, fpw, wg, lds, wb, true, rm);
     return;
   }
   using F = Frag<T>;
@@ -1515,7 +1535,7 @@ DEV void conv12_bwd_body(const uint8_t* __restrict__ x, const T* __restrict__ w2
   V nd2[ND2];
   uint32_t nmk = 0;
   auto fetch = [&](int f) {
-    c1_load_frame<T>(x + (size_t)f * IMG, tid, nv);
+    c1_load_frame<T>(x + rm.map(f) * IMG, tid, nv);
     const T* src = dy2 + (size_t)f * P2 * OC2;
 #pragma unroll
     for (int i = 0; i < ND2; ++i) {

@@ -64,8 +64,8 @@ template <typename T> constexpr int head_split() { return sizeof(T) == 4 ? 8 : 4
 // L2 hit and the loss is one wavefront), then each takes a 64-column slice of dz / dWh.
 // PPO = true: the PPO clipped-surrogate loss (kernels.h::ppo_frame) on flat transitions (T = 1,
 // one lane per transition, targets in `rew`, `disc` unused) instead of V-trace.
-template <typename T, bool PPO = false>
-__global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
+template <typename T, bool PPO = false, class O = ObsDirect>
+__global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a, const O fm) {
   constexpr int HEAD_JC = HID / head_split<T>();  // hidden columns per workgroup in phases 3/4
   static_assert(HEAD_JC == 64 || HEAD_JC == 32, "phase 3 / 4 wave map");
   constexpr int HEAD_CW = HEAD_JC / 16;           // column tiles per workgroup (4 or 2)
@@ -112,14 +112,17 @@ __global__ __launch_bounds__(256) void head_step_kernel(const HeadArgs a) {
   // three serial round trips, 4.8k cycles before phase 1, hstamps5 r04f.)  The action is read
   // as the low word of the int64 (actions are in [0, A)): a 64-bit load whose dead high half
   // gets its register reused costs a wait for the load. ----
-  const int act_q = reinterpret_cast<const int*>(a.act)[2 * nq];
+  // (fm.map: the frame's row in the batch arrays -- a replay ring's row for ObsRows)
+  const size_t nqb = fm.map(nq);
+  const int act_q = reinterpret_cast<const int*>(a.act)[2 * nqb];
   float mub[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) mub[u] = a.mu[nq * A + min(q4 + u, A - 1)];
+  for (int u = 0; u < 4; ++u) mub[u] = a.mu[nqb * A + min(q4 + u, A - 1)];
   float r = 0.f, g = 0.f;
   if (wave == 0) {
-    r = a.rew[f0 + fl];
-    if constexpr (!PPO) g = a.disc[f0 + fl];
+    const size_t fb = fm.map(f0 + fl);
+    r = a.rew[fb];
+    if constexpr (!PPO) g = a.disc[fb];
   }
   constexpr int NHV = 64 * (HID / VEC) / 256, NZV = 64 * (HEAD_JC / 4) / 256;
   constexpr int NKH = HID / F::KSTEP, NKT = HPAD / F::KSTEP;

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <algorithm>
 #include <cctype>
+#include <type_traits>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -131,6 +132,10 @@ struct impala_learner {
   float *params = nullptr, *grads = nullptr, *exp_avg = nullptr, *exp_avg_sq = nullptr,
         *metrics = nullptr;
   float* metrics_host = nullptr;  // impala_set_metrics_host: the step's metrics also to host memory
+  // impala_train_step_rows: while its launches are enqueued, the batch's frames are read from a
+  // replay ring through obs_rows (conv12_fwd_s2d, head_step_kernel, lnc3_conv12_bwd)
+  bool rows_on = false;
+  ObsRows obs_rows{};
   // library-owned
   char* ws = nullptr;
   size_t ws_bytes = 0;
@@ -326,11 +331,15 @@ int launch_forward(impala_learner* h, const uint8_t* obs, int n, hipStream_t st,
       return 0;
     }
 #endif
-    if (int r = klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T>,
-                        dim3(cdiv(n, fpw)), dim3(c12f_threads<T>()), st, obs, sw + sh.w1,
-                        vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
-                        (T*)h->act2, n, fpw, c3, with_heads ? nullptr : step_stamp(h)))
-      return r;
+    // the frames from the batch arrays, or (impala_train_step_rows) from a replay ring in place
+    auto fwd = [&](const auto& rm) {
+      using O = std::decay_t<decltype(rm)>;
+      return klaunch(h, conv3_done ? K_CONV123_FWD : K_CONV12_FWD, "conv12_fwd", conv12_fwd_s2d<T, O>,
+                     dim3(cdiv(n, fpw)), dim3(c12f_threads<T>()), st, obs, sw + sh.w1,
+                     vv + Vecs::b1, sw + sh.w2, vv + Vecs::b2, (T*)h->act1, h->mask1,
+                     (T*)h->act2, n, fpw, c3, with_heads ? nullptr : step_stamp(h), rm);
+    };
+    if (int r = h->rows_on && !with_heads ? fwd(h->obs_rows) : fwd(ObsDirect{})) return r;
   } else {
     if (!with_heads)  // the unfused forward (IMPALA_FWD_FUSED=0): the clock gets a stamp launch
       if (unsigned long long* ss = step_stamp(h))
@@ -468,8 +477,13 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
     ha.clip_hi = (float)(1.0 + (double)h->cfg.ppo_clip);
     const dim3 hg(h->n_loss_wg, head_split<T>());
     if (int r = h->cfg.algo == IMPALA_ALGO_PPO
-                    ? klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, true>, hg, dim3(256), st, ha)
-                    : klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, false>, hg, dim3(256), st, ha))
+                    ? klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, true>, hg, dim3(256), st, ha,
+                              ObsDirect{})
+                    : h->rows_on
+                    ? klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, false, ObsRows>, hg, dim3(256),
+                              st, ha, h->obs_rows)
+                    : klaunch(h, K_HEAD_STEP, "head_step", head_step_kernel<T, false>, hg, dim3(256), st, ha,
+                              ObsDirect{}))
       return r;
   }
   if (int r = fork(1)) return r;  // dz ready
@@ -522,14 +536,17 @@ int launch_backward(impala_learner* h, const impala_batch* b, hipStream_t st, in
   }
 stage_b:
   if (lc12) {
-    if (int r = klaunch(h, K_LNC12_BWD, "ln_conv3_conv2_dgrad_conv1_wgrad", lnc3_conv12_bwd<T>,
-                        dim3(h->n_ln_wg), dim3(lnc3_threads<T>()), st, (const float*)h->dy,
-                        (const T*)h->act3, (const float*)h->lnstat,
-                        (const float*)(h->vecs + Vecs::lng), sw + sh.w3, sw + sh.w3t,
-                        (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, b->obs,
-                        sw + sh.w2, sw + sh.w2t, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
-                        h->ln_fpw))
-      return r;
+    auto bwd = [&](const auto& rm) {
+      using O = std::decay_t<decltype(rm)>;
+      return klaunch(h, K_LNC12_BWD, "ln_conv3_conv2_dgrad_conv1_wgrad", lnc3_conv12_bwd<T, O>,
+                     dim3(h->n_ln_wg), dim3(lnc3_threads<T>()), st, (const float*)h->dy,
+                     (const T*)h->act3, (const float*)h->lnstat,
+                     (const float*)(h->vecs + Vecs::lng), sw + sh.w3, sw + sh.w3t,
+                     (const T*)h->act2, (T*)h->dact3, (T*)h->dact2, h->s_ln, b->obs,
+                     sw + sh.w2, sw + sh.w2t, (const uint32_t*)h->mask1, h->s_w1, h->s_b1, N,
+                     h->ln_fpw, rm);
+    };
+    if (int r = h->rows_on ? bwd(h->obs_rows) : bwd(ObsDirect{})) return r;
   } else if (h->lnc3_fused) {  // LayerNorm backward + conv3 dgrad per frame
     if (int r = klaunch(h, K_LNC3_BWD, "ln_bwd_conv3_dgrad", lnc3_bwd<T>, dim3(h->n_ln_wg),
                         dim3(lnc3_threads<T>()), st, (const float*)h->dy, (const T*)h->act3,
@@ -1495,6 +1512,37 @@ int impala_train_step(impala_learner* h, const impala_batch* b, void* stream) {
     if (int r = enqueue_grads(h, b, s)) return r;
     return enqueue_update(h, s);
   });
+}
+
+int impala_train_step_rows(impala_learner* h, const impala_batch* ring, const int64_t* rows, int n,
+                           int64_t capacity, void* stream) {
+  if (!h || !ring || !rows) return fail(IMPALA_E_INVALID, "null argument");
+  if (h->cfg.world_size != 1 || h->cfg.algo != IMPALA_ALGO_IMPALA)
+    return fail(IMPALA_E_UNSUPPORTED, "impala_train_step_rows: IMPALA handles of world_size 1");
+  // only the default launches read the batch through the row map: the fused forward
+  // (conv12_fwd_s2d), the fused head and the fused per-frame backward (lnc3_conv12_bwd)
+  const bool default_path = h->fwd_fused && h->lc12 && h->lnc3_fused && h->ln_fpw == h->c1_fpw &&
+                            !h->use_side && h->red_mode == 0 && !h->fused_update && !h->fwd_chain;
+  if (!default_path)
+    return fail(IMPALA_E_UNSUPPORTED, "impala_train_step_rows: not on the default kernel path");
+  if (n != h->cfg.batch_size || n > kObsRowsMax)
+    return fail(IMPALA_E_INVALID, "impala_train_step_rows: n must equal batch_size (at most 256)");
+  if (capacity < 1 || capacity > INT32_MAX / h->cfg.rollout_length)
+    return fail(IMPALA_E_INVALID, "impala_train_step_rows: bad capacity");
+  for (int i = 0; i < n; ++i)
+    if (rows[i] < 0 || rows[i] >= capacity)
+      return fail(IMPALA_E_INVALID, "impala_train_step_rows: row index out of range");
+  if (int r = check_bound(h)) return r;
+  if (int r = check_batch(ring)) return r;
+  CK(hipSetDevice(h->device));
+  h->obs_rows.T = h->cfg.rollout_length;
+  for (int i = 0; i < n; ++i) h->obs_rows.rows[i] = (int)rows[i];
+  h->rows_on = true;
+  // direct launches: the rows change every step, a captured graph would hold the first ones
+  int r = enqueue_grads(h, ring, (hipStream_t)stream);
+  if (r == 0) r = enqueue_update(h, (hipStream_t)stream);
+  h->rows_on = false;
+  return r;
 }
 
 namespace {

@@ -461,14 +461,14 @@ __global__ __launch_bounds__(lnc3_threads<T>()) void lnc3_bwd(
 // back from the workgroup's own global stores, ordered by the barrier between the bodies).
 // The two bodies share the LDS (its size is the larger of theirs).  The conv3 / conv2 weight
 // gradients, which need dact3 / dact2 of all frames, run after it.
-template <typename T>
+template <typename T, class O = ObsDirect>
 __global__ __launch_bounds__(lnc3_threads<T>()) void lnc3_conv12_bwd(
     const float* __restrict__ dy, const T* __restrict__ act3, const float* __restrict__ stats,
     const float* __restrict__ gam, const T* __restrict__ w3, const T* __restrict__ w3t,
     const T* __restrict__ act2, T* __restrict__ dact3, T* __restrict__ dact2,
     float* __restrict__ ln_slab, const uint8_t* __restrict__ x, const T* __restrict__ w2,
     const T* __restrict__ w2t, const uint32_t* __restrict__ mask1,
-    float* __restrict__ c1_slab, float* __restrict__ c1_slab_bias, int N, int fpw) {
+    float* __restrict__ c1_slab, float* __restrict__ c1_slab_bias, int N, int fpw, const O rm) {
   static_assert(lnc3_threads<T>() == 256 * c12_groups<T>(), "one block shape for both bodies");
   constexpr int B1 = Lnc3Lds<T>::BYTES, B2 = C12BLds<T>::BYTES;
   __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
@@ -489,15 +489,15 @@ __global__ __launch_bounds__(lnc3_threads<T>()) void lnc3_conv12_bwd(
       lnc3_body_f32r<0>(dy, a3, stats, gam, w3f, a2, d3, d2, ln_slab, N, fpw, wg, lds,
                         [&](int k) { c12_load_w2(w2f, wb, cls, lane, k, k + 1); });
       __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
-      conv12_bwd_body_f32<0>(x, w2f, d2, mask1, c1_slab, c1_slab_bias, N, fpw, wg, lds, wb, false);
+      conv12_bwd_body_f32<0, O>(x, w2f, d2, mask1, c1_slab, c1_slab_bias, N, fpw, wg, lds, wb, false, rm);
     } else {
       lnc3_body_f32r<1>(dy, a3, stats, gam, w3f, a2, d3, d2, ln_slab, N, fpw, wg, lds, [](int) {});
       __syncthreads();
-      conv12_bwd_body_f32<1>(x, w2f, d2, mask1, c1_slab, c1_slab_bias, N, fpw, wg, lds, wb, false);
+      conv12_bwd_body_f32<1, O>(x, w2f, d2, mask1, c1_slab, c1_slab_bias, N, fpw, wg, lds, wb, false, rm);
     }
   } else {
     lnc3_body<T>(dy, act3, stats, gam, w3, w3t, act2, dact3, dact2, ln_slab, N, fpw, (int)blockIdx.x, lds);
     __syncthreads();  // this workgroup's dact2 stores are visible to all its waves; LDS is reused
-    conv12_bwd_body<T>(x, w2, w2t, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds);
+    conv12_bwd_body<T, O>(x, w2, w2t, dact2, mask1, c1_slab, c1_slab_bias, N, fpw, (int)blockIdx.x, lds, rm);
   }
 }

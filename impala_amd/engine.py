@@ -121,8 +121,12 @@ class Engine:
                                  host.numel() < _lib.NUM_METRICS or not host.is_contiguous()):
             raise ValueError(f"host metrics must be a contiguous float32 CPU vector of >= "
                              f"{_lib.NUM_METRICS}")
+        self._bind_metrics(metrics, host)
+
+    def _bind_metrics(self, metrics, host=None):
+        """bind_metrics without the argument checks (for vectors the caller made to measure)."""
         L = _lib.lib()
-        check(L.impala_set_metrics(self._h, ptr(metrics)), "impala_set_metrics")
+        check(L.impala_set_metrics(self._h, metrics.data_ptr()), "impala_set_metrics")
         if host is not None or self._metrics_host:
             check(L.impala_set_metrics_host(self._h, None if host is None else host.data_ptr()),
                   "impala_set_metrics_host")
@@ -248,6 +252,43 @@ class Engine:
         self._sync_weights(stream)
         check(_lib.lib().impala_train_step(self._h, C.byref(b), stream_ptr(stream)),
               "impala_train_step")
+        self._updated()
+
+    def ring_batch(self, ring):
+        """Check a replay ring's five device arrays -- (obs u8 [C,T,3,64,64], actions i64 [C,T],
+        rewards [C,T], discounts [C,T], behaviour logits [C,T,A]) -- once -> (the library's batch
+        struct of their base addresses, C) for train_step_rows (the caller keeps the arrays)."""
+        obs = ring[0]
+        C_, T, A = obs.shape[0], self.rollout_length, self.num_actions
+        exp = (((C_, T, 3, 64, 64), torch.uint8), ((C_, T), torch.int64), ((C_, T), torch.float32),
+               ((C_, T), torch.float32), ((C_, T, A), torch.float32))
+        if len(ring) != 5:
+            raise ValueError("a ring is (obs, actions, rewards, discounts, behaviour logits)")
+        for t, (shape, dt) in zip(ring, exp):
+            if tuple(t.shape) != shape or t.dtype != dt or t.device != self.device or not t.is_contiguous():
+                raise ValueError(f"ring field: expected contiguous {dt} {shape} on {self.device}, "
+                                 f"got {t.dtype} {tuple(t.shape)} on {t.device}")
+        return ImpalaBatch(*[ptr(t) for t in ring]), int(C_)
+
+    def train_step_rows(self, ring, rows, stream=None):
+        """The full update on the trajectories ``rows`` (host int64 slot indices, one per batch
+        row) read in place from a replay ring -- the five device arrays, or ring_batch's result
+        for them -- (impala_train_step_rows; bitwise the same step as train_step on the gathered
+        batch).  Raises _lib.Unsupported when the handle does not run the default fused
+        kernels."""
+        import numpy as np
+        b, cap = ring if isinstance(ring[0], ImpalaBatch) else self.ring_batch(ring)
+        idx = rows if isinstance(rows, np.ndarray) and rows.dtype == np.int64 and \
+            rows.flags.c_contiguous else np.ascontiguousarray(rows, dtype=np.int64)
+        self._train_step_rows(b, cap, idx, stream)
+
+    def _train_step_rows(self, b, cap, idx, stream):
+        """train_step_rows on a ring_batch struct and a contiguous int64 index array."""
+        if self._version != self.model._version:
+            self.refresh_weights(stream)
+        check(_lib.lib().impala_train_step_rows(self._h, b, idx.ctypes.data, idx.size, cap,
+                                                stream_ptr(stream)),
+              "impala_train_step_rows")
         self._updated()
 
     def compute_grads(self, *batch, stream=None):

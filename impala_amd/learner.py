@@ -8,6 +8,7 @@ all-reduce of the flat gradient + ``impala_apply_update``.
 from __future__ import annotations
 
 import collections
+import os
 import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Sequence, Tuple
@@ -17,6 +18,7 @@ import torch
 from impala_amd import _lib
 from impala_amd.core import Learner
 from impala_amd.engine import Engine
+from impala_amd.replay import RowSample
 
 
 @dataclass
@@ -133,6 +135,8 @@ class ImpalaLearner(Learner):
         # the prefetched (batch, slot, n_samples, sample seconds), oldest first
         self._queue = collections.deque()
         self._mhost = None  # the page-locked metrics ring (_host_row), False off the GPU
+        self._rows_ok = None  # _rows_in_place
+        self._ring = None  # (replay, Engine.ring_batch of its arrays)
         self._step_count = 0
         self._step_counter = 0
         self.can_train = True
@@ -221,6 +225,11 @@ class ImpalaLearner(Learner):
         spent).  Host batches are staged (copies enqueued) here; their slot's device views are
         taken by _resolve on the thread that runs the step."""
         t0 = time.perf_counter()
+        if self._rows_in_place():
+            # the sampled slots only: the step reads them from the ring in place
+            # (Engine.train_step_rows), no gather
+            _, rs, _ = self._replay_buffer.sample_rows(self._batch_size)
+            return (rs,), None, self._batch_size * self._rollout_length, time.perf_counter() - t0, None
         _, batch, _ = self._replay_buffer.sample(self._batch_size)
         slot = None
         if isinstance(batch, list) and batch and isinstance(batch[0][0], torch.Tensor) \
@@ -242,6 +251,18 @@ class ImpalaLearner(Learner):
         if slot is not None:  # the step's stream waits for the slot's copies
             batch = (self._engine.slot_batch(slot),)
         return batch, slot, n_samples, sample_s, keep
+
+    def _rows_in_place(self) -> bool:
+        """Whether the learner's steps read a DeviceReplayBuffer's slots in place
+        (IMPALA_REPLAY_ROWS=0 turns it off; world size 1 only, batch <= 256; a handle that turns
+        out not to support it -- A/B kernel knobs -- falls back to gathers for good)."""
+        if self._rows_ok is None:
+            from impala_amd.replay import DeviceReplayBuffer
+            self._rows_ok = (isinstance(self._replay_buffer, DeviceReplayBuffer) and
+                             self._world_size == 1 and self._batch_size <= 256 and
+                             self._replay_buffer.T == self._rollout_length and
+                             os.environ.get("IMPALA_REPLAY_ROWS", "1") != "0")
+        return self._rows_ok
 
     def _refill(self):
         """Sample and stage batches until `prefetch` are queued (a device replay's gathers go on
@@ -303,8 +324,18 @@ class ImpalaLearner(Learner):
         # ring that the step's last kernel writes (impala_set_metrics_host)
         m = torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device)
         row = self._host_row()
-        e.bind_metrics(m, host=row)
-        if self._world_size == 1:
+        e._bind_metrics(m, row)
+        if len(batch) == 1 and isinstance(batch[0], RowSample):
+            rs = batch[0]
+            try:
+                if self._ring is None or self._ring[0] is not rs.replay:  # checked once per replay
+                    self._ring = (rs.replay,) + e.ring_batch(rs.replay.fields)
+                _, rb_, cap = self._ring
+                rs.replay.read_rows(rs, lambda fields, idx, st: e._train_step_rows(rb_, cap, idx, st))
+            except _lib.Unsupported:  # not on the default kernels: gather, for good
+                self._rows_ok = False
+                e.train_step(*rs.gather())
+        elif self._world_size == 1:
             e.train_step(*batch)
         else:
             from .distributed import (compute_grads_allreduced, native_dp_buckets,

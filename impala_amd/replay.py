@@ -125,6 +125,21 @@ class ReplayBuffer:
         return keys, batch, probs
 
 
+class RowSample:
+    """DeviceReplayBuffer.sample_rows: the sampled slots (host int64), read in place."""
+    __slots__ = ("replay", "idx")
+
+    def __init__(self, replay, idx):
+        self.replay, self.idx = replay, np.ascontiguousarray(idx, dtype=np.int64)
+
+    def gather(self, stream=None):
+        """The rows collated on the device (what ``sample`` returns), for a caller that cannot
+        read them in place."""
+        from impala_amd.engine import gather_rollouts
+        return self.replay.read_rows(self, lambda fields, idx, st: gather_rollouts(fields, idx, st),
+                                     stream)
+
+
 class DeviceReplayBuffer(ReplayBuffer):
     """HBM-resident circular rollout store with pinned-host staging (see module doc)."""
 
@@ -202,6 +217,39 @@ class DeviceReplayBuffer(ReplayBuffer):
             self._size = min(self._size + 1, self.capacity)
             self._cv.notify_all()
             return key
+
+    def sample_rows(self, batch_size: int):
+        """-> (keys, RowSample, probs): the same draw as ``sample`` (the same generator call),
+        without a gather -- the step reads the sampled slots in place
+        (``read_rows`` / Engine.train_step_rows).  A slot overwritten between this call and
+        the step is read with its new trajectory (the draw is of slots)."""
+        with self._cv:
+            idx = self._indices(batch_size)
+            keys = self._keys[idx].copy()
+            size = self._size
+        return keys, RowSample(self, idx), np.full(batch_size, 1.0 / size)
+
+    @property
+    def fields(self):
+        """The ring's five arrays (obs, actions, rewards, discounts, behaviour logits)."""
+        return (self.obs, self.act, self.rew, self.disc, self.mu)
+
+    def read_rows(self, rs: "RowSample", enqueue, stream=None):
+        """Run ``enqueue(fields, idx, stream)`` -- which enqueues work reading the ring slots
+        ``rs.idx`` on ``stream`` (the current stream when None) -- under the lock that ``append`` takes,
+        after that stream waits for every staged append, then mark the slots as read by it (the
+        fence an append into them waits for, as for a gather in ``sample``)."""
+        cur = torch.cuda.current_stream(self.device) if stream is None else stream
+        with self._cv:
+            if self._pending:
+                pending, self._pending = self._pending, []
+                for ev in pending:
+                    cur.wait_event(ev)
+            out = enqueue(self.fields, rs.idx, cur)
+            self._read_stream = cur
+            self._gen += 1
+            self._slot_gen[rs.idx] = self._gen
+        return out
 
     def sample(self, batch_size: int, stream=None):
         """-> (keys, (obs, act, rew, disc, mu) collated on the device, probs).

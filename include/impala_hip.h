@@ -238,6 +238,19 @@ int impala_gather_rows(const void* const* src, void* const* dst, const size_t* r
 int impala_gather_rows_hidx(const void* const* src, void* const* dst, const size_t* row_bytes,
                             int nfields, const int64_t* host_idx, int n, void* stream);
 
+/* The full learner step (impala_train_step) on B trajectories read IN PLACE from a replay ring
+ * (agents/impala/builder.py:30-36 replay + learning.py:121-123,142 sample / collate / .to):
+ * `ring` holds the ring's five arrays -- obs u8 [capacity][T][3][64][64], actions i64
+ * [capacity][T], rewards / discounts f32 [capacity][T], behaviour logits f32 [capacity][T][A]
+ * (device memory) -- and rows[0..n) (host memory, n == batch_size <= 256, each in
+ * [0, capacity)) the sampled slots: trajectory b of the step is slot rows[b].  No gather is
+ * enqueued; the forward, the fused head and the per-frame backward read the ring's rows
+ * through a row map in their launch arguments.  Bitwise equal to impala_train_step on the
+ * gathered batch.  IMPALA_E_UNSUPPORTED when the handle does not run the default fused
+ * kernels (A/B knobs), world_size > 1 or PPO: gather, then impala_train_step. */
+int impala_train_step_rows(impala_learner* h, const impala_batch* ring, const int64_t* rows, int n,
+                           int64_t capacity, void* stream);
+
 /* Host staging ring (SURVEY.md §8(b) impala_stage; replaces the 5·B pageable `.to(device)`
  * copies of learning.py:121-123).  The handle owns `nslots` device batch slots of B*T frames
  * and a non-blocking H2D stream:

@@ -637,6 +637,90 @@ def test_host_metrics_rows_match_device_vectors(monkeypatch):
             assert abs(stats[k]["mean"] - mean) <= 1e-6 * (1 + abs(mean)), (sync, k)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_train_step_rows_matches_the_gathered_batch(dtype):
+    """impala_train_step_rows: the step on ring slots read in place (duplicates included) is
+    bitwise the step on the same rows gathered into a batch; an out-of-range slot is refused
+    before anything is enqueued."""
+    dev = _dev()
+    from impala_amd import _lib
+    from impala_amd.engine import Engine, gather_rollouts
+    from impala_amd.model import AtariPPOModel
+    from impala_amd.replay import DeviceReplayBuffer
+    B, T, A, C = 8, 20, 15, 24
+    rb = DeviceReplayBuffer(C, T, A, device=dev, seed=3)
+    for i in range(C):
+        rb.append(ref_cpu.to_trajectories(*ref_cpu.synthetic_batch(1, T, A, seed=300 + i))[0])
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(7)
+    idxs = [rng.integers(0, C, size=B) for _ in range(4)]
+    idxs[1][3] = idxs[1][5]  # a slot twice in one batch
+
+    def make():
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype=dtype, seed=0)
+        e = Engine(m, batch_size=B, rollout_length=T, dtype=dtype)
+        m._train_engine = e
+        return m, e
+
+    m1, e1 = make()
+    m2, e2 = make()
+    for idx in idxs:
+        e1.train_step(*gather_rollouts(rb.fields, idx))
+        e2.train_step_rows(rb.fields, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(m1.flat, m2.flat)
+    assert torch.equal(e1.metrics, e2.metrics)
+    bad = idxs[0].copy()
+    bad[2] = C
+    with pytest.raises(RuntimeError, match="out of range"):
+        e2.train_step_rows(rb.fields, bad)
+    assert torch.equal(m1.flat, m2.flat)
+
+
+def test_learner_reads_device_replay_rows_in_place(monkeypatch):
+    """ImpalaLearner over a DeviceReplayBuffer reads the sampled slots in place (no gather):
+    bitwise the learner that gathers them (IMPALA_REPLAY_ROWS=0), with appends between the
+    steps (prefetch 0: sampled and read at the step) and without (prefetch 2); and a handle on
+    non-default kernels (IMPALA_FWD_FUSED=0) falls back to gathers with the same result."""
+    dev = _dev()
+    from impala_amd.learner import ImpalaLearner
+    from impala_amd.model import AtariPPOModel
+    from impala_amd.replay import DeviceReplayBuffer
+    B, T, A, C, steps = 4, 20, 15, 12, 5
+    trajs = [ref_cpu.to_trajectories(*ref_cpu.synthetic_batch(1, T, A, seed=900 + i))[0]
+             for i in range(C + steps)]
+
+    def run(rows, prefetch, appends, env=None):
+        monkeypatch.setenv("IMPALA_REPLAY_ROWS", "1" if rows else "0")
+        if env:
+            monkeypatch.setenv(*env)
+        rb = DeviceReplayBuffer(C, T, A, device=dev, seed=9)
+        for t in trajs[:C]:
+            rb.append(t)
+        m = AtariPPOModel((3, 64, 64), A, device=dev, dtype="fp32", seed=0)
+        ln = ImpalaLearner(m, rb, batch_size=B, rollout_length=T, prefetch=prefetch)
+        losses = []
+        for k in range(steps):
+            losses.append(ln.train_step()["train/loss"])
+            if appends:
+                rb.append(trajs[C + k])
+        torch.cuda.synchronize()
+        if env:
+            monkeypatch.delenv(env[0])
+        return m.flat.clone(), [float(x) for x in losses], ln._rows_ok
+
+    for prefetch, appends in ((0, True), (2, False)):
+        p0, l0, ok0 = run(False, prefetch, appends)
+        p1, l1, ok1 = run(True, prefetch, appends)
+        assert not ok0 and ok1
+        assert l0 == l1, (prefetch, appends)
+        assert torch.equal(p0, p1), (prefetch, appends)
+    p2, l2, ok2 = run(True, 2, False, env=("IMPALA_FWD_FUSED", "0"))
+    p3, l3, _ = run(False, 2, False, env=("IMPALA_FWD_FUSED", "0"))
+    assert ok2 is False  # fell back
+    assert l2 == l3 and torch.equal(p2, p3)
+
+
 @pytest.mark.parametrize("kind", ["device", "host_list"])
 def test_learner_prefetch_matches_sampling_inside_the_step(kind):
     """ImpalaLearner(prefetch=1 or 2) samples and stages the next steps' batches right after a

@@ -34,12 +34,22 @@ def main():
     torch.cuda.synchronize()
     marks = {"read_end": [], "launch": [], "read_start": []}
     L = _lib.lib()
-    f_step = L.impala_train_step
+    f_step, f_rows = L.impala_train_step, L.impala_train_step_rows
+    marks["returned"] = []
 
     def step_wrap(*a):
         marks["launch"].append(time.perf_counter())
-        return f_step(*a)
+        r = f_step(*a)
+        marks["returned"].append(time.perf_counter())
+        return r
+
+    def rows_wrap(*a):
+        marks["launch"].append(time.perf_counter())
+        r = f_rows(*a)
+        marks["returned"].append(time.perf_counter())
+        return r
     L.impala_train_step = step_wrap
+    L.impala_train_step_rows = rows_wrap
     rv = agent_mod._read_values
 
     def read_wrap(p):
@@ -53,14 +63,19 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
     L.impala_train_step = f_step
+    L.impala_train_step_rows = f_rows
     agent_mod._read_values = rv
+    ret = np.array(marks["returned"])
     re, la, rs = (np.array(marks[k]) for k in ("read_end", "launch", "read_start"))
     n = min(len(re), len(la)) - 1
     gap = (la[1:n + 1] - re[:n]) * 1e6          # metrics read done -> next step's train call
     enq = (rs[:n] - la[:n]) * 1e6               # train call -> this step's metrics read starts
     wait = (re[:n] - rs[:n]) * 1e6              # the read itself (device wait + D2H)
-    print(f"sync_every 1, {steps} steps: {wall * 1e3:.4f} ms per step (wall)")
-    for name, x in (("read -> next train call", gap), ("train call -> read start", enq),
+    call = (ret[:n] - la[:n]) * 1e6             # the library call (the step's launches)
+    print(f"sync_every 1, {steps} steps: {wall * 1e3:.4f} ms per step (wall), "
+          f"IMPALA_REPLAY_ROWS={os.environ.get('IMPALA_REPLAY_ROWS', '1')}")
+    for name, x in (("read -> next train call", gap), ("library call", call),
+                    ("train call -> read start", enq),
                     ("read (wait + copy)", wait)):
         print(f"  {name:26s} median {np.median(x):7.1f} us  p90 {np.percentile(x, 90):7.1f}")
 
