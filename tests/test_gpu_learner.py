@@ -476,6 +476,61 @@ def test_device_replay_append_during_sample_threaded():
     assert not errors, errors
 
 
+def test_device_replay_rows_read_during_appends_threaded():
+    """The in-place read (sample_rows, then read_rows -- the path impala_train_step_rows takes)
+    against a writer thread overwriting a capacity-8 ring: every row read is one whole
+    trajectory (all five fields encode the same k), from the drawn slot, and the drawn one or a
+    later one (a slot overwritten between the draw and the read is read with its new
+    trajectory)."""
+    import threading
+    dev = _dev()
+    from impala_amd.replay import DeviceReplayBuffer
+    T, A, C = 20, 15, 8
+
+    def item(k):
+        return [torch.full((T, 3, 64, 64), k % 251, dtype=torch.uint8),
+                torch.full((T, 1), k % A, dtype=torch.int64),
+                torch.full((T, 1), float(k)), torch.full((T, 1), 0.5 * k),
+                torch.full((T, A), float(-k))]
+
+    rb = DeviceReplayBuffer(capacity=C, rollout_length=T, num_actions=A, device=dev, seed=4,
+                            staging_slots=4)
+    for k in range(C):
+        rb.append(item(k))
+    stop = threading.Event()
+    errors = []
+
+    def writer():
+        k = C
+        try:
+            while not stop.is_set() and k < 5000:
+                rb.append(item(k))
+                k += 1
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = threading.Thread(target=writer)
+    th.start()
+    try:
+        for _ in range(150):
+            keys, rs, _ = rb.sample_rows(C)
+            obs, act, rew, disc, mu = rs.gather()
+            torch.cuda.synchronize()
+            r = rew.cpu().numpy()
+            for j, (slot, key) in enumerate(zip(rs.idx.tolist(), keys.tolist())):
+                k = int(r[j][0])
+                assert np.all(r[j] == float(k)), (j, r[j][:3])
+                assert k % C == slot and k >= key, (j, slot, key, k)
+                assert np.all(obs[j].cpu().numpy() == k % 251)
+                assert np.all(act[j].cpu().numpy() == k % A)
+                assert np.all(disc[j].cpu().numpy() == 0.5 * k)
+                assert np.all(mu[j].cpu().numpy() == -float(k))
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors
+
+
 def test_whole_model_checkpoint_after_learner_step(tmp_path):
     """reference main.py:117 torch.save(builder.learner_model, ...) with the learner's engine
     (a native handle) attached: the model pickles, reloads with its parameters and gradients
