@@ -248,6 +248,28 @@ def launch_cmd(nproc, argv):
             os.path.abspath(__file__)] + list(argv)
 
 
+_JSON_FD = None
+
+
+def claim_stdout():
+    """From here on everything written to fd 1 -- RCCL's version banner at communicator init,
+    anything a library prints -- goes to stderr; the original stdout is kept for the ONE JSON
+    line (emit_line), which the driver parses."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit_line(line):
+    """Write the result line to the stdout claim_stdout kept (or stdout)."""
+    if _JSON_FD is None:
+        print(line, flush=True)
+    else:
+        os.write(_JSON_FD, (line + "\n").encode())
+
+
 def maybe_launch_ranks(args, argv):
     """--gpus N > 1 outside torch.distributed.run: start the N ranks as a child process (this
     process has not touched the GPU) and return its exit status; None = run in this process.
@@ -792,7 +814,7 @@ def run_sac(args):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_sac(N, D, K, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit_line(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
 
@@ -849,6 +871,7 @@ def main():
     rc = maybe_launch_ranks(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
+    claim_stdout()  # (a rank process: RCCL prints its banner to stdout at the first collective)
     if args.algo == "sac":
         if args.batch == 64:
             args.batch = 256
@@ -1002,7 +1025,7 @@ def main():
             cb["single_thread"] = cpu_baseline(B, T, A, args.cpu_seconds_1t, threads=1, warmup=1)
             out["cpu_baseline"] = cb
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit_line(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -1,12 +1,15 @@
 """bench.py's rank launcher: `bench.py --gpus N` outside torch.distributed.run
 starts N ranks itself; under a launcher WORLD_SIZE must equal --gpus."""
 import argparse
+import os
 import subprocess
 import sys
 
 import pytest
 
 import bench
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _args(gpus):
@@ -170,3 +173,17 @@ def test_step_time_stats_finds_the_stall():
     assert s["slow_steps"] == [2] and len(s["step_ms"]) == 20
     assert abs(s["steps_sum_ms"] - (19 * 0.3 + 7.3)) < 1e-9
     assert "step_ms" not in bench.step_time_stats([1.0] * 300)
+
+
+def test_stdout_carries_only_the_json_line():
+    """bench.py claims fd 1 before any GPU / RCCL work: whatever is printed to stdout afterwards
+    (RCCL's version banner at communicator init, library prints) goes to stderr, and stdout
+    holds exactly the one JSON line the driver parses."""
+    import subprocess
+    code = ("import os, sys; sys.path.insert(0, %r); import bench; bench.claim_stdout(); "
+            "os.write(1, b'RCCL version : x\\n'); print('noise', flush=True); "
+            "bench.emit_line('{\"metric\": 1}')") % (HERE,)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == '{"metric": 1}\n'
+    assert "RCCL version" in r.stderr and "noise" in r.stderr
