@@ -136,6 +136,7 @@ class ImpalaLearner(Learner):
         self._queue = collections.deque()
         self._mhost = None  # the page-locked metrics ring (_host_row), False off the GPU
         self._rows_ok = None  # _rows_in_place
+        self._next_m = None  # (the next step's metrics vector, the stream it was made on)
         self._ring = None  # (replay, Engine.ring_batch of its arrays)
         self._step_count = 0
         self._step_counter = 0
@@ -289,6 +290,9 @@ class ImpalaLearner(Learner):
             self._engine.slot_release(slot)
         t2 = time.perf_counter()
         self._refill()  # the next steps' batches, while this step runs on the device
+        if self._engine.device.type == "cuda":  # the next step's metrics vector, made now
+            self._next_m = (torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=self._engine.device),
+                            torch.cuda.current_stream(self._engine.device))
         update_time = 0
         self._step_count += 1
         self._step_counter = self._step_count
@@ -322,7 +326,11 @@ class ImpalaLearner(Learner):
         # this step's metrics go to a vector of its own, which the returned values are views
         # of (impala_set_metrics: no device copy after the step), and to a row of a page-locked
         # ring that the step's last kernel writes (impala_set_metrics_host)
-        m = torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device)
+        cur = torch.cuda.current_stream(e.device) if e.device.type == "cuda" else None
+        m, self._next_m = self._next_m, None
+        if m is None or m[1] != cur:  # (made on another stream: not reused across streams)
+            m = (torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device), cur)
+        m = m[0]
         row = self._host_row()
         e._bind_metrics(m, row)
         if len(batch) == 1 and isinstance(batch[0], RowSample):
@@ -331,7 +339,8 @@ class ImpalaLearner(Learner):
                 if self._ring is None or self._ring[0] is not rs.replay:  # checked once per replay
                     self._ring = (rs.replay,) + e.ring_batch(rs.replay.fields)
                 _, rb_, cap = self._ring
-                rs.replay.read_rows(rs, lambda fields, idx, st: e._train_step_rows(rb_, cap, idx, st))
+                rs.replay.read_rows(rs, lambda fields, idx, st: e._train_step_rows(rb_, cap, idx, st),
+                                    cur)
             except _lib.Unsupported:  # not on the default kernels: gather, for good
                 self._rows_ok = False
                 e.train_step(*rs.gather())
