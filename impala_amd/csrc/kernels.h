@@ -816,6 +816,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 // builder.py:43-44), then re-emission of the kernel-layout weights.  Every block re-sums
 // the sum-of-squares partials itself (deterministic, no grid barrier).
 // =========================================================================================
+// impala_set_metrics_host: the word of the 16-float host row the Adam kernel sets last
+constexpr int kMetricsHostFlag = 15;
 struct AdamArgs {
   float *params, *grads, *m, *v, *metrics;
   float* metrics_host;  // (or null) page-locked host copy of the step's metrics vector
@@ -909,14 +911,21 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     a.metrics[6] = norm;
     a.metrics[7] = (float)step;
   }
-  if (a.metrics_host && blockIdx.x == 0 && threadIdx.x < IMPALA_NUM_METRICS) {
+  if (a.metrics_host && blockIdx.x == 0 && threadIdx.x == 0) {
     // the whole vector (slots other than 6 and 7 were final when the reduction kernel ended) to
-    // host memory, with system-scope stores; the caller reads it once an event recorded after
-    // this kernel has completed (no device-to-host copy on the stream)
-    const int i = (int)threadIdx.x;
-    const float x = i == 6 ? norm : i == 7 ? (float)step : a.metrics[i];
-    __hip_atomic_store(reinterpret_cast<unsigned*>(a.metrics_host) + i, __float_as_uint(x),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // host memory with system-scope stores, then a nonzero word at [15] after a system fence:
+    // the caller (which zeroed that word before enqueueing the step) may read the vector as soon
+    // as it sees the word -- before this kernel's other workgroups have finished -- or after an
+    // event recorded behind the step (no device-to-host copy on the stream either way)
+    unsigned* out = reinterpret_cast<unsigned*>(a.metrics_host);
+    float x[IMPALA_NUM_METRICS];  // every load issued before the first store
+#pragma unroll
+    for (int i = 0; i < IMPALA_NUM_METRICS; ++i) x[i] = i == 6 ? norm : i == 7 ? (float)step : a.metrics[i];
+#pragma unroll
+    for (int i = 0; i < IMPALA_NUM_METRICS; ++i)
+      __hip_atomic_store(out + i, __float_as_uint(x[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(out + kMetricsHostFlag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (n == 0) return;  // (never an FC block: those are full)
   const float gscale = a.inv_world * coef;

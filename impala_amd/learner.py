@@ -13,6 +13,7 @@ import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from impala_amd import _lib
@@ -70,18 +71,28 @@ HOST_METRICS_RING = 1024
 @dataclass
 class HostMetrics:
     """Where a step's metrics vector also lands in host memory (impala_set_metrics_host): the
-    ring row, the event recorded after the step, the learner and the step's index."""
-    row: torch.Tensor
+    ring row (a numpy view of 16 floats; word 15 is the ready word the step's Adam kernel sets),
+    the event recorded after the step, the learner and the step's index."""
+    row: "np.ndarray"
     event: "torch.cuda.Event"
     learner: "ImpalaLearner"
     index: int
 
     def values(self):
-        """-> the row's NUM_METRICS floats once the step has completed, or None when the row
-        has been handed to a later step since (the caller then reads the device vector)."""
+        """-> the row's NUM_METRICS floats once the step's Adam kernel has stored them (its
+        ready word; a short spin, then the event), or None when the row has been handed to a
+        later step since, or was never written (the caller then reads the device vector)."""
         if self.learner._step_count - self.index > HOST_METRICS_RING - 1:
             return None
-        self.event.synchronize()
+        ready = self.row.view(np.uint32)
+        if ready[15] == 0:
+            t_end = time.perf_counter() + 2e-3
+            while ready[15] == 0 and time.perf_counter() < t_end:
+                pass
+            if ready[15] == 0:
+                self.event.synchronize()
+                if ready[15] == 0:
+                    return None
         return self.row[:_lib.NUM_METRICS].tolist()
 
 
@@ -316,10 +327,14 @@ class ImpalaLearner(Learner):
             if self._engine.device.type != "cuda":
                 self._mhost = False
             else:
-                self._mhost = torch.zeros(HOST_METRICS_RING, 16, dtype=torch.float32, pin_memory=True)
+                t = torch.zeros(HOST_METRICS_RING, 16, dtype=torch.float32, pin_memory=True)
+                self._mhost = (t, t.numpy(), [r for r in t])  # (numpy view and rows share t)
         if self._mhost is False:
             return None
-        return self._mhost[self._step_count % HOST_METRICS_RING]
+        i = self._step_count % HOST_METRICS_RING
+        t, tn, rows = self._mhost
+        tn[i].view(np.uint32)[15] = 0  # the ready word, set again by this step's Adam kernel
+        return rows[i], tn[i]
 
     def _train_step(self, batch) -> Dict[str, torch.Tensor]:  # learning.py:140-177
         e = self._engine
@@ -331,8 +346,8 @@ class ImpalaLearner(Learner):
         if m is None or m[1] != cur:  # (made on another stream: not reused across streams)
             m = (torch.empty(_lib.NUM_METRICS, dtype=torch.float32, device=e.device), cur)
         m = m[0]
-        row = self._host_row()
-        e._bind_metrics(m, row)
+        hr = self._host_row()
+        e._bind_metrics(m, None if hr is None else hr[0])
         if len(batch) == 1 and isinstance(batch[0], RowSample):
             rs = batch[0]
             try:
@@ -363,10 +378,10 @@ class ImpalaLearner(Learner):
         # DistributedAgent reads the host row once the event after the step has completed
         # (agent._read_values), or moves all of a step's values with one copy
         out = StepMetrics(zip(_lib.METRIC_NAMES, m.unbind(0)))
-        if row is not None:
+        if hr is not None:
             ev = torch.cuda.Event()
             ev.record()
-            out.host = HostMetrics(row, ev, self, self._step_count)
+            out.host = HostMetrics(hr[1], ev, self, self._step_count)
         return out
 
     # ---------------------------------------------------------------- checkpoint

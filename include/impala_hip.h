@@ -144,11 +144,13 @@ int impala_bind_state(impala_learner* h, float* params, float* grads, float* exp
  * fresh vector -- the values it returns (agents/impala/learning.py:161-174) -- instead of
  * copying the bound one after the step (a device copy of 36 bytes costs ~5 us of the stream). */
 int impala_set_metrics(impala_learner* h, float* metrics);
-/* Also write each following step's metrics vector to `host` (IMPALA_NUM_METRICS floats of
- * page-locked host memory, e.g. hipHostMalloc / torch pin_memory; NULL stops it): the step's
- * last kernel stores them there, so a caller that records an event after the step reads
- * `float(v)` of every metric (agents/distributed_agent.py:29-31) from host memory once the event
- * has completed, with no device-to-host copy enqueued.  Not with the A/B fused update. */
+/* Also write each following step's metrics vector to `host` (16 floats of page-locked host
+ * memory, e.g. hipHostMalloc / torch pin_memory; NULL stops it): the step's last kernel stores
+ * the IMPALA_NUM_METRICS values there, then sets the 32-bit word host[15] to 1 after a system
+ * fence.  A caller that zeroes host[15] before enqueueing the step reads `float(v)` of every
+ * metric (agents/distributed_agent.py:29-31) from host memory as soon as it sees the word (or
+ * after an event recorded behind the step), with no device-to-host copy enqueued.  Not with the
+ * A/B fused update. */
 int impala_set_metrics_host(impala_learner* h, float* host);
 /* Re-derive the kernel-layout weights after the caller changed `params` (load_state_dict). */
 int impala_refresh_weights(impala_learner* h, void* stream);

@@ -661,6 +661,8 @@ def test_host_metrics_rows_match_device_vectors(monkeypatch):
     for i, met in enumerate(mets):
         assert met.host is not None and met.host.index == i
         vals = met.host.values()
+        if vals is not None:
+            assert met.host.row.view(np.uint32)[15] == 1  # the ready word
         dev_vals = met["train/loss"]._base.cpu().tolist()
         if i >= n - 3:
             assert vals == dev_vals[:_lib.NUM_METRICS], i
