@@ -321,8 +321,8 @@ class ImpalaLearner(Learner):
         return metrics
 
     def _host_row(self):
-        """This step's row of the page-locked metrics ring (impala_set_metrics_host), or None
-        off the GPU."""
+        """This step's row of the page-locked metrics ring (impala_set_metrics_host) as (tensor,
+        numpy view) with its ready word cleared, or None off the GPU."""
         if self._mhost is None:
             if self._engine.device.type != "cuda":
                 self._mhost = False
