@@ -61,8 +61,9 @@ def _host_floats(pending: List[Dict]) -> List[Dict[str, float]]:
 def _read_values(pending: List[Dict]):
     """The synchronising half of _host_floats: the one device-to-host copy -> (pending, host
     rows by base id); _to_dicts builds the float dicts from them later.  Metrics dicts that
-    carry their step's host row (ImpalaLearner's StepMetrics) are read from it once the step's
-    event has completed, with no copy enqueued behind the work queued since."""
+    carry their step's host row (ImpalaLearner's StepMetrics) are read from it as soon as the
+    step's Adam kernel has set the row's ready word (HostMetrics.values), with no copy enqueued
+    behind the work queued since."""
     host = {}
     rest = []
     for m in pending:

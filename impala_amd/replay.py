@@ -236,9 +236,9 @@ class DeviceReplayBuffer(ReplayBuffer):
 
     def read_rows(self, rs: "RowSample", enqueue, stream=None):
         """Run ``enqueue(fields, idx, stream)`` -- which enqueues work reading the ring slots
-        ``rs.idx`` on ``stream`` (the current stream when None) -- under the lock that ``append`` takes,
-        after that stream waits for every staged append, then mark the slots as read by it (the
-        fence an append into them waits for, as for a gather in ``sample``)."""
+        ``rs.idx`` on ``stream`` (the current stream when None) -- under the lock ``append``
+        takes, after that stream waits for every staged append; then mark the slots as read by
+        it (the fence an append into them waits for, as for a gather in ``sample``)."""
         cur = torch.cuda.current_stream(self.device) if stream is None else stream
         with self._cv:
             if self._pending:
