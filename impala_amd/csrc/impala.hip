@@ -928,8 +928,13 @@ int impala_create(const impala_config* cfg, int device, impala_learner** out) {
   h->fc_direct = false;
   if (const char* e = std::getenv("IMPALA_FC_DIRECT")) h->fc_direct = N <= 8192 && e[0] == '1';
   h->n_fc_wg = (FLAT / FCD_BC) * (HID / FCD_BR);
-  h->sp3 = plan_split((long)N * P3, K3 / 64, 256);
-  h->sp2 = plan_split((long)N * P2, K2 / 128, 256);
+  // the conv weight gradients' m splits: ~256 workgroups each (IMPALA_WG3_TARGET /
+  // IMPALA_WG2_TARGET override the count for A/B runs; more splits, more slab bytes to reduce)
+  int wg3 = 256, wg2 = 256;
+  if (const char* e = std::getenv("IMPALA_WG3_TARGET")) wg3 = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("IMPALA_WG2_TARGET")) wg2 = std::max(1, std::atoi(e));
+  h->sp3 = plan_split((long)N * P3, K3 / 64, wg3);
+  h->sp2 = plan_split((long)N * P2, K2 / 128, wg2);
   h->c1_fpw = std::max(1, cdiv(N, h->n_cu));
   if (const char* e = std::getenv("IMPALA_C1_FPW")) h->c1_fpw = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("IMPALA_C12F_FPW")) h->c12f_fpw = std::max(0, std::atoi(e));
