@@ -72,16 +72,17 @@ HOST_METRICS_RING = 1024
 class HostMetrics:
     """Where a step's metrics vector also lands in host memory (impala_set_metrics_host): the
     ring row (a numpy view of 16 floats; word 15 is the ready word the step's Adam kernel sets),
-    the event recorded after the step, the learner and the step's index."""
+    the stream the step ran on, the learner and the step's index."""
     row: "np.ndarray"
-    event: "torch.cuda.Event"
+    stream: "torch.cuda.Stream"
     learner: "ImpalaLearner"
     index: int
 
     def values(self):
         """-> the row's NUM_METRICS floats once the step's Adam kernel has stored them (its
-        ready word; a short spin, then the event), or None when the row has been handed to a
-        later step since, or was never written (the caller then reads the device vector)."""
+        ready word; a short spin, then a stream synchronize), or None when the row has been
+        handed to a later step since, or was never written (the caller then reads the device
+        vector)."""
         if self.learner._step_count - self.index > HOST_METRICS_RING - 1:
             return None
         ready = self.row.view(np.uint32)
@@ -90,7 +91,7 @@ class HostMetrics:
             while ready[15] == 0 and time.perf_counter() < t_end:
                 pass
             if ready[15] == 0:
-                self.event.synchronize()
+                self.stream.synchronize()
                 if ready[15] == 0:
                     return None
         return self.row[:_lib.NUM_METRICS].tolist()
@@ -375,13 +376,11 @@ class ImpalaLearner(Learner):
                 compute_grads_allreduced(e, batch, self._model.flat_grad, group=self._pg)
                 e.apply_update()
         # device scalars, views of the step's metrics vector: float(v) synchronises lazily;
-        # DistributedAgent reads the host row once the event after the step has completed
+        # DistributedAgent reads the host row once the step's Adam kernel has set its ready word
         # (agent._read_values), or moves all of a step's values with one copy
         out = StepMetrics(zip(_lib.METRIC_NAMES, m.unbind(0)))
-        if hr is not None:
-            ev = torch.cuda.Event()
-            ev.record()
-            out.host = HostMetrics(hr[1], ev, self, self._step_count)
+        if hr is not None:  # (no event per step: its marker left a 6 us gap, profiles/r06lt)
+            out.host = HostMetrics(hr[1], cur, self, self._step_count)
         return out
 
     # ---------------------------------------------------------------- checkpoint
