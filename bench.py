@@ -586,11 +586,13 @@ SAC_PROFILE_NAMES = {"actor_chain": "actor_chain", "critic_loss_chain": "critic_
 def profiled_kernel(kernel, dtype, names=None, algo="impala"):
     """The newest committed rocprofv3 summary record of `kernel` for the same algorithm and
     dtype (profiles/<tag>/summary.json, "algo" defaulting to impala) that carries PMC HBM bytes
-    -> (record, tag), or (None, None).  Tags sort by round and letter (r05r6 < r06a)."""
+    -> (record, tag), or (None, None).  Newest = the latest "created" stamp
+    (tools/summarize_profile.py); summaries without one are older, ordered by tag (r05r6 <
+    r06a)."""
     root = os.path.join(HERE, "profiles")
     if not os.path.isdir(root):
         return None, None
-    best = None
+    found = []
     for tag in sorted(os.listdir(root)):
         p = os.path.join(root, tag, "summary.json")
         if not os.path.exists(p):
@@ -603,8 +605,11 @@ def profiled_kernel(kernel, dtype, names=None, algo="impala"):
             continue
         for k in js.get("kernels", []):
             if k.get("kernel") == (names or PROFILE_NAMES).get(kernel) and k.get("hbm_bytes"):
-                best = (k, tag)
-    return best if best else (None, None)
+                found.append((str(js.get("created", "")), tag, k))
+    if not found:
+        return None, None
+    _, tag, k = max(found, key=lambda f: (f[0], f[1]))
+    return k, tag
 
 
 def profiled_traffic(kernel, dtype, names=None, algo="impala"):

@@ -109,7 +109,10 @@ def main(tag, src_root="gpurun_out", dst_root="profiles"):
                                         "sac" if "SAC" in line.get("metric", "") else "impala")
         except Exception:
             pass
-    json.dump({"tag": tag, "algo": algo, "dtype": dtype, "total_kernel_ns": total_ns, "kernels": out},
+    import datetime
+    created = datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+    json.dump({"tag": tag, "algo": algo, "dtype": dtype, "created": created,
+               "total_kernel_ns": total_ns, "kernels": out},
               open(os.path.join(dst, "summary.json"), "w"), indent=1)
     with open(os.path.join(dst, "summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary `{tag}`\n\n`tools/profile.sh {tag}` = `rocprofv3 --kernel-trace --stats` "
