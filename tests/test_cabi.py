@@ -86,3 +86,21 @@ def test_kernel_entry_points_validate_before_launch():
     # device step clock: a null handle is refused before any HIP call
     assert lib.impala_step_clock(None, None, 3) == 1001
     assert lib.impala_step_clock_end(None, None, None) == 1001
+
+
+def test_headers_compile_as_c99(tmp_path):
+    """include/*.h are the boundary a C (or cgo / FFI) binding includes: they must be plain C99,
+    with no C++ in the declarations."""
+    import os
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    src = tmp_path / "hdr.c"
+    src.write_text('#include "impala_hip.h"\n#include "sac_hip.h"\n'
+                   "int main(void) { return IMPALA_NUM_METRICS == 9 ? 0 : 1; }\n")
+    r = subprocess.run([cc, "-std=c99", "-Wall", "-Werror", "-I", inc, "-c", str(src), "-o",
+                        str(tmp_path / "hdr.o")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
