@@ -569,6 +569,38 @@ def run_learner_loop(args, dev, headline_ms):
     return out
 
 
+def run_actor_act(args, dev, batch=128, calls=200):
+    """actor-side batched inference, ``AtariPPOModel.act``
+    (models/distributed_models.py:21-32: forward, argmax where deterministic, else a draw from
+    softmax(logits); action, logits and value back on the host) on ``batch`` frames per call --
+    the reference's inference batch (conf/config.yaml:28, <= 128) -- with the observations
+    coming from host memory (the actors' page-locked buffers) and, for the kernel side alone,
+    already in HBM.  Wall ms per call (host-synced by the .cpu() results), median of ``calls``."""
+    from impala_amd.model import AtariPPOModel
+    m = AtariPPOModel((3, 64, 64), args.actions, device=dev, dtype=args.dtype, seed=0)
+    g = torch.Generator().manual_seed(77)
+    obs_host = torch.randint(0, 256, (batch, 3, 64, 64), dtype=torch.uint8, generator=g).pin_memory()
+    obs_dev = obs_host.to(dev)
+    det = torch.zeros(batch, dtype=torch.bool)
+    det[::4] = True  # a quarter of the actors in evaluation mode (per-frame argmax)
+    out = {"batch": batch, "calls": calls, "dtype": args.dtype,
+           "note": "wall ms per AtariPPOModel.act call (forward + argmax / softmax draw in one "
+                   "HIP launch chain, impala_act), results copied to the host; median over calls"}
+    for name, obs in (("host_obs", obs_host), ("device_obs", obs_dev)):
+        for _ in range(20):
+            m.act(obs, det)
+        times = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            m.act(obs, det)
+            times.append(time.perf_counter() - t0)
+        med = float(np.median(times))
+        out[name] = {"ms_per_call_median": round(med * 1e3, 4),
+                     "ms_per_call_p90": round(float(np.percentile(times, 90)) * 1e3, 4),
+                     "frames_per_s": round(batch / med, 1)}
+    return out
+
+
 PROFILE_NAMES = {"conv1_fwd": "Conv1Fwd", "conv1_fwd_conv2_fwd": "Conv12Fwd", "conv2_fwd": "Conv2Fwd", "conv3_fwd": "Conv3LnFwd",
                  "fc_fwd": "FcFwd", "heads_fwd": "HeadsFwd", "head_step": "head_step",
                  "fc_dgrad": "FcDgrad", "ln_bwd": "ln_bwd", "conv3_dgrad": "Conv3Dgrad",
@@ -860,6 +892,8 @@ def main():
                          "-> replay, N=1 IMPALA only)")
     ap.add_argument("--loop-steps", type=int, default=100,
                     help="train_steps per learner_loop record")
+    ap.add_argument("--no-actor-act", action="store_true",
+                    help="skip the actor inference sub-record (AtariPPOModel.act, N=1 IMPALA only)")
     ap.add_argument("--loop-warmup", type=int, default=None,
                     help="untimed train_steps before each learner_loop record (default: "
                          "max(--warmup, 5))")
@@ -1012,6 +1046,8 @@ def main():
     # engine's ring (profiles/r06w).  The copy streams are now one set per device (r06x)
     if world == 1 and dist is None and not ppo and not args.no_learner_loop:
         out["learner_loop"] = run_learner_loop(args, dev, round(ms_step, 4))
+    if world == 1 and dist is None and not ppo and not args.no_actor_act:
+        out["actor_act"] = run_actor_act(args, dev)
     if not args.no_host_staged:
         out["host_staged"] = run_host_staged(eng, batch, args, dist, model, world)
         if "learner_loop" in out and "host_list_replay" in out["learner_loop"]:
